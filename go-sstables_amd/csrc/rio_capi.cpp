@@ -1,0 +1,719 @@
+// rio_capi.cpp — host runtime and C-ABI of librio (include/rio.h).
+//
+// Owns HIP contexts (device, stream, grow-only device arenas, pinned staging) and the reader
+// handles that mirror recordio.ReaderI / recordio.ReadAtI:
+//   FileReader  Open/ReadNext/SkipNext/Close   recordio/file_reader.go:26-172, 272-279
+//   MMapReader  Open/ReadNextAt/SeekNext/Size  recordio/mmap_reader.go:25-203, 358-371
+// Every decode runs on the device (rio_kernels.hip); host code only moves bytes, parses the
+// 8-byte file header at Open (readFileHeaderFromBuffer, common_reader.go:22-44) and iterates the
+// decoded arena. There is no CPU decode fallback: a missing GPU is an error.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rio.h"
+#include "rio_device.h"
+
+namespace rio {
+hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t* out, uint64_t out_cap,
+                          ReadAtResult* res, hipStream_t s);
+hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
+                            uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off, hipStream_t s);
+}  // namespace rio
+
+using namespace rio;
+
+// ------------------------------------------------------------------------------------------
+// status helpers
+// ------------------------------------------------------------------------------------------
+extern "C" const char* rio_strerror(int s) {
+    switch (s) {
+    case RIO_OK: return "ok";
+    case RIO_EOF: return "EOF";
+    case RIO_EOF_ZERO_TAIL: return "EOF (zero-padded tail)";
+    case RIO_EOF_HEADER: return "EOF inside record header";
+    case RIO_EOF_PAYLOAD: return "EOF reading record payload";
+    case RIO_ERR_UNEXPECTED_EOF: return "unexpected EOF";
+    case RIO_ERR_MAGIC: return "magic number mismatch";
+    case RIO_ERR_HEADER_CRC: return "header checksum mismatch";
+    case RIO_ERR_VARINT_OVERFLOW: return "binary: varint overflows a 64-bit integer";
+    case RIO_ERR_HEADER_TOO_LONG: return "checksum byte reader out of range";
+    case RIO_ERR_DECOMPRESS: return "snappy: corrupt input";
+    case RIO_ERR_VERSION: return "version mismatch";
+    case RIO_ERR_COMPRESSION_TYPE: return "unknown compression type";
+    case RIO_ERR_SHORT_FILE_HEADER: return "not enough bytes in the file header";
+    case RIO_ERR_INVALID_OFFSET: return "mmap: invalid ReadAt offset";
+    case RIO_ERR_UNSUPPORTED: return "not supported by the GPU decode path";
+    case RIO_ERR_CAPACITY: return "output capacity too small";
+    case RIO_ERR_ARG: return "invalid argument";
+    case RIO_ERR_HIP: return "HIP runtime error";
+    case RIO_ERR_STATE: return "reader state error";
+    case RIO_ERR_IO: return "I/O error";
+    default: return "unknown status";
+    }
+}
+
+extern "C" int rio_status_is_eof(int s) {
+    return s == RIO_EOF || s == RIO_EOF_ZERO_TAIL || s == RIO_EOF_HEADER || s == RIO_EOF_PAYLOAD;
+}
+
+extern "C" const char* rio_build_info(void) { return "librio gfx950 recordio v3/v4 decode"; }
+
+extern "C" uint64_t rio_max_records(uint64_t len) {
+    return len <= RIO_FILE_HEADER_BYTES ? 1 : (len - RIO_FILE_HEADER_BYTES) / 6 + 1;
+}
+
+#define HIP_TRY(x)                                  \
+    do {                                            \
+        hipError_t e_ = (x);                        \
+        if (e_ != hipSuccess) return RIO_ERR_HIP;   \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// context
+// ------------------------------------------------------------------------------------------
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+    const char* v = getenv(name);
+    if (!v || !*v) return dflt;
+    return strtoull(v, nullptr, 0);
+}
+
+constexpr size_t kStage = 32ull << 20;  // pinned staging piece
+
+}  // namespace
+
+struct rio_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // timing ring: slot i holds the 5 stage events of the i-th decode since rio_ctx_set_timing
+    std::vector<std::array<hipEvent_t, 5>> ev;
+    uint64_t ev_cursor = 0;
+    uint64_t chunk_bytes = 4096;
+    hipEvent_t* next_events() {
+        if (ev.empty()) return nullptr;
+        return ev[ev_cursor++ % ev.size()].data();
+    }
+    hipEvent_t* same_events() {  // phase B of the call whose phase A took the last slot
+        if (ev.empty() || ev_cursor == 0) return nullptr;
+        return ev[(ev_cursor - 1) % ev.size()].data();
+    }
+    void set_ring(size_t n) {
+        for (auto& s : ev)
+            for (auto& e : s) hipEventDestroy(e);
+        ev.assign(n, {});
+        for (auto& s : ev)
+            for (auto& e : s) hipEventCreate(&e);
+        ev_cursor = 0;
+    }
+    // framing arenas
+    DevBuf scratch_off, scratch_len, chunks, block_runs, chunk_excl, place, block_excl, state, info;
+    // host-API arenas
+    DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
+    uint8_t* pinned[2] = {nullptr, nullptr};
+    hipEvent_t pin_ev[2] = {};
+    // last host-API framing (rio_frame -> rio_decode)
+    FrameParams last{};
+    bool framed = false;
+    uint64_t file_len = 0;
+    rio_file_info frame_info{};
+};
+
+static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P) {
+    memset(&P, 0, sizeof P);
+    P.file = d_file;
+    P.len = len;
+    P.chunk_bytes = ctx->chunk_bytes;
+    P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + ctx->chunk_bytes - 1) / ctx->chunk_bytes : 0;
+    P.slots = ctx->chunk_bytes / 6 + 1;
+    P.n_blocks = (P.n_chunks + 255) / 256;
+    const uint64_t nc = std::max<uint64_t>(P.n_chunks, 1), nb = std::max<uint64_t>(P.n_blocks, 1);
+    HIP_TRY(ctx->scratch_off.ensure(nc * P.slots * 8));
+    HIP_TRY(ctx->scratch_len.ensure(nc * P.slots * 8));
+    HIP_TRY(ctx->chunks.ensure(nc * sizeof(ChunkSum)));
+    HIP_TRY(ctx->chunk_excl.ensure(nc * sizeof(RunSum)));
+    HIP_TRY(ctx->place.ensure(nc * sizeof(ChunkPlace)));
+    HIP_TRY(ctx->block_runs.ensure(nb * sizeof(RunSum)));
+    HIP_TRY(ctx->block_excl.ensure(nb * sizeof(RunSum)));
+    HIP_TRY(ctx->state.ensure(sizeof(ScanState)));
+    HIP_TRY(ctx->info.ensure(sizeof(rio_file_info)));
+    P.scratch_off = ctx->scratch_off.as<uint64_t>();
+    P.scratch_len = ctx->scratch_len.as<uint64_t>();
+    P.chunks = ctx->chunks.as<ChunkSum>();
+    P.chunk_excl = ctx->chunk_excl.as<RunSum>();
+    P.place = ctx->place.as<ChunkPlace>();
+    P.block_runs = ctx->block_runs.as<RunSum>();
+    P.block_excl = ctx->block_excl.as<RunSum>();
+    P.state = ctx->state.as<ScanState>();
+    P.info = ctx->info.as<rio_file_info>();
+    return RIO_OK;
+}
+
+extern "C" int rio_device_count(int* out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    if (out) *out = n;
+    return n > 0 ? RIO_OK : RIO_ERR_HIP;
+}
+
+extern "C" int rio_ctx_create(int device, rio_ctx** out) {
+    if (!out) return RIO_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RIO_ERR_HIP;
+    if (device < 0 || device >= n) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(device));
+    auto* c = new rio_ctx();
+    c->device = device;
+    c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 4096);
+    if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 4096;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return RIO_ERR_HIP;
+    }
+    c->set_ring(1);
+    *out = c;
+    return RIO_OK;
+}
+
+extern "C" void rio_ctx_destroy(rio_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
+                      &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
+                      &c->readat_out, &c->readat_res, &c->seek_off})
+        b->release();
+    for (int i = 0; i < 2; i++) {
+        if (c->pinned[i]) hipHostFree(c->pinned[i]);
+        if (c->pin_ev[i]) hipEventDestroy(c->pin_ev[i]);
+    }
+    c->set_ring(0);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// slots == 0 disables stage events; slots == n keeps the events of the last n decodes
+extern "C" int rio_ctx_set_timing(rio_ctx* c, int slots) {
+    if (!c || slots < 0) return RIO_ERR_ARG;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    c->set_ring((size_t)slots);
+    return RIO_OK;
+}
+
+// Mean per-stage device milliseconds over the decodes recorded in the ring:
+// [0] header + walk, [1] scan + zero-tail check, [2] placement, [3] decode kernels.
+extern "C" int rio_ctx_last_stage_ms(rio_ctx* c, float* ms, int n) {
+    if (!c || !ms || c->ev.empty() || c->ev_cursor == 0) return 0;
+    const uint64_t used = std::min<uint64_t>(c->ev_cursor, c->ev.size());
+    double acc[4] = {0, 0, 0, 0};
+    for (uint64_t s = 0; s < used; s++) {
+        auto& e = c->ev[s];
+        hipEventSynchronize(e[4]);
+        for (int k = 0; k < 4; k++) {
+            float v = 0;
+            hipEventElapsedTime(&v, e[k], e[k + 1]);
+            acc[k] += v;
+        }
+    }
+    int k = std::min(n, 4);
+    for (int i = 0; i < k; i++) ms[i] = (float)(acc[i] / (double)used);
+    return k;
+}
+
+// ------------------------------------------------------------------------------------------
+// device-resident single call
+// ------------------------------------------------------------------------------------------
+extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
+                                 uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
+                                 uint64_t rec_cap, rio_file_info* d_info, void* stream) {
+    if (!ctx || !d_file || !d_out_off || !d_rec_off || !d_flags || !d_info) return RIO_ERR_ARG;
+    if ((reinterpret_cast<uintptr_t>(d_file) & 15) != 0) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    FrameParams P;
+    int rc = ctx_frame_params(ctx, d_file, len, P);
+    if (rc) return rc;
+    P.out = d_out;
+    P.out_cap = out_cap;
+    P.out_off = d_out_off;
+    P.rec_off = d_rec_off;
+    P.flags = d_flags;
+    P.rec_cap = rec_cap;
+    P.info = d_info;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipEvent_t* ev = ctx->next_events();
+    HIP_TRY(launch_phase_a(P, s, ev));
+    HIP_TRY(launch_phase_b(P, s, ev));
+    return RIO_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// host two-phase API (cgo)
+// ------------------------------------------------------------------------------------------
+static int ensure_pinned(rio_ctx* c) {
+    for (int i = 0; i < 2; i++) {
+        if (!c->pinned[i]) {
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pinned[i]), kStage, hipHostMallocDefault));
+            HIP_TRY(hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
+        }
+    }
+    return RIO_OK;
+}
+
+// pageable host -> device through two pinned staging pieces (copy of piece k+1 overlaps the DMA
+// of piece k)
+static int h2d_staged(rio_ctx* c, void* dst, const uint8_t* src, uint64_t n) {
+    int rc = ensure_pinned(c);
+    if (rc) return rc;
+    uint64_t o = 0;
+    int k = 0;
+    while (o < n) {
+        const uint64_t m = std::min<uint64_t>(kStage, n - o);
+        HIP_TRY(hipEventSynchronize(c->pin_ev[k]));
+        memcpy(c->pinned[k], src + o, m);
+        HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, c->pinned[k], m, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(c->pin_ev[k], c->stream));
+        o += m;
+        k ^= 1;
+    }
+    return RIO_OK;
+}
+
+// device -> pageable host through pinned staging
+static int d2h_staged(rio_ctx* c, uint8_t* dst, const void* src, uint64_t n) {
+    int rc = ensure_pinned(c);
+    if (rc) return rc;
+    uint64_t o = 0, prev_o = 0, prev_m = 0;
+    int k = 0;
+    bool have_prev = false;
+    while (o < n) {
+        const uint64_t m = std::min<uint64_t>(kStage, n - o);
+        HIP_TRY(hipEventSynchronize(c->pin_ev[k]));
+        HIP_TRY(hipMemcpyAsync(c->pinned[k], static_cast<const uint8_t*>(src) + o, m, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipEventRecord(c->pin_ev[k], c->stream));
+        if (have_prev) {
+            HIP_TRY(hipEventSynchronize(c->pin_ev[k ^ 1]));
+            memcpy(dst + prev_o, c->pinned[k ^ 1], prev_m);
+        }
+        have_prev = true;
+        prev_o = o;
+        prev_m = m;
+        o += m;
+        k ^= 1;
+    }
+    if (have_prev) {
+        HIP_TRY(hipEventSynchronize(c->pin_ev[k ^ 1]));
+        memcpy(dst + prev_o, c->pinned[k ^ 1], prev_m);
+    }
+    return RIO_OK;
+}
+
+extern "C" int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_file_info* info) {
+    if (!ctx || (!file && len) || !info) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    ctx->framed = false;
+    HIP_TRY(ctx->file.ensure(len + RIO_DEVICE_PAD));
+    int rc = h2d_staged(ctx, ctx->file.p, file, len);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->file.as<uint8_t>() + len, 0, RIO_DEVICE_PAD, ctx->stream));
+    FrameParams P;
+    rc = ctx_frame_params(ctx, ctx->file.as<uint8_t>(), len, P);
+    if (rc) return rc;
+    HIP_TRY(launch_phase_a(P, ctx->stream, ctx->next_events()));
+    HIP_TRY(hipMemcpyAsync(&ctx->frame_info, P.info, sizeof(rio_file_info), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *info = ctx->frame_info;
+    ctx->last = P;
+    ctx->framed = true;
+    ctx->file_len = len;
+    return RIO_OK;
+}
+
+extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, uint64_t* rec_off,
+                          uint8_t* flags, uint64_t rec_cap, rio_file_info* info) {
+    if (!ctx || !info) return RIO_ERR_ARG;
+    if (!ctx->framed) return RIO_ERR_STATE;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const rio_file_info fi = ctx->frame_info;
+    if (fi.status == RIO_ERR_VERSION || fi.status == RIO_ERR_COMPRESSION_TYPE || fi.status == RIO_ERR_UNSUPPORTED ||
+        fi.status == RIO_ERR_SHORT_FILE_HEADER) {
+        *info = fi;
+        return RIO_OK;
+    }
+    const uint64_t n = fi.n_records, nb = fi.total_out_bytes;
+    if (rec_cap < n || out_cap < nb || (n && (!out_off || !rec_off || !flags)) || (nb && !out)) return RIO_ERR_CAPACITY;
+    HIP_TRY(ctx->out.ensure(nb + 16));
+    HIP_TRY(ctx->out_off.ensure((n + 1) * 8));
+    HIP_TRY(ctx->rec_off.ensure(n * 8 + 8));
+    HIP_TRY(ctx->flags.ensure(n + 8));
+    FrameParams P = ctx->last;
+    P.out = ctx->out.as<uint8_t>();
+    P.out_cap = nb;
+    P.out_off = ctx->out_off.as<uint64_t>();
+    P.rec_off = ctx->rec_off.as<uint64_t>();
+    P.flags = ctx->flags.as<uint8_t>();
+    P.rec_cap = n;
+    HIP_TRY(launch_phase_b(P, ctx->stream, ctx->same_events()));
+    rio_file_info fin{};
+    HIP_TRY(hipMemcpyAsync(&fin, P.info, sizeof fin, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int rc;
+    if (fin.total_out_bytes && (rc = d2h_staged(ctx, out, P.out, fin.total_out_bytes))) return rc;
+    if (out_off && (rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(out_off), P.out_off, (fin.n_records + 1) * 8))) return rc;
+    if (fin.n_records) {
+        if ((rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(rec_off), P.rec_off, fin.n_records * 8))) return rc;
+        if ((rc = d2h_staged(ctx, flags, P.flags, fin.n_records))) return rc;
+    }
+    *info = fin;
+    return RIO_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// single-record decode (ReadNextAt) / seek (SeekNext) on a device-resident file
+// ------------------------------------------------------------------------------------------
+static int read_at_impl(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint64_t offset, bool seek,
+                        uint64_t seek_len, ReadAtResult* res, uint64_t* rec_offset) {
+    HIP_TRY(ctx->readat_res.ensure(sizeof(ReadAtResult)));
+    HIP_TRY(ctx->seek_off.ensure(8));
+    if (ctx->readat_out.cap == 0) HIP_TRY(ctx->readat_out.ensure(1 << 20));
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if (seek)
+            HIP_TRY(launch_seek_next(d_file, len, offset, seek_len, ctx->readat_out.as<uint8_t>(), ctx->readat_out.cap,
+                                     ctx->readat_res.as<ReadAtResult>(), ctx->seek_off.as<uint64_t>(), ctx->stream));
+        else
+            HIP_TRY(launch_read_at(d_file, len, offset, ctx->readat_out.as<uint8_t>(), ctx->readat_out.cap,
+                                   ctx->readat_res.as<ReadAtResult>(), ctx->stream));
+        HIP_TRY(hipMemcpyAsync(res, ctx->readat_res.p, sizeof(ReadAtResult), hipMemcpyDeviceToHost, ctx->stream));
+        if (rec_offset) HIP_TRY(hipMemcpyAsync(rec_offset, ctx->seek_off.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (res->status != RIO_ERR_CAPACITY) return RIO_OK;
+        HIP_TRY(ctx->readat_out.ensure(res->len + 16));
+    }
+    return RIO_OK;
+}
+
+extern "C" int rio_device_read_at(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint64_t offset,
+                                  uint8_t* d_out, uint64_t out_cap, uint64_t* len_out, int* nil_out,
+                                  uint64_t* detail0, uint64_t* detail1) {
+    if (!ctx || !d_file) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    ReadAtResult r{};
+    HIP_TRY(ctx->readat_res.ensure(sizeof(ReadAtResult)));
+    HIP_TRY(launch_read_at(d_file, len, offset, d_out, out_cap, ctx->readat_res.as<ReadAtResult>(), ctx->stream));
+    HIP_TRY(hipMemcpyAsync(&r, ctx->readat_res.p, sizeof r, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (len_out) *len_out = r.len;
+    if (nil_out) *nil_out = r.nil;
+    if (detail0) *detail0 = r.det0;
+    if (detail1) *detail1 = r.det1;
+    return r.status;
+}
+
+// ------------------------------------------------------------------------------------------
+// reader handles
+// ------------------------------------------------------------------------------------------
+struct rio_reader {
+    rio_ctx* ctx = nullptr;
+    std::string path;
+    bool mmap_mode = false;
+    bool open = false, closed = false;
+    int fd = -1;
+    const uint8_t* map = nullptr;
+    uint64_t size = 0;
+    uint32_t version = 0, compression = 0;
+    std::mutex mu;
+    // FILE mode: whole-file decode result
+    bool decoded = false;
+    int decode_rc = RIO_OK;
+    rio_file_info info{};
+    std::vector<uint8_t> out;
+    std::vector<uint64_t> out_off, rec_off;
+    std::vector<uint8_t> flags;
+    uint64_t cursor = 0;
+    bool past_end = false;
+    // MMAP mode
+    bool on_device = false;
+    DevBuf dfile;
+    std::vector<uint8_t> rec_buf;
+    uint64_t seek_len = 4096;
+    // last error details
+    uint64_t det0 = 0, det1 = 0, err_off = 0;
+};
+
+static int reader_new(rio_ctx* ctx, const char* path, bool mm, rio_reader** out) {
+    if (!ctx || !path || !out) return RIO_ERR_ARG;
+    *out = nullptr;
+    // NewFileReader / mmap.Open fail on a missing file (file_reader.go:507, mmap_reader.go:366)
+    int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return RIO_ERR_IO;
+    auto* r = new rio_reader();
+    r->ctx = ctx;
+    r->path = path;
+    r->mmap_mode = mm;
+    r->fd = fd;
+    struct stat st;
+    if (fstat(fd, &st) == 0) r->size = (uint64_t)st.st_size;
+    *out = r;
+    return RIO_OK;
+}
+
+extern "C" int rio_reader_new_file(rio_ctx* ctx, const char* path, rio_reader** out) {
+    return reader_new(ctx, path, false, out);
+}
+extern "C" int rio_reader_new_mmap(rio_ctx* ctx, const char* path, rio_reader** out) {
+    return reader_new(ctx, path, true, out);
+}
+
+extern "C" int rio_reader_open(rio_reader* r) {
+    if (!r) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (r->open) return RIO_ERR_STATE;    // "already opened"
+    if (r->closed) return RIO_ERR_STATE;  // "already closed"
+    struct stat st;
+    if (fstat(r->fd, &st) != 0) return RIO_ERR_IO;
+    r->size = (uint64_t)st.st_size;
+    if (r->size) {
+        void* m = mmap(nullptr, r->size, PROT_READ, MAP_PRIVATE, r->fd, 0);
+        if (m == MAP_FAILED) return RIO_ERR_IO;
+        r->map = static_cast<const uint8_t*>(m);
+    }
+    if (r->size < RIO_FILE_HEADER_BYTES) return RIO_ERR_SHORT_FILE_HEADER;
+    const uint8_t* f = r->map;
+    r->version = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+    r->compression = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+    if (r->version > RIO_VERSION4 || r->version < RIO_VERSION1) {
+        r->det0 = r->version;
+        return RIO_ERR_VERSION;
+    }
+    if (r->compression > RIO_COMP_LZW) {
+        r->det0 = r->compression;
+        return RIO_ERR_COMPRESSION_TYPE;
+    }
+    r->open = true;
+    return RIO_OK;
+}
+
+extern "C" int rio_reader_close(rio_reader* r) {
+    if (!r) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    r->closed = true;
+    r->open = false;
+    if (r->map) munmap(const_cast<uint8_t*>(r->map), r->size);
+    r->map = nullptr;
+    r->dfile.release();
+    r->on_device = false;
+    return RIO_OK;
+}
+
+extern "C" void rio_reader_free(rio_reader* r) {
+    if (!r) return;
+    rio_reader_close(r);
+    if (r->fd >= 0) ::close(r->fd);
+    delete r;
+}
+
+extern "C" int rio_reader_header(rio_reader* r, uint32_t* version, uint32_t* compression) {
+    if (!r) return RIO_ERR_ARG;
+    if (version) *version = r->version;
+    if (compression) *compression = r->compression;
+    return r->open ? RIO_OK : RIO_ERR_STATE;
+}
+
+extern "C" uint64_t rio_reader_size(rio_reader* r) { return r ? r->size : 0; }
+
+extern "C" void rio_reader_last_detail(rio_reader* r, uint64_t* d0, uint64_t* d1, uint64_t* off) {
+    if (!r) return;
+    if (d0) *d0 = r->det0;
+    if (d1) *d1 = r->det1;
+    if (off) *off = r->err_off;
+}
+
+static int file_decode(rio_reader* r) {
+    if (r->decoded) return r->decode_rc;
+    r->decoded = true;
+    rio_file_info fi{};
+    int rc = rio_frame(r->ctx, r->map, r->size, &fi);
+    if (rc) return r->decode_rc = rc;
+    if (fi.status == RIO_ERR_UNSUPPORTED) return r->decode_rc = RIO_ERR_UNSUPPORTED;
+    r->out.resize(fi.total_out_bytes + 1);
+    r->out_off.resize(fi.n_records + 1);
+    r->rec_off.resize(fi.n_records + 1);
+    r->flags.resize(fi.n_records + 1);
+    rc = rio_decode(r->ctx, r->out.data(), fi.total_out_bytes, r->out_off.data(), r->rec_off.data(), r->flags.data(),
+                    fi.n_records, &fi);
+    if (rc) return r->decode_rc = rc;
+    r->info = fi;
+    return r->decode_rc = RIO_OK;
+}
+
+extern "C" int rio_reader_file_info(rio_reader* r, rio_file_info* info) {
+    if (!r || !info) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (!r->open || r->closed || r->mmap_mode) return RIO_ERR_STATE;
+    int rc = file_decode(r);
+    if (rc) return rc;
+    *info = r->info;
+    return RIO_OK;
+}
+
+// terminal status as ReadNext reports it
+static int terminal(rio_reader* r) {
+    r->det0 = r->info.detail0;
+    r->det1 = r->info.detail1;
+    r->err_off = r->info.status_offset;
+    return r->info.status;
+}
+
+extern "C" int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil) {
+    if (!r) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (data) *data = nullptr;
+    if (len) *len = 0;
+    if (is_nil) *is_nil = 0;
+    if (!r->open || r->closed || r->mmap_mode) return RIO_ERR_STATE;
+    int rc = file_decode(r);
+    if (rc) return rc;
+    if (r->past_end) return RIO_EOF;
+    if (r->cursor >= r->info.n_records) return terminal(r);
+    const uint64_t i = r->cursor++;
+    if (data) *data = r->out.data() + r->out_off[i];
+    if (len) *len = r->out_off[i + 1] - r->out_off[i];
+    if (is_nil) *is_nil = (r->flags[i] & RIO_FLAG_NIL) ? 1 : 0;
+    return RIO_OK;
+}
+
+// FileReader.SkipNext (file_reader.go:133-172): header parse + seek, no payload read, no
+// zero-tail check. Divergence (documented): a nil record in a compressed file is skipped by its
+// true extent, not by c bytes (the reference's :151-157 quirk).
+extern "C" int rio_reader_skip_next(rio_reader* r) {
+    if (!r) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (!r->open || r->closed || r->mmap_mode) return RIO_ERR_STATE;
+    int rc = file_decode(r);
+    if (rc) return rc;
+    if (r->past_end) return RIO_EOF;
+    if (r->cursor < r->info.n_records) {
+        r->cursor++;
+        return RIO_OK;
+    }
+    const int s = terminal(r);
+    switch (s) {
+    case RIO_EOF_ZERO_TAIL: return RIO_ERR_MAGIC;  // SkipNext does not test for a zero tail
+    case RIO_EOF_PAYLOAD:
+    case RIO_ERR_UNEXPECTED_EOF:
+    case RIO_ERR_DECOMPRESS:  // header parsed fine: SkipNext seeks past the payload
+        r->past_end = true;
+        return RIO_OK;
+    default: return s;
+    }
+}
+
+static int ensure_on_device(rio_reader* r) {
+    if (r->on_device) return RIO_OK;
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    HIP_TRY(r->dfile.ensure(r->size + RIO_DEVICE_PAD));
+    int rc = h2d_staged(r->ctx, r->dfile.p, r->map, r->size);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(r->dfile.as<uint8_t>() + r->size, 0, RIO_DEVICE_PAD, r->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(r->ctx->stream));
+    r->on_device = true;
+    return RIO_OK;
+}
+
+static int fetch_result(rio_reader* r, const ReadAtResult& res, const uint8_t** data, uint64_t* len, int* is_nil) {
+    r->det0 = res.det0;
+    r->det1 = res.det1;
+    if (res.status != RIO_OK) return res.status;
+    if (is_nil) *is_nil = res.nil;
+    if (len) *len = res.nil ? 0 : res.len;
+    r->rec_buf.resize(res.len + 1);
+    if (!res.nil && res.len) {
+        HIP_TRY(hipMemcpy(r->rec_buf.data(), r->ctx->readat_out.p, res.len, hipMemcpyDeviceToHost));
+    }
+    if (data) *data = r->rec_buf.data();
+    return RIO_OK;
+}
+
+extern "C" int rio_reader_read_next_at(rio_reader* r, uint64_t offset, const uint8_t** data, uint64_t* len,
+                                       int* is_nil) {
+    if (!r) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (data) *data = nullptr;
+    if (len) *len = 0;
+    if (is_nil) *is_nil = 0;
+    if (!r->open || r->closed) return RIO_ERR_STATE;
+    if (r->version < RIO_VERSION3 || r->compression == RIO_COMP_GZIP || r->compression == RIO_COMP_LZW)
+        return RIO_ERR_UNSUPPORTED;
+    int rc = ensure_on_device(r);
+    if (rc) return rc;
+    ReadAtResult res{};
+    rc = read_at_impl(r->ctx, r->dfile.as<uint8_t>(), r->size, offset, false, 0, &res, nullptr);
+    if (rc) return rc;
+    r->err_off = offset;
+    return fetch_result(r, res, data, len, is_nil);
+}
+
+extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, const uint8_t** data,
+                                    uint64_t* len, int* is_nil) {
+    if (!r) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (data) *data = nullptr;
+    if (len) *len = 0;
+    if (is_nil) *is_nil = 0;
+    if (rec_offset) *rec_offset = 0;
+    if (!r->open || r->closed) return RIO_ERR_STATE;
+    if (r->version < RIO_VERSION3 || r->compression == RIO_COMP_GZIP || r->compression == RIO_COMP_LZW)
+        return RIO_ERR_UNSUPPORTED;
+    int rc = ensure_on_device(r);
+    if (rc) return rc;
+    ReadAtResult res{};
+    uint64_t ro = 0;
+    rc = read_at_impl(r->ctx, r->dfile.as<uint8_t>(), r->size, offset, true, r->seek_len, &res, &ro);
+    if (rc) return rc;
+    if (rec_offset) *rec_offset = ro;
+    return fetch_result(r, res, data, len, is_nil);
+}
+
+extern "C" int rio_reader_set_seek_len(rio_reader* r, uint64_t seek_len) {
+    if (!r || seek_len == 0) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    r->seek_len = seek_len;
+    return RIO_OK;
+}

@@ -1,0 +1,101 @@
+// rio_device.h — structures shared by the HIP kernels (rio_kernels.hip) and the host runtime
+// (rio_capi.cpp). Internal to librio; the public boundary is include/rio.h.
+#pragma once
+#include <stdint.h>
+
+#include "rio.h"
+
+namespace rio {
+
+constexpr uint64_t kNone = ~0ull;       // "no speculative entry found in this chunk"
+constexpr uint64_t kNilBit = 1ull << 63;  // scratch out_len | kNilBit => nil record
+
+// Framing chunk: a byte range [cs, ce) of the file; a chunk OWNS the records whose header starts
+// in its range. Written by the walk kernel, consumed by the scan / place kernels.
+struct ChunkSum {
+    uint64_t entry;    // speculative first record start in [cs, ce) (kNone if none validated)
+    uint64_t exit;     // first record start >= ce reached from `entry` (or err_off if status != OK)
+    uint64_t bytes;    // decoded bytes of the records walked from `entry`
+    uint64_t err_off;  // offset of the header that raised `status`
+    uint64_t det0, det1;  // HEADER_CRC expected/actual; MAGIC: bytes consumed by the magic varint
+    uint32_t count;    // records walked from `entry` (all stored in scratch)
+    int32_t status;    // RIO_OK or the terminal status raised inside this chunk
+};
+
+// Key-point summary of a run of chunks: the composed chunk functions
+// evaluated at the run's first speculative entry `key`; identity (pass-through) for inputs >= ce.
+struct RunSum {
+    uint64_t key;      // kNone: the run has no speculative entry (owns nothing unless broken)
+    uint64_t out;      // chain position after the run when entered at `key`
+    uint64_t cnt;      // records owned
+    uint64_t bytes;    // decoded bytes owned
+    uint64_t ce;       // end of the run's byte range (0 = identity element)
+    uint32_t term;     // the chain terminated (status) inside the run
+    uint32_t broken;   // a speculative entry did not chain: slow path required
+    uint64_t term_chunk;  // chunk index that raised the terminal status
+};
+
+// Per-chunk placement decided by the scan: records [base_idx, base_idx + owned) of the file are
+// this chunk's scratch slots [0, owned).
+struct ChunkPlace {
+    uint64_t base_idx;
+    uint64_t base_bytes;
+    uint64_t owned;
+};
+
+// Device-side scan state (one per decode call).
+struct ScanState {
+    uint32_t version, compression;
+    int32_t hdr_status;     // file header status
+    uint32_t slow;          // 1 => ChunkPlace array is authoritative (sequential repair ran)
+    uint64_t n_records;
+    uint64_t total_bytes;
+    int32_t status;         // terminal status
+    uint32_t zero_nonzero;  // zero-tail check result (1 = a non-zero byte found)
+    uint64_t status_offset;
+    uint64_t det0, det1;
+    uint64_t zero_from;     // zero-tail check range start (kNone = no check)
+    uint64_t n_repairs;
+    uint64_t decode_err_rec;  // min record index that failed to decompress (kNone = none)
+    uint32_t capacity_fail;
+    uint32_t pad;
+};
+
+// Result of the single-record (ReadNextAt) kernel.
+struct ReadAtResult {
+    int32_t status;
+    int32_t nil;
+    uint64_t len;
+    uint64_t det0, det1;
+    uint64_t hdr_len;
+    uint64_t payload_off;
+};
+
+// Launch configuration passed from the host runtime.
+struct FrameParams {
+    const uint8_t* file;
+    uint64_t len;
+    uint64_t chunk_bytes;
+    uint64_t n_chunks;
+    uint64_t slots;  // scratch slots per chunk
+    uint64_t* scratch_off;   // [n_chunks * slots] record header offsets
+    uint64_t* scratch_len;   // [n_chunks * slots] decoded length | kNilBit
+    ChunkSum* chunks;
+    RunSum* block_runs;      // [n_blocks] (scan level 1 output)
+    RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix
+    ChunkPlace* place;       // [n_chunks]
+    uint64_t* block_in;      // [n_blocks] chain position entering each block
+    RunSum* block_excl;      // [n_blocks] exclusive prefix over blocks
+    uint64_t n_blocks;
+    ScanState* state;
+    // outputs
+    uint8_t* out;
+    uint64_t out_cap;
+    uint64_t* out_off;
+    uint64_t* rec_off;
+    uint8_t* flags;
+    uint64_t rec_cap;
+    rio_file_info* info;  // device copy of the public result
+};
+
+}  // namespace rio

@@ -1,0 +1,881 @@
+// rio_kernels.hip — CDNA4 (gfx950) kernels of the recordio v3/v4 decode path.
+//
+// Pipeline for one file already in HBM:
+//   k_header        file header (readFileHeaderFromBuffer, common_reader.go:22-44)
+//   k_walk          one thread per 4 KiB chunk: speculative entry (first CRC-validated header in
+//                   the chunk) then header-to-header hops (readRecordHeaderV4/V3,
+//                   common_reader.go:83-151; payload sizing common_reader.go:162-169; snappy
+//                   preamble = decoded size). Records go to per-chunk scratch slots.
+//   k_scan_blocks   256-chunk blocks: inclusive scan of key-point chunk summaries (stitches each
+//   k_scan_top      chunk's speculative entry to its predecessor's exit; a mismatch => sequential
+//                   repair walk), record/byte prefix sums, terminal status (FileReader.ReadNext
+//                   loop, file_reader.go:61-131).
+//   k_place         scratch -> rec_off / out_off / flags at their global record index.
+//   k_zero          zero-tail check behind a magic mismatch (file_reader.go:76-91).
+//   k_decode_*      payload -> record bytes (copy, or golang/snappy v1.0.0 block decode).
+//   k_finalize      public rio_file_info.
+// Byte/integer work only: no MFMA. All offsets 64-bit.
+#include <hip/hip_runtime.h>
+
+#include "rio_device.h"
+
+namespace rio {
+
+// ------------------------------------------------------------------------------------------
+// Byte-level primitives
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t crc32c_byte(uint32_t c, uint32_t b) {
+    c ^= b;
+#pragma unroll
+    for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    return c;
+}
+
+// io.ByteReader over file bytes [base, base+avail); `cap` = checksumByteReader cache (36 for v4
+// FileReader, checksum_byte_reader.go:25-27), ~0 when no cache applies.
+struct Src {
+    const uint8_t* f;
+    uint64_t base, avail, pos, cap;
+};
+
+__device__ __forceinline__ int src_byte(Src& s, uint32_t& b) {
+    if (s.pos >= s.avail) return RIO_EOF;
+    if (s.pos >= s.cap) {
+        s.pos++;
+        return RIO_ERR_HEADER_TOO_LONG;
+    }
+    b = s.f[s.base + s.pos++];
+    return RIO_OK;
+}
+
+// encoding/binary.ReadUvarint semantics
+__device__ int read_uvarint(Src& s, uint64_t& x) {
+    uint64_t v = 0;
+    uint32_t sh = 0;
+    for (int i = 0; i < 10; i++) {
+        uint32_t b;
+        int e = src_byte(s, b);
+        if (e) return (e == RIO_EOF && i > 0) ? RIO_ERR_UNEXPECTED_EOF : e;
+        if (b < 0x80) {
+            if (i == 9 && b > 1) return RIO_ERR_VARINT_OVERFLOW;
+            x = v | ((uint64_t)b << sh);
+            return RIO_OK;
+        }
+        v |= (uint64_t)(b & 0x7F) << sh;
+        sh += 7;
+    }
+    return RIO_ERR_VARINT_OVERFLOW;
+}
+
+// encoding/binary.Uvarint semantics: >0 bytes read, 0 buffer too small, <0 overflow
+__device__ int uvarint_buf(const uint8_t* p, uint64_t n, uint64_t& x) {
+    uint64_t v = 0;
+    uint32_t sh = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (i == 10) return -(int)(i + 1);
+        uint32_t b = p[i];
+        if (b < 0x80) {
+            if (i == 9 && b > 1) return -(int)(i + 1);
+            x = v | ((uint64_t)b << sh);
+            return (int)(i + 1);
+        }
+        v |= (uint64_t)(b & 0x7F) << sh;
+        sh += 7;
+    }
+    return 0;
+}
+
+struct Hdr {
+    uint64_t u, c, exp_crc, act_crc;
+    uint32_t hdr_len, magic_len;
+    int nil;
+};
+
+__device__ __forceinline__ int later_field(int e) { return e == RIO_EOF ? RIO_EOF_HEADER : e; }
+
+// readRecordHeaderV4 (common_reader.go:110-151) / readRecordHeaderV3 (:83-108)
+__device__ int parse_header(const uint8_t* f, uint64_t p, uint64_t avail, uint64_t cap, uint32_t ver,
+                            Hdr& h) {
+    Src s{f, p, avail, 0, cap};
+    uint64_t m = 0;
+    h.nil = 0;
+    h.hdr_len = 0;
+    int e = read_uvarint(s, m);
+    h.magic_len = (uint32_t)s.pos;
+    if (e) return e;
+    if (m != RIO_MAGIC) return RIO_ERR_MAGIC;
+    uint32_t nb;
+    e = src_byte(s, nb);
+    if (e) return later_field(e);
+    e = read_uvarint(s, h.u);
+    if (e) return later_field(e);
+    e = read_uvarint(s, h.c);
+    if (e) return later_field(e);
+    if (ver == RIO_VERSION4) {
+        uint32_t crc = 0xFFFFFFFFu;
+        for (uint64_t i = 0; i < s.pos; i++) crc = crc32c_byte(crc, f[p + i]);
+        h.act_crc = crc ^ 0xFFFFFFFFu;
+        e = read_uvarint(s, h.exp_crc);
+        if (e) return later_field(e);
+        if (h.act_crc != h.exp_crc) return RIO_ERR_HEADER_CRC;
+    }
+    h.nil = (nb == 1);
+    h.hdr_len = (uint32_t)s.pos;
+    return RIO_OK;
+}
+
+// FileReader sequential semantics at record start p: header + payload availability + decoded
+// size. next = start of the following record.
+__device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t ver, uint32_t comp,
+                            Hdr& h, uint64_t& next, uint64_t& out_len) {
+    uint64_t cap = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : ~0ull;
+    int e = parse_header(f, p, len - p, cap, ver, h);
+    if (e) return e;
+    if (h.nil) {  // file_reader.go:96-99: nil => no payload bytes
+        next = p + h.hdr_len;
+        out_len = 0;
+        return RIO_OK;
+    }
+    uint64_t plen = comp != RIO_COMP_NONE ? h.c : h.u;
+    uint64_t avail = len - p - h.hdr_len;
+    if (plen > avail) return avail == 0 ? RIO_EOF_PAYLOAD : RIO_ERR_UNEXPECTED_EOF;
+    if (comp == RIO_COMP_SNAPPY) {
+        uint64_t d = 0;
+        int k = uvarint_buf(f + p + h.hdr_len, plen, d);
+        // snappy decodedLen: n<=0 or > 0xffffffff => ErrCorrupt; a preamble above 22x the element
+        // bytes cannot be produced (max 64 output bytes per 3-byte tagCopy2) => ErrCorrupt later.
+        if (k <= 0 || d > 0xFFFFFFFFull || d > 22ull * (plen - (uint64_t)k) + 64) return RIO_ERR_DECOMPRESS;
+        out_len = d;
+    } else {
+        out_len = plen;
+    }
+    next = p + h.hdr_len + plen;
+    return RIO_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// k_header
+// ------------------------------------------------------------------------------------------
+__global__ void k_header(FrameParams P) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    ScanState* st = P.state;
+    const uint8_t* f = P.file;
+    st->n_records = 0;
+    st->total_bytes = 0;
+    st->status = RIO_OK;
+    st->status_offset = RIO_FILE_HEADER_BYTES;
+    st->det0 = st->det1 = 0;
+    st->zero_from = kNone;
+    st->zero_nonzero = 0;
+    st->n_repairs = 0;
+    st->decode_err_rec = kNone;
+    st->capacity_fail = 0;
+    st->slow = 0;
+    if (P.len < RIO_FILE_HEADER_BYTES) {
+        st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;
+        st->version = st->compression = 0;
+        return;
+    }
+    uint32_t v = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+    uint32_t c = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+    st->version = v;
+    st->compression = c;
+    int hs = RIO_OK;
+    if (v > RIO_VERSION4 || v < RIO_VERSION1) {
+        hs = RIO_ERR_VERSION;
+        st->det0 = v;
+    } else if (c > RIO_COMP_LZW) {
+        hs = RIO_ERR_COMPRESSION_TYPE;
+        st->det0 = c;
+    } else if (v < RIO_VERSION3 || c == RIO_COMP_GZIP || c == RIO_COMP_LZW) {
+        hs = RIO_ERR_UNSUPPORTED;  // reference reader keeps these
+    }
+    st->hdr_status = hs;
+}
+
+// ------------------------------------------------------------------------------------------
+// Chunk walk
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t chunk_start(const FrameParams& P, uint64_t c) {
+    return RIO_FILE_HEADER_BYTES + c * P.chunk_bytes;
+}
+__device__ __forceinline__ uint64_t chunk_end(const FrameParams& P, uint64_t c) {
+    uint64_t e = chunk_start(P, c) + P.chunk_bytes;
+    return e < P.len ? e : P.len;
+}
+
+// First position in [cs, ce) holding the canonical magic bytes 91 8d 4c whose header and payload
+// validate under FileReader semantics (CRC for v4). Speculative; stitched by the scan.
+__device__ uint64_t find_entry(const FrameParams& P, uint64_t cs, uint64_t ce, uint32_t ver, uint32_t comp) {
+    const uint8_t* f = P.file;
+    for (uint64_t q = cs & ~15ull; q < ce; q += 16) {
+        const uint4 w = *reinterpret_cast<const uint4*>(f + q);
+        uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t x = ws[k] ^ 0x91919191u;
+            uint32_t hit = (x - 0x01010101u) & ~x & 0x80808080u;
+            while (hit) {
+                int b = __builtin_ctz(hit) >> 3;
+                hit &= hit - 1;
+                uint64_t p = q + 4 * k + b;
+                if (p < cs || p >= ce || p + 2 >= P.len) continue;
+                if (f[p + 1] != 0x8D || f[p + 2] != 0x4C) continue;
+                Hdr h;
+                uint64_t nx, ol;
+                if (frame_record(f, P.len, p, ver, comp, h, nx, ol) == RIO_OK) return p;
+            }
+        }
+    }
+    return kNone;
+}
+
+// Walk chunk c from record start `from` (kNone => nothing to walk), filling its scratch slots.
+__device__ void walk_chunk(const FrameParams& P, uint64_t c, uint64_t from, uint32_t ver, uint32_t comp) {
+    const uint64_t ce = chunk_end(P, c);
+    ChunkSum s;
+    s.entry = from;
+    s.exit = kNone;
+    s.bytes = 0;
+    s.err_off = 0;
+    s.det0 = s.det1 = 0;
+    s.count = 0;
+    s.status = RIO_OK;
+    if (from != kNone) {
+        uint64_t p = from;
+        uint64_t* so = P.scratch_off + c * P.slots;
+        uint64_t* sl = P.scratch_len + c * P.slots;
+        while (p < ce) {
+            Hdr h;
+            uint64_t next = 0, olen = 0;
+            int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen);
+            if (e) {
+                s.status = e;
+                s.err_off = p;
+                if (e == RIO_ERR_HEADER_CRC) {
+                    s.det0 = h.exp_crc;
+                    s.det1 = h.act_crc;
+                } else if (e == RIO_ERR_MAGIC) {
+                    s.det0 = h.magic_len;
+                } else if (e == RIO_ERR_UNEXPECTED_EOF && h.hdr_len != 0) {
+                    s.det0 = 1;  // raised by the payload read, not by a header varint
+                }
+                break;
+            }
+            if (s.count < P.slots) {
+                so[s.count] = p;
+                sl[s.count] = olen | (h.nil ? kNilBit : 0);
+            }
+            s.count++;
+            s.bytes += olen;
+            p = next;
+        }
+        s.exit = s.status ? s.err_off : p;
+    }
+    P.chunks[c] = s;
+}
+
+__global__ void __launch_bounds__(256) k_walk(FrameParams P) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= P.n_chunks) return;
+    const ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK) return;
+    const uint32_t ver = st->version, comp = st->compression;
+    const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
+    uint64_t entry = (c == 0) ? (uint64_t)RIO_FILE_HEADER_BYTES : find_entry(P, cs, ce, ver, comp);
+    walk_chunk(P, c, entry, ver, comp);
+}
+
+// ------------------------------------------------------------------------------------------
+// Key-point run composition. combine(A, B): A's byte range precedes B's.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ RunSum run_identity() {
+    RunSum r;
+    r.key = kNone;
+    r.out = 0;
+    r.cnt = 0;
+    r.bytes = 0;
+    r.ce = 0;
+    r.term = 0;
+    r.broken = 0;
+    r.term_chunk = 0;
+    return r;
+}
+
+__device__ __forceinline__ RunSum combine(const RunSum& A, const RunSum& B) {
+    if (B.ce == 0) return A;
+    if (A.ce == 0) return B;
+    if (A.key == kNone) {  // A owns nothing for the inputs the composite can represent
+        RunSum r = B;
+        return r;
+    }
+    RunSum r = A;
+    r.ce = B.ce;
+    if (A.broken || A.term) return r;
+    const uint64_t y = A.out;
+    if (y >= B.ce) return r;  // B passed through
+    if (B.key != kNone && y == B.key) {
+        r.out = B.out;
+        r.cnt = A.cnt + B.cnt;
+        r.bytes = A.bytes + B.bytes;
+        r.term = B.term;
+        r.broken = B.broken;
+        r.term_chunk = B.term_chunk;
+        return r;
+    }
+    r.broken = 1;
+    return r;
+}
+
+__device__ __forceinline__ RunSum chunk_run(const FrameParams& P, uint64_t c) {
+    const ChunkSum s = P.chunks[c];
+    RunSum r;
+    r.key = s.entry;
+    r.out = s.exit;
+    r.cnt = s.count;
+    r.bytes = s.bytes;
+    r.ce = chunk_end(P, c);
+    r.term = s.status != RIO_OK;
+    r.broken = 0;
+    r.term_chunk = c;
+    return r;
+}
+
+constexpr int kScanBlock = 256;
+
+// Level 1: inclusive scan of 256 chunk runs per block in LDS (Hillis-Steele, 8 steps).
+__global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
+    __shared__ RunSum buf[2][kScanBlock];
+    const int t = threadIdx.x;
+    const uint64_t c = (uint64_t)blockIdx.x * kScanBlock + t;
+    if (P.state->hdr_status != RIO_OK) return;
+    RunSum v = c < P.n_chunks ? chunk_run(P, c) : run_identity();
+    int cur = 0;
+    buf[cur][t] = v;
+    __syncthreads();
+    for (int d = 1; d < kScanBlock; d <<= 1) {
+        RunSum x = buf[cur][t];
+        if (t >= d) x = combine(buf[cur][t - d], x);
+        buf[cur ^ 1][t] = x;
+        cur ^= 1;
+        __syncthreads();
+    }
+    if (c < P.n_chunks) P.chunk_excl[c] = t > 0 ? buf[cur][t - 1] : run_identity();
+    if (t == kScanBlock - 1) P.block_runs[blockIdx.x] = buf[cur][t];
+}
+
+// Sequential repair (slow path): walks the true chain chunk by chunk, re-walking any chunk whose
+// speculative entry does not match. Runs on one thread; only for files whose speculation broke.
+__device__ void slow_path(const FrameParams& P, uint32_t ver, uint32_t comp) {
+    ScanState* st = P.state;
+    uint64_t cur = RIO_FILE_HEADER_BYTES, base_idx = 0, base_bytes = 0, repairs = 0;
+    bool term = false;
+    uint64_t term_chunk = 0;
+    for (uint64_t c = 0; c < P.n_chunks; c++) {
+        ChunkPlace pl{base_idx, base_bytes, 0};
+        if (!term && cur < chunk_end(P, c)) {
+            if (P.chunks[c].entry != cur) {
+                walk_chunk(P, c, cur, ver, comp);
+                repairs++;
+            }
+            const ChunkSum s = P.chunks[c];
+            pl.owned = s.count;
+            base_idx += s.count;
+            base_bytes += s.bytes;
+            if (s.status != RIO_OK) {
+                term = true;
+                term_chunk = c;
+            } else {
+                cur = s.exit;
+            }
+        }
+        P.place[c] = pl;
+    }
+    st->slow = 1;
+    st->n_repairs = repairs;
+    st->n_records = base_idx;
+    st->total_bytes = base_bytes;
+    if (term) {
+        const ChunkSum s = P.chunks[term_chunk];
+        st->status = s.status;
+        st->status_offset = s.err_off;
+        st->det0 = s.det0;
+        st->det1 = s.det1;
+    } else {
+        st->status = RIO_EOF;
+        st->status_offset = cur;
+    }
+}
+
+// Level 2: one workgroup scans the block runs (tiles of 1024 with a carry), decides fast/slow
+// path and the terminal status.
+__global__ void __launch_bounds__(1024) k_scan_top(FrameParams P) {
+    __shared__ RunSum buf[2][1024];
+    __shared__ RunSum carry_s;
+    ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK) return;
+    const uint32_t ver = st->version, comp = st->compression;
+    const int t = threadIdx.x;
+    if (P.n_chunks == 0) {
+        if (t == 0) {
+            st->status = RIO_EOF;
+            st->status_offset = P.len;
+        }
+        return;  // (len == 8: the first ReadNext hits EOF)
+    }
+    if (t == 0) carry_s = run_identity();
+    __syncthreads();
+    for (uint64_t base = 0; base < P.n_blocks; base += 1024) {
+        const uint64_t b = base + t;
+        RunSum v = b < P.n_blocks ? P.block_runs[b] : run_identity();
+        int cur = 0;
+        buf[cur][t] = v;
+        __syncthreads();
+        for (int d = 1; d < 1024; d <<= 1) {
+            RunSum x = buf[cur][t];
+            if (t >= d) x = combine(buf[cur][t - d], x);
+            buf[cur ^ 1][t] = x;
+            cur ^= 1;
+            __syncthreads();
+        }
+        const RunSum carry = carry_s;
+        RunSum excl = combine(carry, t > 0 ? buf[cur][t - 1] : run_identity());
+        if (b < P.n_blocks) P.block_excl[b] = excl;
+        __syncthreads();
+        if (t == 1023) carry_s = combine(carry, buf[cur][t]);
+        __syncthreads();
+    }
+    const RunSum total = carry_s;
+    if (t != 0) return;
+    // total.key is chunk 0's forced entry (8): total describes the true chain unless broken.
+    if (total.broken) {
+        slow_path(P, ver, comp);
+        if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
+        return;
+    }
+    st->n_records = total.cnt;
+    st->total_bytes = total.bytes;
+    if (total.term) {
+        const ChunkSum s = P.chunks[total.term_chunk];
+        st->status = s.status;
+        st->status_offset = s.err_off;
+        st->det0 = s.det0;
+        st->det1 = s.det1;
+    } else {
+        st->status = RIO_EOF;  // chain ended exactly at the file end
+        st->status_offset = total.out;
+    }
+    if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
+}
+
+// Placement: one thread per chunk copies its owned scratch records to the global index.
+__global__ void __launch_bounds__(256) k_place(FrameParams P) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const ScanState* st = P.state;
+    if (c >= P.n_chunks || st->hdr_status != RIO_OK) return;
+    ChunkPlace pl;
+    if (st->slow) {
+        pl = P.place[c];
+    } else {
+        const uint64_t b = c / kScanBlock;
+        const RunSum B = P.block_excl[b];
+        const RunSum E = P.chunk_excl[c];
+        // chain position entering block b (block 0 is entered at 8 = its forced key). A block
+        // owns records only if the chain enters it exactly at its key; otherwise it was passed
+        // through (a record spans it) or the chain terminated before it.
+        const uint64_t xb = (b == 0) ? (uint64_t)RIO_FILE_HEADER_BYTES : B.out;
+        const bool entered = (b == 0) || (!B.term && !B.broken && xb == P.block_runs[b].key);
+        pl.owned = 0;
+        pl.base_idx = B.cnt + E.cnt;
+        pl.base_bytes = B.bytes + E.bytes;
+        if (entered && !E.term && !E.broken) {
+            const uint64_t y = (E.key == kNone) ? xb : E.out;
+            const ChunkSum s = P.chunks[c];
+            if (s.entry != kNone && y == s.entry) pl.owned = s.count;
+        }
+        P.place[c] = pl;
+    }
+    if (pl.owned == 0) return;
+    if (pl.base_idx + pl.owned > P.rec_cap || st->n_records > P.rec_cap) return;
+    const uint64_t* so = P.scratch_off + c * P.slots;
+    const uint64_t* sl = P.scratch_len + c * P.slots;
+    uint64_t ob = pl.base_bytes;
+    for (uint64_t k = 0; k < pl.owned; k++) {
+        const uint64_t i = pl.base_idx + k;
+        const uint64_t l = sl[k];
+        P.rec_off[i] = so[k];
+        P.out_off[i] = ob;
+        P.flags[i] = (l & kNilBit) ? RIO_FLAG_NIL : 0;
+        ob += l & ~kNilBit;
+    }
+}
+
+// Capacity check + sentinel out_off[n] + zero-tail range.
+__global__ void k_post_scan(FrameParams P) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK) return;
+    if (st->n_records > P.rec_cap || st->total_bytes > P.out_cap) {
+        st->capacity_fail = 1;
+        return;
+    }
+    P.out_off[st->n_records] = st->total_bytes;
+}
+
+__global__ void __launch_bounds__(256) k_zero(FrameParams P) {
+    ScanState* st = P.state;
+    const uint64_t from = st->zero_from;
+    if (from == kNone || st->hdr_status != RIO_OK) return;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t nz = 0;
+    for (uint64_t q = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < P.len; q += stride)
+        nz |= P.file[q];
+    if (nz) atomicOr(&st->zero_nonzero, 1u);
+}
+
+// ------------------------------------------------------------------------------------------
+// Decode
+// ------------------------------------------------------------------------------------------
+// Re-parse an already validated header at a record start: sizes and header length, no checks.
+__device__ __forceinline__ uint64_t vread(const uint8_t* f, uint64_t& i) {
+    uint64_t v = 0;
+    uint32_t sh = 0, b;
+    do {
+        b = f[i++];
+        v |= (uint64_t)(b & 0x7F) << sh;
+        sh += 7;
+    } while ((b & 0x80) && sh < 70);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t header_fields_fast(const uint8_t* f, uint64_t p, uint32_t ver, uint64_t& u,
+                                                       uint64_t& c) {
+    uint64_t i = p;
+    (void)vread(f, i);  // magic
+    i++;                // nil byte
+    u = vread(f, i);
+    c = vread(f, i);
+    if (ver == RIO_VERSION4) (void)vread(f, i);  // crc
+    return (uint32_t)(i - p);
+}
+
+// One wave per record: lanes stride the payload bytes (uncompressed files).
+__global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
+    const ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_NONE) return;
+    const uint64_t n = st->n_records;
+    const uint32_t ver = st->version;
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i = wave; i < n; i += nwaves) {
+        const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
+        if (o1 == o0) continue;
+        const uint64_t p = P.rec_off[i];
+        uint64_t u, cl;
+        const uint64_t src = p + header_fields_fast(P.file, p, ver, u, cl);
+        for (uint64_t k = lane; k < o1 - o0; k += 64) P.out[o0 + k] = P.file[src + k];
+    }
+}
+
+// golang/snappy v1.0.0 decode (decode_other.go) of one record by one thread.
+__device__ bool snappy_decode_thread(const uint8_t* src, uint64_t slen, uint8_t* dst, uint64_t dlen) {
+    uint64_t s = 0, d = 0;
+    while (s < slen) {
+        const uint32_t tag = src[s];
+        uint64_t length, offset;
+        if ((tag & 3) == 0) {
+            uint32_t x = tag >> 2;
+            if (x < 60) {
+                s += 1;
+            } else {
+                const uint32_t nb = x - 59;  // 1..4 extra length bytes
+                s += 1 + nb;
+                if (s > slen) return false;
+                x = 0;
+                for (uint32_t k = 0; k < nb; k++) x |= (uint32_t)src[s - nb + k] << (8 * k);
+            }
+            length = (uint64_t)x + 1;
+            if (length > dlen - d || length > slen - s) return false;
+            for (uint64_t k = 0; k < length; k++) dst[d + k] = src[s + k];
+            d += length;
+            s += length;
+            continue;
+        }
+        if ((tag & 3) == 1) {
+            s += 2;
+            if (s > slen) return false;
+            length = 4 + ((tag >> 2) & 7);
+            offset = ((tag & 0xE0u) << 3) | src[s - 1];
+        } else if ((tag & 3) == 2) {
+            s += 3;
+            if (s > slen) return false;
+            length = 1 + (tag >> 2);
+            offset = (uint64_t)src[s - 2] | (uint64_t)src[s - 1] << 8;
+        } else {
+            s += 5;
+            if (s > slen) return false;
+            length = 1 + (tag >> 2);
+            offset = (uint64_t)src[s - 4] | (uint64_t)src[s - 3] << 8 | (uint64_t)src[s - 2] << 16 |
+                     (uint64_t)src[s - 1] << 24;
+        }
+        if (offset == 0 || d < offset || length > dlen - d) return false;
+        for (uint64_t k = 0; k < length; k++) dst[d + k] = dst[d - offset + k];
+        d += length;
+    }
+    return d == dlen;
+}
+
+__global__ void __launch_bounds__(256) k_decode_snappy(FrameParams P) {
+    ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
+    const uint64_t n = st->n_records;
+    const uint32_t ver = st->version;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (P.flags[i] & RIO_FLAG_NIL) continue;
+        const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
+        const uint64_t p = P.rec_off[i];
+        uint64_t u, cl;
+        const uint32_t hl = header_fields_fast(P.file, p, ver, u, cl);
+        const uint8_t* pay = P.file + p + hl;
+        uint64_t dl = 0;
+        const int k = uvarint_buf(pay, cl, dl);
+        if (k <= 0 || dl != o1 - o0 ||
+            !snappy_decode_thread(pay + k, cl - (uint64_t)k, P.out + o0, o1 - o0))
+            atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)i);
+    }
+}
+
+__global__ void k_finalize(FrameParams P) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    ScanState* st = P.state;
+    rio_file_info info;
+    info.version = st->version;
+    info.compression = st->compression;
+    info.reserved0 = 0;
+    info.n_chunks = P.n_chunks;
+    info.n_repairs = st->n_repairs;
+    info.detail0 = 0;
+    info.detail1 = 0;
+    if (st->hdr_status != RIO_OK) {
+        info.n_records = 0;
+        info.total_out_bytes = 0;
+        info.status = st->hdr_status;
+        info.status_offset = 0;
+        info.detail0 = st->det0;
+        *P.info = info;
+        return;
+    }
+    info.n_records = st->n_records;
+    info.total_out_bytes = st->total_bytes;
+    info.status = st->status;
+    info.status_offset = st->status_offset;
+    info.detail0 = st->det0;
+    info.detail1 = st->det1;
+    if (st->status == RIO_ERR_MAGIC && st->zero_from != kNone && !st->zero_nonzero) {
+        info.status = RIO_EOF_ZERO_TAIL;
+        info.detail0 = 0;
+    }
+    if (st->capacity_fail) {
+        info.status = RIO_ERR_CAPACITY;
+    } else if (st->decode_err_rec != kNone && st->decode_err_rec < st->n_records) {
+        const uint64_t r = st->decode_err_rec;
+        info.n_records = r;
+        info.total_out_bytes = P.out_off[r];
+        info.status = RIO_ERR_DECOMPRESS;
+        info.status_offset = P.rec_off[r];
+        info.detail0 = info.detail1 = 0;
+    }
+    *P.info = info;
+}
+
+// ------------------------------------------------------------------------------------------
+// Single record at an arbitrary offset: MMapReader.ReadNextAt (mmap_reader.go:130-203, 298-356)
+// ------------------------------------------------------------------------------------------
+__device__ int read_at_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_t comp, uint64_t off,
+                           uint8_t* out, uint64_t out_cap, ReadAtResult& r, bool write) {
+    r.nil = 0;
+    r.len = 0;
+    r.det0 = r.det1 = 0;
+    if (off > len) return RIO_ERR_INVALID_OFFSET;  // x/exp/mmap ReadAt bounds
+    const uint64_t wmax = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : RIO_RECORD_HEADER_V3_MAX;
+    const uint64_t w = len - off < wmax ? len - off : wmax;
+    if (w == 0) return RIO_EOF;  // bare io.EOF
+    Hdr h;
+    int e = parse_header(f, off, w, ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : ~0ull, ver, h);
+    if (e == RIO_EOF) e = RIO_EOF_HEADER;
+    if (e == RIO_ERR_HEADER_CRC) {
+        r.det0 = h.exp_crc;
+        r.det1 = h.act_crc;
+    }
+    if (e) return e;
+    r.hdr_len = h.hdr_len;
+    if (h.nil) {
+        r.nil = 1;
+        return RIO_OK;
+    }
+    const uint64_t plen = comp != RIO_COMP_NONE ? h.c : h.u;
+    if (plen > len - off - h.hdr_len) return RIO_EOF_PAYLOAD;
+    const uint8_t* pay = f + off + h.hdr_len;
+    r.payload_off = off + h.hdr_len;
+    if (comp == RIO_COMP_NONE) {
+        r.len = plen;
+        if (!write) return RIO_OK;
+        if (plen > out_cap) return RIO_ERR_CAPACITY;
+        for (uint64_t k = 0; k < plen; k++) out[k] = pay[k];
+        return RIO_OK;
+    }
+    uint64_t dl = 0;
+    const int k = uvarint_buf(pay, plen, dl);
+    if (k <= 0 || dl > 0xFFFFFFFFull || dl > 22ull * (plen - (uint64_t)k) + 64) return RIO_ERR_DECOMPRESS;
+    r.len = dl;
+    if (dl > out_cap) return RIO_ERR_CAPACITY;
+    if (!snappy_decode_thread(pay + k, plen - (uint64_t)k, out, dl)) return RIO_ERR_DECOMPRESS;
+    return RIO_OK;
+}
+
+__global__ void k_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t* out, uint64_t out_cap,
+                          ReadAtResult* res) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    ReadAtResult r{};
+    uint32_t ver = 0, comp = 0;
+    int e = RIO_OK;
+    if (len < RIO_FILE_HEADER_BYTES) {
+        e = RIO_ERR_SHORT_FILE_HEADER;
+    } else {
+        ver = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+        comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+        if (ver > RIO_VERSION4 || ver < RIO_VERSION1) e = RIO_ERR_VERSION;
+        else if (comp > RIO_COMP_LZW) e = RIO_ERR_COMPRESSION_TYPE;
+        else if (ver < RIO_VERSION3 || comp == RIO_COMP_GZIP || comp == RIO_COMP_LZW) e = RIO_ERR_UNSUPPORTED;
+    }
+    if (e == RIO_OK) e = read_at_dev(f, len, ver, comp, off, out, out_cap, r, true);
+    r.status = e;
+    *res = r;
+}
+
+// MMapReader.SeekNext (mmap_reader.go:58-128): windowed scan for 91 8d 4c with its skip rule,
+// trial ReadNextAt per hit; CRC / magic / io.EOF-class failures continue the scan.
+__global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
+                            uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    ReadAtResult r{};
+    *rec_off = 0;
+    uint32_t ver = 0, comp = 0;
+    int e = RIO_OK;
+    if (len < RIO_FILE_HEADER_BYTES) {
+        e = RIO_ERR_SHORT_FILE_HEADER;
+    } else {
+        ver = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+        comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+        if (ver > RIO_VERSION4 || ver < RIO_VERSION1) e = RIO_ERR_VERSION;
+        else if (comp > RIO_COMP_LZW) e = RIO_ERR_COMPRESSION_TYPE;
+        else if (ver < RIO_VERSION3 || comp == RIO_COMP_GZIP || comp == RIO_COMP_LZW) e = RIO_ERR_UNSUPPORTED;
+    }
+    if (e) {
+        r.status = e;
+        *res = r;
+        return;
+    }
+    const uint8_t M[3] = {0x91, 0x8D, 0x4C};
+    uint64_t next = off;
+    for (;;) {
+        if (next > len) {
+            r.status = RIO_ERR_INVALID_OFFSET;
+            break;
+        }
+        const uint64_t num = len - next < seek_len ? len - next : seek_len;
+        if (num == 0) {
+            r.status = RIO_EOF;
+            break;
+        }
+        uint64_t i = 0;
+        bool boundary = false, done = false;
+        while (i < num) {
+            uint64_t ix = i;
+            for (int j = 0; j < 3; j++) {
+                if (f[next + ix] != M[j]) break;
+                ix++;
+                if (ix >= num) {
+                    boundary = true;
+                    break;
+                }
+            }
+            if (boundary) break;
+            if (ix - i < 3) {
+                i = ix + 1;
+                continue;
+            }
+            const uint64_t trial = next + i;
+            ReadAtResult t{};
+            const int te = read_at_dev(f, len, ver, comp, trial, out, out_cap, t, true);
+            if (te != RIO_OK && (te == RIO_ERR_HEADER_CRC || te == RIO_ERR_MAGIC || te == RIO_EOF ||
+                                 te == RIO_EOF_HEADER || te == RIO_EOF_PAYLOAD)) {
+                i = ix;
+                continue;
+            }
+            t.status = te;
+            r = t;
+            *rec_off = trial;
+            done = true;
+            break;
+        }
+        if (done) break;
+        if (i == 0) {
+            r.status = RIO_EOF;
+            break;
+        }
+        next += i;
+    }
+    *res = r;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host-side launchers (called by rio_capi.cpp)
+// ------------------------------------------------------------------------------------------
+static inline unsigned blocks_for(uint64_t n, unsigned bs) {
+    uint64_t b = (n + bs - 1) / bs;
+    return (unsigned)(b == 0 ? 1 : b);
+}
+
+// Phase A: framing + scan + zero-tail check; k_finalize publishes the framing result (sizes).
+hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
+    if (ev) (void)hipEventRecord(ev[0], s);
+    hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, P);
+    hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, 256)), dim3(256), 0, s, P);
+    if (ev) (void)hipEventRecord(ev[1], s);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, P);
+    hipLaunchKernelGGL(k_zero, dim3(256), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, P);
+    if (ev) (void)hipEventRecord(ev[2], s);
+    return hipGetLastError();
+}
+
+// Phase B: placement into the caller's arrays, decode, final result.
+hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
+    const unsigned grid = 2048;
+    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 256)), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_post_scan, dim3(1), dim3(64), 0, s, P);
+    if (ev) (void)hipEventRecord(ev[3], s);
+    hipLaunchKernelGGL(k_decode_copy, dim3(grid), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_decode_snappy, dim3(grid), dim3(256), 0, s, P);
+    if (ev) (void)hipEventRecord(ev[4], s);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t* out, uint64_t out_cap,
+                          ReadAtResult* res, hipStream_t s) {
+    hipLaunchKernelGGL(k_read_at, dim3(1), dim3(64), 0, s, f, len, off, out, out_cap, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
+                            uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off, hipStream_t s) {
+    hipLaunchKernelGGL(k_seek_next, dim3(1), dim3(64), 0, s, f, len, off, seek_len, out, out_cap, res, rec_off);
+    return hipGetLastError();
+}
+
+}  // namespace rio

@@ -1,0 +1,152 @@
+"""ctypes binding of librio.so (include/rio.h).
+
+The library is built in-tree (go-sstables_amd/librio.so) by __graft_entry__.build() /
+`make -C go-sstables_amd/csrc`. Loading it needs no GPU; every decode entry point needs one and
+fails loudly (RIO_ERR_HIP) without it. There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "librio.so"))
+
+# status codes (rio.h rio_status)
+RIO_OK = 0
+RIO_EOF = 1
+RIO_EOF_ZERO_TAIL = 2
+RIO_EOF_HEADER = 3
+RIO_EOF_PAYLOAD = 4
+RIO_ERR_UNEXPECTED_EOF = 5
+RIO_ERR_MAGIC = 6
+RIO_ERR_HEADER_CRC = 7
+RIO_ERR_VARINT_OVERFLOW = 8
+RIO_ERR_HEADER_TOO_LONG = 9
+RIO_ERR_DECOMPRESS = 10
+RIO_ERR_VERSION = 11
+RIO_ERR_COMPRESSION_TYPE = 12
+RIO_ERR_SHORT_FILE_HEADER = 13
+RIO_ERR_INVALID_OFFSET = 14
+RIO_ERR_UNSUPPORTED = 15
+RIO_ERR_CAPACITY = 16
+RIO_ERR_ARG = 17
+RIO_ERR_HIP = 18
+RIO_ERR_STATE = 19
+RIO_ERR_IO = 20
+
+EOF_CLASS = (RIO_EOF, RIO_EOF_ZERO_TAIL, RIO_EOF_HEADER, RIO_EOF_PAYLOAD)
+
+RIO_FLAG_NIL = 1
+RIO_DEVICE_PAD = 64
+COMP_NONE, COMP_GZIP, COMP_SNAPPY, COMP_LZW = 0, 1, 2, 3
+
+
+class FileInfo(ctypes.Structure):
+    _fields_ = [
+        ("version", c_uint32),
+        ("compression", c_uint32),
+        ("n_records", c_uint64),
+        ("total_out_bytes", c_uint64),
+        ("status", ctypes.c_int32),
+        ("reserved0", c_uint32),
+        ("status_offset", c_uint64),
+        ("detail0", c_uint64),
+        ("detail1", c_uint64),
+        ("n_chunks", c_uint64),
+        ("n_repairs", c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "rio_strerror": (c_char_p, [c_int]),
+    "rio_status_is_eof": (c_int, [c_int]),
+    "rio_build_info": (c_char_p, []),
+    "rio_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "rio_ctx_destroy": (None, [c_void_p]),
+    "rio_device_count": (c_int, [POINTER(c_int)]),
+    "rio_frame": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(FileInfo)]),
+    "rio_decode": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, POINTER(FileInfo)]),
+    "rio_device_decode": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p],
+    ),
+    "rio_max_records": (c_uint64, [c_uint64]),
+    "rio_ctx_last_stage_ms": (c_int, [c_void_p, POINTER(c_float), c_int]),
+    "rio_ctx_set_timing": (c_int, [c_void_p, c_int]),
+    "rio_device_read_at": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_int),
+         POINTER(c_uint64), POINTER(c_uint64)],
+    ),
+    "rio_reader_new_file": (c_int, [c_void_p, c_char_p, POINTER(c_void_p)]),
+    "rio_reader_new_mmap": (c_int, [c_void_p, c_char_p, POINTER(c_void_p)]),
+    "rio_reader_open": (c_int, [c_void_p]),
+    "rio_reader_close": (c_int, [c_void_p]),
+    "rio_reader_free": (None, [c_void_p]),
+    "rio_reader_header": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "rio_reader_size": (c_uint64, [c_void_p]),
+    "rio_reader_last_detail": (None, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
+    "rio_reader_read_next": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_int)]),
+    "rio_reader_skip_next": (c_int, [c_void_p]),
+    "rio_reader_read_next_at": (c_int, [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_int)]),
+    "rio_reader_seek_next": (
+        c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_uint64), POINTER(c_int)]),
+    "rio_reader_set_seek_len": (c_int, [c_void_p, c_uint64]),
+    "rio_reader_file_info": (c_int, [c_void_p, POINTER(FileInfo)]),
+    "rio_writer_new": (c_int, [c_char_p, c_uint32, POINTER(c_void_p)]),
+    "rio_writer_write": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "rio_writer_size": (c_uint64, [c_void_p]),
+    "rio_writer_close": (c_int, [c_void_p]),
+    "rio_encode_record_v4": (c_uint64, [c_void_p, c_uint64, c_uint32, c_void_p, c_uint64]),
+    "rio_encode_file_header": (None, [c_void_p, c_uint32, c_uint32]),
+    "rio_snappy_max_encoded_len": (c_uint64, [c_uint64]),
+    "rio_snappy_encode": (c_uint64, [c_void_p, c_uint64, c_void_p, c_uint64]),
+    "rio_generate": (c_uint64, [c_void_p, c_uint64, c_uint32, c_uint64, c_uint64, c_int, c_uint64, c_int]),
+    "rio_generate_bound": (c_uint64, [c_uint32, c_uint64, c_uint64]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """Load librio.so (in-tree). Raises if it has not been built: there is no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"librio.so not built at {LIB_PATH}: run `make -C go-sstables_amd/csrc` "
+                "(or __graft_entry__.build()); the recordio GPU path has no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def strerror(status: int) -> str:
+    return lib().rio_strerror(status).decode()
+
+
+_ctx = {}
+
+
+def default_ctx(device: int = 0) -> int:
+    """A per-device rio_ctx (created lazily; needs a GPU)."""
+    if device not in _ctx:
+        h = c_void_p()
+        rc = lib().rio_ctx_create(device, ctypes.byref(h))
+        if rc != RIO_OK:
+            raise RuntimeError(f"rio_ctx_create(device={device}) failed: {strerror(rc)} "
+                               "(the recordio decode path needs a HIP device)")
+        _ctx[device] = h.value
+    return _ctx[device]

@@ -1,0 +1,85 @@
+"""Device-resident decode (torch tensors as HBM buffers) over rio_device_decode.
+
+torch is plumbing here (allocation, streams, events); every byte of decode work is done by the
+HIP kernels of librio.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+
+
+@dataclass
+class DecodeBuffers:
+    out: torch.Tensor      # uint8 [>= total_out_bytes]
+    out_off: torch.Tensor  # int64 [n + 1]
+    rec_off: torch.Tensor  # int64 [n]
+    flags: torch.Tensor    # uint8 [n]
+    info: torch.Tensor     # uint8 [sizeof(rio_file_info)]
+
+
+INFO_BYTES = ctypes.sizeof(L.FileInfo)
+
+
+def to_device_file(image, device: int = 0) -> tuple[torch.Tensor, int]:
+    """Copy a file image (bytes / numpy uint8) into HBM with RIO_DEVICE_PAD readable pad bytes."""
+    import numpy as np
+
+    arr = np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray)) else image
+    n = int(arr.shape[0])
+    t = torch.zeros(n + L.RIO_DEVICE_PAD, dtype=torch.uint8, device=f"cuda:{device}")
+    t[:n].copy_(torch.from_numpy(np.ascontiguousarray(arr)))
+    return t, n
+
+
+class DeviceDecoder:
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.ctx = L.default_ctx(device)
+
+    def alloc(self, n_records: int, total_bytes: int) -> DecodeBuffers:
+        dev = f"cuda:{self.device}"
+        return DecodeBuffers(
+            out=torch.empty(max(total_bytes, 1) + 16, dtype=torch.uint8, device=dev),
+            out_off=torch.empty(n_records + 1, dtype=torch.int64, device=dev),
+            rec_off=torch.empty(max(n_records, 1), dtype=torch.int64, device=dev),
+            flags=torch.empty(max(n_records, 1), dtype=torch.uint8, device=dev),
+            info=torch.zeros(INFO_BYTES, dtype=torch.uint8, device=dev),
+        )
+
+    def launch(self, d_file: torch.Tensor, length: int, b: DecodeBuffers, stream=None) -> None:
+        """Enqueue the whole decode on `stream` (default: torch's current stream); no host sync."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = L.lib().rio_device_decode(
+            self.ctx, d_file.data_ptr(), length, b.out.data_ptr(), b.out.numel(), b.out_off.data_ptr(),
+            b.rec_off.data_ptr(), b.flags.data_ptr(), b.out_off.numel() - 1, b.info.data_ptr(),
+            ctypes.c_void_p(s.cuda_stream))
+        if rc != L.RIO_OK:
+            raise RuntimeError(f"rio_device_decode: {L.strerror(rc)}")
+
+    @staticmethod
+    def info(b: DecodeBuffers) -> dict:
+        raw = bytes(b.info.cpu().numpy().tobytes())
+        return L.FileInfo.from_buffer_copy(raw).as_dict()
+
+    def decode(self, d_file: torch.Tensor, length: int, stream=None):
+        """Size the outputs with a capacity-0 probe, then decode. Returns (buffers, info)."""
+        probe = self.alloc(0, 0)
+        self.launch(d_file, length, probe, stream)
+        torch.cuda.synchronize(self.device)
+        pi = self.info(probe)
+        if pi["status"] != L.RIO_ERR_CAPACITY:
+            return probe, pi
+        b = self.alloc(pi["n_records"], pi["total_out_bytes"])
+        self.launch(d_file, length, b, stream)
+        torch.cuda.synchronize(self.device)
+        return b, self.info(b)
+
+    def stage_ms(self):
+        ms = (ctypes.c_float * 4)()
+        n = L.lib().rio_ctx_last_stage_ms(self.ctx, ms, 4)
+        return list(ms)[:n]

@@ -1,0 +1,219 @@
+/*
+ * rio.h — C-ABI of the MI355X-native recordio v3/v4 decode path.
+ *
+ * This is the drop-in boundary a Go `recordio` adapter (behind `//go:build cgo && rocm`) binds
+ * with cgo; see INTEGRATION.md for the binding. Plain pointers and sizes only, no torch/HIP types
+ * in any signature (a HIP stream is passed as `void*`). The library never retains a caller pointer
+ * after a call returns.
+ *
+ * Reference interfaces replaced (github.com/thomasjungblut/go-sstables, paths relative to the repo):
+ *   recordio.ReaderI  {Open, Close, ReadNext, SkipNext}          recordio/recordio.go:83-89
+ *   recordio.ReadAtI  {Open, Close, Size, ReadNextAt, SeekNext}   recordio/recordio.go:91-105
+ *   NewFileReaderWithPath / NewFileReader                         recordio/file_reader.go:490-524
+ *   NewMemoryMappedReaderWithPath                                 recordio/mmap_reader.go:364-371
+ *   FileReader.ReadNext v4 / v3 (sequential whole-file semantics) recordio/file_reader.go:61-131, 389-447
+ *   MMapReader.ReadNextAt v4 / v3                                 recordio/mmap_reader.go:130-203, 298-356
+ *   MMapReader.SeekNext                                           recordio/mmap_reader.go:58-128
+ *   readFileHeaderFromBuffer                                      recordio/common_reader.go:22-44
+ *   readRecordHeaderV3 / V4 + checksumByteReader                  recordio/common_reader.go:83-151,
+ *                                                                 recordio/checksum_byte_reader.go:11-60
+ *   SnappyCompressor.DecompressWithBuf (golang/snappy v1.0.0)     recordio/compressor/snappy_compression.go:22-24
+ *   FileWriter.Write + fillRecordHeaderV4 (input generator only)  recordio/file_writer.go:160-233
+ */
+#ifndef RIO_H
+#define RIO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* Format constants (recordio/recordio.go:11-43)                                               */
+/* ------------------------------------------------------------------------------------------ */
+#define RIO_VERSION1 1u
+#define RIO_VERSION2 2u
+#define RIO_VERSION3 3u
+#define RIO_VERSION4 4u
+#define RIO_MAGIC 0x130691u /* MagicNumberSeparatorLong, uvarint bytes 91 8d 4c */
+#define RIO_FILE_HEADER_BYTES 8u
+#define RIO_RECORD_HEADER_V3_MAX 31u /* RecordHeaderV3MaxSizeBytes */
+#define RIO_RECORD_HEADER_V4_MAX 36u /* RecordHeaderV4MaxSizeBytes */
+#define RIO_COMP_NONE 0u
+#define RIO_COMP_GZIP 1u
+#define RIO_COMP_SNAPPY 2u
+#define RIO_COMP_LZW 3u
+/* Device input buffers handed to rio_device_decode must have this many readable bytes past
+ * `len` (the kernels load whole aligned 16-B words around headers; bytes past `len` are never
+ * interpreted). */
+#define RIO_DEVICE_PAD 64u
+
+/* ------------------------------------------------------------------------------------------ */
+/* Status codes: one per error class the reference's readers distinguish.                     */
+/* `rio_status_is_eof(s)` answers `errors.Is(err, io.EOF)` for the error the reference returns. */
+/* ------------------------------------------------------------------------------------------ */
+typedef enum rio_status {
+    RIO_OK = 0,
+    /* header read hit EOF before its first byte: FileReader wraps io.EOF once
+     * (file_reader.go:93), MMapReader.ReadNextAt returns a bare io.EOF (mmap_reader.go:153-155) */
+    RIO_EOF = 1,
+    /* FileReader only: magic mismatch and every byte after the consumed magic varint is zero
+     * (DirectIO padding) -> bare io.EOF (file_reader.go:76-91) */
+    RIO_EOF_ZERO_TAIL = 2,
+    /* io.EOF on the first byte of a later header field (nil byte / u / c / crc varint) */
+    RIO_EOF_HEADER = 3,
+    /* payload read classified as io.EOF: FileReader io.ReadFull read 0 bytes (file_reader.go:104-107);
+     * MMapReader any short ReadAt (mmap_reader.go:175-178) */
+    RIO_EOF_PAYLOAD = 4,
+    RIO_ERR_UNEXPECTED_EOF = 5,   /* io.ErrUnexpectedEOF (partial varint / partial payload) */
+    RIO_ERR_MAGIC = 6,            /* MagicNumberMismatchErr (common_reader.go:19) */
+    RIO_ERR_HEADER_CRC = 7,       /* HeaderChecksumMismatchErr (common_reader.go:20,140-148) */
+    RIO_ERR_VARINT_OVERFLOW = 8,  /* binary.ReadUvarint overflow */
+    RIO_ERR_HEADER_TOO_LONG = 9,  /* "checksum byte reader out of range" (checksum_byte_reader.go:25-27) */
+    RIO_ERR_DECOMPRESS = 10,      /* codec error (snappy ErrCorrupt, gzip errors) */
+    RIO_ERR_VERSION = 11,         /* "version mismatch, expected a value from 1 to 4 but was N" */
+    RIO_ERR_COMPRESSION_TYPE = 12,/* "unknown compression type [N]" */
+    RIO_ERR_SHORT_FILE_HEADER = 13,/* fewer than 8 bytes in the file */
+    RIO_ERR_INVALID_OFFSET = 14,  /* "mmap: invalid ReadAt offset N" (offset > size) */
+    RIO_ERR_UNSUPPORTED = 15,     /* valid file the GPU path does not decode (v1/v2, gzip, lzw):
+                                     the adapter keeps the reference reader for it */
+    RIO_ERR_CAPACITY = 16,        /* caller-provided output arrays too small */
+    RIO_ERR_ARG = 17,             /* bad argument */
+    RIO_ERR_HIP = 18,             /* HIP runtime failure */
+    RIO_ERR_STATE = 19,           /* reader not opened / already closed / already opened */
+    RIO_ERR_IO = 20,              /* file open / mmap / read failure */
+    RIO_STATUS_COUNT_ = 21
+} rio_status;
+
+const char* rio_strerror(int status);
+int rio_status_is_eof(int status);
+const char* rio_build_info(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Whole-file decode result.                                                                   */
+/* Sequential semantics: `n_records` records are delivered in file order, then `status`.       */
+/* A clean end is one of the RIO_EOF family. Records with index < n_records are valid even if   */
+/* status is an error: the reference's ReadNext loop returns them before the error.            */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct rio_file_info {
+    uint32_t version;         /* file header version (1..4) */
+    uint32_t compression;     /* file header compression type (0..3) */
+    uint64_t n_records;       /* records delivered before `status` */
+    uint64_t total_out_bytes; /* sum of decoded record lengths of those records */
+    int32_t status;           /* terminal status of the ReadNext loop */
+    uint32_t reserved0;
+    uint64_t status_offset;   /* file offset of the record header at which `status` was raised */
+    uint64_t detail0;         /* HEADER_CRC: expected crc; VERSION/COMPRESSION_TYPE: value */
+    uint64_t detail1;         /* HEADER_CRC: actual crc */
+    uint64_t n_chunks;        /* framing chunks used (diagnostic) */
+    uint64_t n_repairs;       /* chunks whose speculative entry had to be re-walked (diagnostic) */
+} rio_file_info;
+
+/* Per-record flag bits (rio_decode `flags`) */
+#define RIO_FLAG_NIL 0x1u /* record written as nil: ReadNext returns nil, not []byte{} */
+
+/* ------------------------------------------------------------------------------------------ */
+/* Context: one HIP device + stream + device arenas + pinned staging. NOT thread-safe: use one  */
+/* per goroutine / host thread. Independent files on different devices need no communication. */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct rio_ctx rio_ctx;
+
+int rio_ctx_create(int device, rio_ctx** out);
+void rio_ctx_destroy(rio_ctx* ctx);
+int rio_device_count(int* out);
+
+/* ---- host-memory two-phase API (the cgo binding: one call pair per file) --------------------
+ * rio_frame: H2D copy of the file through pinned staging, device framing (record boundaries,
+ * header CRC, decoded sizes) and the scan; fills `info` (sizes the caller must allocate).
+ * rio_decode: device decode of every framed record + D2H of the results into caller buffers:
+ *   out      [>= info->total_out_bytes]  concatenated record bytes
+ *   out_off  [n_records + 1]             record i = out[out_off[i] .. out_off[i+1])
+ *   rec_off  [n_records]                 file offset of record i's header (ReadNextAt offset)
+ *   flags    [n_records]                 RIO_FLAG_NIL
+ * rio_decode may lower info->n_records (a record that fails to decompress ends the sequence). */
+int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_file_info* info);
+int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, uint64_t* rec_off,
+               uint8_t* flags, uint64_t rec_cap, rio_file_info* info);
+
+/* ---- device-resident API: the file is already in HBM; everything runs on `stream` with no host
+ * synchronisation (graph-capturable). Outputs are device pointers with the layout above; the
+ * result struct is written to device memory `d_info`. `d_file` must have RIO_DEVICE_PAD readable
+ * bytes past `len`. If the decoded size exceeds out_cap or rec_cap, d_info->status is
+ * RIO_ERR_CAPACITY and nothing is decoded. `stream` is a hipStream_t (NULL = the ctx stream). */
+int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
+                      uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
+                      uint64_t rec_cap, rio_file_info* d_info, void* stream);
+/* Upper bound on records in a file of `len` bytes (smallest v3/v4 record is 6/7 bytes). */
+uint64_t rio_max_records(uint64_t len);
+/* Kernel-timing probe for benchmarks: per-stage device milliseconds of the last
+ * rio_device_decode on this ctx (frame, scan, decode); fills up to n entries, returns count. */
+int rio_ctx_last_stage_ms(rio_ctx* ctx, float* ms, int n);
+int rio_ctx_set_timing(rio_ctx* ctx, int enable);
+
+/* ---- single-record decode at an arbitrary offset (MMapReader.ReadNextAt semantics) on the
+ * device; `d_file` device-resident. The decoded record is written to `d_out` (capacity out_cap);
+ * *len_out / *nil_out / status go to host memory (this call synchronises). */
+int rio_device_read_at(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint64_t offset,
+                       uint8_t* d_out, uint64_t out_cap, uint64_t* len_out, int* nil_out,
+                       uint64_t* detail0, uint64_t* detail1);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Reader handles mirroring recordio.ReaderI / recordio.ReadAtI on top of the device path.     */
+/* Returned data pointers stay valid until the next call on the same reader (ReadNextAt,       */
+/* SeekNext) or until Close (ReadNext); the Go adapter slices/copies them into Go memory.       */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct rio_reader rio_reader;
+
+int rio_reader_new_file(rio_ctx* ctx, const char* path, rio_reader** out); /* NewFileReaderWithPath */
+int rio_reader_new_mmap(rio_ctx* ctx, const char* path, rio_reader** out); /* NewMemoryMappedReaderWithPath */
+int rio_reader_open(rio_reader* r);
+int rio_reader_close(rio_reader* r);
+void rio_reader_free(rio_reader* r);
+int rio_reader_header(rio_reader* r, uint32_t* version, uint32_t* compression);
+uint64_t rio_reader_size(rio_reader* r);
+/* detail values of the last error (HEADER_CRC: expected/actual; VERSION etc.: value) */
+void rio_reader_last_detail(rio_reader* r, uint64_t* detail0, uint64_t* detail1, uint64_t* offset);
+/* ReaderI */
+int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil);
+int rio_reader_skip_next(rio_reader* r);
+/* ReadAtI (thread-safe in the reference; here serialised per handle) */
+int rio_reader_read_next_at(rio_reader* r, uint64_t offset, const uint8_t** data, uint64_t* len,
+                            int* is_nil);
+int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, const uint8_t** data,
+                         uint64_t* len, int* is_nil);
+/* MMapReader.seekLen (mmap_reader.go:370, default 4096; tests shrink it to 10) */
+int rio_reader_set_seek_len(rio_reader* r, uint64_t seek_len);
+/* whole-file result of a file reader after its (lazy) device decode */
+int rio_reader_file_info(rio_reader* r, rio_file_info* info);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Input generator (host): byte-identical to FileWriter for v4 files (file_writer.go:160-233);   */
+/* Snappy records use a golang/snappy v1.0.0-compatible block encoder. Not on the decode path.  */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct rio_writer rio_writer;
+int rio_writer_new(const char* path, uint32_t compression, rio_writer** out);
+/* record == NULL writes a nil record; returns the record's offset in *offset */
+int rio_writer_write(rio_writer* w, const uint8_t* record, uint64_t len, uint64_t* offset);
+uint64_t rio_writer_size(rio_writer* w);
+int rio_writer_close(rio_writer* w);
+/* In-memory encoder used by the generators: appends one record to buf (capacity cap), returns
+ * bytes written or 0 if it does not fit. record == NULL => nil record. */
+uint64_t rio_encode_record_v4(uint8_t* buf, uint64_t cap, uint32_t compression,
+                              const uint8_t* record, uint64_t len);
+void rio_encode_file_header(uint8_t* buf8, uint32_t version, uint32_t compression);
+uint64_t rio_snappy_max_encoded_len(uint64_t n);
+uint64_t rio_snappy_encode(uint8_t* dst, uint64_t dst_cap, const uint8_t* src, uint64_t n);
+/* Synthetic workloads of BASELINE.json. Writes a complete v4 file
+ * image into buf; returns its length (0 if cap too small). kind: 0 = ref-random (one record of
+ * bytes in [0,254] repeated, benchmark/recordio_read_test.go:32-42), 1 = text-like (seeded
+ * Zipf words, distinct per record), 2 = random bytes distinct per record. */
+uint64_t rio_generate(uint8_t* buf, uint64_t cap, uint32_t compression, uint64_t n_records,
+                      uint64_t record_len, int kind, uint64_t seed, int threads);
+uint64_t rio_generate_bound(uint32_t compression, uint64_t n_records, uint64_t record_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RIO_H */

@@ -1,0 +1,556 @@
+/*
+ * rio_oracle.c — CPU restatement of github.com/thomasjungblut/go-sstables recordio decode
+ * semantics. TEST INFRASTRUCTURE ONLY (see rio_oracle.h): the parity checker for the HIP path and
+ * the "port" CPU baseline of bench.py. Never linked into the product library.
+ *
+ * Every function cites the reference file:line it restates. Third-party algorithms restated here
+ * (their code is not under /root/reference):
+ *   - Go stdlib encoding/binary ReadUvarint / Uvarint (go 1.25, go.mod:27): LEB128, <=10 bytes,
+ *     10th byte must be <= 1, io.EOF on 0 bytes, io.ErrUnexpectedEOF on a partial varint.
+ *   - Go stdlib hash/crc32 Castagnoli (reflected poly 0x82F63B78, init/xorout 0xFFFFFFFF).
+ *   - github.com/golang/snappy v1.0.0 (go.mod:6) block decoder (decode.go, decode_other.go).
+ *   - golang.org/x/exp/mmap ReaderAt.ReadAt bounds semantics (go.mod:10).
+ *   - Go stdlib compress/gzip reader via zlib (multistream, CRC-32 + ISIZE verified).
+ */
+#include "rio_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#include "../include/rio.h"
+
+/* ---------------------------------------------------------------------------------------- */
+/* CRC-32C (hash/crc32 MakeTable(Castagnoli)); used by checksum_byte_reader.go:44-50          */
+/* ---------------------------------------------------------------------------------------- */
+static uint32_t crc_tab[256];
+static int crc_ready = 0;
+
+static void crc_init(void) {
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+        crc_tab[i] = c;
+    }
+    crc_ready = 1;
+}
+
+uint32_t orc_crc32c(const uint8_t* p, uint64_t n) {
+    if (!crc_ready) crc_init();
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint64_t i = 0; i < n; i++) c = crc_tab[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    return c ^ 0xFFFFFFFFu;
+}
+
+void orc_free(void* p) { free(p); }
+
+/* ---------------------------------------------------------------------------------------- */
+/* io.ByteReader over a byte window, optionally teed through checksumByteReader's cache.      */
+/* checksum_byte_reader.go:19-33: the underlying ReadByte error (io.EOF) wins; then the cache  */
+/* bound check raises "checksum byte reader out of range".                                    */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t* p;
+    uint64_t avail; /* bytes the underlying reader can deliver */
+    uint64_t pos;
+    uint64_t cap; /* checksum cache size; UINT64_MAX = no checksum reader */
+} brd;
+
+static int brd_byte(brd* r, uint8_t* b) {
+    if (r->pos >= r->avail) return RIO_EOF;
+    if (r->pos >= r->cap) { r->pos++; return RIO_ERR_HEADER_TOO_LONG; }
+    *b = r->p[r->pos++];
+    return RIO_OK;
+}
+
+/* encoding/binary.ReadUvarint */
+static int go_read_uvarint(brd* r, uint64_t* x) {
+    uint64_t v = 0;
+    unsigned s = 0;
+    for (int i = 0; i < 10; i++) {
+        uint8_t b;
+        int e = brd_byte(r, &b);
+        if (e) {
+            if (e == RIO_EOF && i > 0) return RIO_ERR_UNEXPECTED_EOF;
+            return e;
+        }
+        if (b < 0x80) {
+            if (i == 9 && b > 1) return RIO_ERR_VARINT_OVERFLOW;
+            *x = v | ((uint64_t)b << s);
+            return RIO_OK;
+        }
+        v |= (uint64_t)(b & 0x7F) << s;
+        s += 7;
+    }
+    return RIO_ERR_VARINT_OVERFLOW;
+}
+
+/* encoding/binary.Uvarint: returns n>0 bytes read, 0 if buf too small, <0 on overflow */
+static int go_uvarint(const uint8_t* buf, uint64_t len, uint64_t* x) {
+    uint64_t v = 0;
+    unsigned s = 0;
+    for (uint64_t i = 0; i < len; i++) {
+        if (i == 10) return -(int)(i + 1);
+        uint8_t b = buf[i];
+        if (b < 0x80) {
+            if (i == 9 && b > 1) return -(int)(i + 1);
+            *x = v | ((uint64_t)b << s);
+            return (int)(i + 1);
+        }
+        v |= (uint64_t)(b & 0x7F) << s;
+        s += 7;
+    }
+    return 0;
+}
+
+/* a header field after the magic that hits io.EOF on its first byte returns io.EOF unchanged;
+ * we tag it RIO_EOF_HEADER to keep "EOF at a record boundary" distinguishable. */
+static int later_field(int e) { return e == RIO_EOF ? RIO_EOF_HEADER : e; }
+
+typedef struct {
+    uint64_t u, c;
+    int nil;
+    uint64_t hdr_len;
+    uint64_t magic_len; /* bytes consumed by the magic varint (for the zero-tail check) */
+    uint64_t exp_crc, act_crc;
+} hdr_t;
+
+/* readRecordHeaderV4 (common_reader.go:110-151) */
+static int read_header_v4(brd* r, hdr_t* h) {
+    uint64_t m = 0;
+    int e = go_read_uvarint(r, &m);
+    h->magic_len = r->pos;
+    if (e) return e;
+    if (m != RIO_MAGIC) return RIO_ERR_MAGIC;
+    uint8_t nb;
+    e = brd_byte(r, &nb);
+    if (e) return later_field(e);
+    e = go_read_uvarint(r, &h->u);
+    if (e) return later_field(e);
+    e = go_read_uvarint(r, &h->c);
+    if (e) return later_field(e);
+    /* checksumByteReader.Checksum over bytes cached so far (checksum_byte_reader.go:44-50) */
+    h->act_crc = orc_crc32c(r->p, r->pos);
+    e = go_read_uvarint(r, &h->exp_crc);
+    if (e) return later_field(e);
+    if (h->act_crc != h->exp_crc) return RIO_ERR_HEADER_CRC;
+    h->nil = (nb == 1);
+    h->hdr_len = r->pos;
+    return RIO_OK;
+}
+
+/* readRecordHeaderV3 (common_reader.go:83-108) */
+static int read_header_v3(brd* r, hdr_t* h) {
+    uint64_t m = 0;
+    int e = go_read_uvarint(r, &m);
+    h->magic_len = r->pos;
+    if (e) return e;
+    if (m != RIO_MAGIC) return RIO_ERR_MAGIC;
+    uint8_t nb;
+    e = brd_byte(r, &nb);
+    if (e) return later_field(e);
+    e = go_read_uvarint(r, &h->u);
+    if (e) return later_field(e);
+    e = go_read_uvarint(r, &h->c);
+    if (e) return later_field(e);
+    h->nil = (nb == 1);
+    h->hdr_len = r->pos;
+    return RIO_OK;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* golang/snappy v1.0.0 Decode(dst, src): decodedLen (binary.Uvarint, >0xffffffff => ErrCorrupt) */
+/* then decode() with its bounds checks; output length = the preamble, not the header's u.     */
+/* ---------------------------------------------------------------------------------------- */
+int orc_snappy_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len) {
+    uint64_t dlen = 0;
+    int k = go_uvarint(src, n, &dlen);
+    *out = NULL;
+    *out_len = 0;
+    if (k <= 0 || dlen > 0xFFFFFFFFull) return RIO_ERR_DECOMPRESS;
+    /* a stream of m bytes yields at most 64 bytes per 3 (tagCopy2): larger preambles cannot
+     * decode (d != len(dst) at the end); refuse before allocating */
+    if (dlen > 22ull * (n - (uint64_t)k) + 64) return RIO_ERR_DECOMPRESS;
+    uint8_t* dst = (uint8_t*)malloc(dlen ? dlen : 1);
+    const uint8_t* s0 = src + k;
+    int64_t slen = (int64_t)(n - (uint64_t)k), s = 0, d = 0, dl = (int64_t)dlen;
+    int64_t offset = 0, length = 0;
+    while (s < slen) {
+        switch (s0[s] & 3) {
+        case 0: { /* tagLiteral */
+            uint32_t x = s0[s] >> 2;
+            if (x < 60) {
+                s++;
+            } else if (x == 60) {
+                s += 2;
+                if (s > slen) goto corrupt;
+                x = s0[s - 1];
+            } else if (x == 61) {
+                s += 3;
+                if (s > slen) goto corrupt;
+                x = (uint32_t)s0[s - 2] | (uint32_t)s0[s - 1] << 8;
+            } else if (x == 62) {
+                s += 4;
+                if (s > slen) goto corrupt;
+                x = (uint32_t)s0[s - 3] | (uint32_t)s0[s - 2] << 8 | (uint32_t)s0[s - 1] << 16;
+            } else {
+                s += 5;
+                if (s > slen) goto corrupt;
+                x = (uint32_t)s0[s - 4] | (uint32_t)s0[s - 3] << 8 | (uint32_t)s0[s - 2] << 16 |
+                    (uint32_t)s0[s - 1] << 24;
+            }
+            length = (int64_t)x + 1;
+            if (length > dl - d || length > slen - s) goto corrupt;
+            memcpy(dst + d, s0 + s, (size_t)length);
+            d += length;
+            s += length;
+            continue;
+        }
+        case 1: /* tagCopy1 */
+            s += 2;
+            if (s > slen) goto corrupt;
+            length = 4 + ((s0[s - 2] >> 2) & 7);
+            offset = (int64_t)(((uint32_t)s0[s - 2] & 0xE0) << 3 | (uint32_t)s0[s - 1]);
+            break;
+        case 2: /* tagCopy2 */
+            s += 3;
+            if (s > slen) goto corrupt;
+            length = 1 + (s0[s - 3] >> 2);
+            offset = (int64_t)((uint32_t)s0[s - 2] | (uint32_t)s0[s - 1] << 8);
+            break;
+        default: /* tagCopy4 */
+            s += 5;
+            if (s > slen) goto corrupt;
+            length = 1 + (s0[s - 5] >> 2);
+            offset = (int64_t)((uint32_t)s0[s - 4] | (uint32_t)s0[s - 3] << 8 |
+                               (uint32_t)s0[s - 2] << 16 | (uint32_t)s0[s - 1] << 24);
+            break;
+        }
+        if (offset <= 0 || d < offset || length > dl - d) goto corrupt;
+        /* forward byte copy: overlapping copies replicate the pattern (decode_other.go) */
+        for (int64_t i = 0; i < length; i++) dst[d + i] = dst[d - offset + i];
+        d += length;
+    }
+    if (d != dl) goto corrupt;
+    *out = dst;
+    *out_len = dlen;
+    return RIO_OK;
+corrupt:
+    free(dst);
+    return RIO_ERR_DECOMPRESS;
+}
+
+/* GzipCompressor.DecompressWithBuf (gzip_compression.go:54-69): gzip.NewReader (multistream)
+ * + ReadFrom. zlib restatement; parity pinned only by the _comp1 fixture. */
+static int gzip_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len) {
+    *out = NULL;
+    *out_len = 0;
+    if (n == 0) return RIO_ERR_DECOMPRESS; /* gzip.NewReader(empty) -> io.EOF */
+    uint64_t cap = n * 4 + 64, used = 0;
+    uint8_t* dst = (uint8_t*)malloc(cap);
+    z_stream z;
+    memset(&z, 0, sizeof z);
+    if (inflateInit2(&z, 16 + 15) != Z_OK) { free(dst); return RIO_ERR_DECOMPRESS; }
+    z.next_in = (Bytef*)src;
+    z.avail_in = (uInt)n;
+    for (;;) {
+        if (used == cap) {
+            cap *= 2;
+            dst = (uint8_t*)realloc(dst, cap);
+        }
+        z.next_out = dst + used;
+        z.avail_out = (uInt)(cap - used);
+        int rc = inflate(&z, Z_NO_FLUSH);
+        used = cap - z.avail_out;
+        if (rc == Z_STREAM_END) {
+            if (z.avail_in == 0) break;
+            inflateReset(&z); /* next gzip member (multistream) */
+            continue;
+        }
+        if (rc == Z_OK) continue;
+        if (rc == Z_BUF_ERROR && z.avail_out == 0) continue;
+        inflateEnd(&z);
+        free(dst);
+        return RIO_ERR_DECOMPRESS;
+    }
+    inflateEnd(&z);
+    *out = dst;
+    *out_len = used;
+    return RIO_OK;
+}
+
+static int decompress(uint32_t comp, const uint8_t* src, uint64_t n, uint8_t** out,
+                      uint64_t* out_len) {
+    if (comp == RIO_COMP_SNAPPY) return orc_snappy_decode(src, n, out, out_len);
+    if (comp == RIO_COMP_GZIP) return gzip_decode(src, n, out, out_len);
+    return RIO_ERR_UNSUPPORTED; /* lzw: no fixture, parity unpinned, not restated */
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* readFileHeaderFromBuffer (common_reader.go:22-44); short files: io.ReadFull in Open         */
+/* ---------------------------------------------------------------------------------------- */
+int orc_file_header(const uint8_t* f, uint64_t len, uint32_t* version, uint32_t* compression,
+                    uint64_t* detail) {
+    *detail = 0;
+    if (len < RIO_FILE_HEADER_BYTES) return RIO_ERR_SHORT_FILE_HEADER;
+    uint32_t v = (uint32_t)f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+    uint32_t c = (uint32_t)f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+    *version = v;
+    *compression = c;
+    if (v > RIO_VERSION4 || v < RIO_VERSION1) { *detail = v; return RIO_ERR_VERSION; }
+    if (c > RIO_COMP_LZW) { *detail = c; return RIO_ERR_COMPRESSION_TYPE; }
+    return RIO_OK;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* FileReader: Open + ReadNext loop (file_reader.go:26-131 v4, 389-447 v3)                    */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct {
+    uint8_t* out;
+    uint64_t out_len, out_cap;
+    uint64_t *out_off, *rec_off;
+    uint8_t* flags;
+    uint64_t n, cap;
+} arena_t;
+
+static void arena_push(arena_t* a, uint64_t rec_off, const uint8_t* data, uint64_t len, int nil) {
+    if (a->n + 1 >= a->cap) {
+        a->cap = a->cap ? a->cap * 2 : 1024;
+        a->out_off = (uint64_t*)realloc(a->out_off, (a->cap + 1) * sizeof(uint64_t));
+        a->rec_off = (uint64_t*)realloc(a->rec_off, a->cap * sizeof(uint64_t));
+        a->flags = (uint8_t*)realloc(a->flags, a->cap);
+    }
+    if (a->out_len + len > a->out_cap) {
+        uint64_t nc = a->out_cap ? a->out_cap * 2 : 4096;
+        while (nc < a->out_len + len) nc *= 2;
+        a->out = (uint8_t*)realloc(a->out, nc);
+        a->out_cap = nc;
+    }
+    a->out_off[a->n] = a->out_len;
+    a->rec_off[a->n] = rec_off;
+    a->flags[a->n] = nil ? RIO_FLAG_NIL : 0;
+    if (len) memcpy(a->out + a->out_len, data, len);
+    a->out_len += len;
+    a->n++;
+    a->out_off[a->n] = a->out_len;
+}
+
+int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res) {
+    memset(res, 0, sizeof *res);
+    int e = orc_file_header(f, len, &res->version, &res->compression, &res->detail0);
+    if (e) { res->status = e; return e; }
+    if (res->version < RIO_VERSION3) { res->status = RIO_ERR_UNSUPPORTED; return RIO_ERR_UNSUPPORTED; }
+    arena_t a;
+    memset(&a, 0, sizeof a);
+    a.out_off = (uint64_t*)calloc(1, sizeof(uint64_t));
+    uint64_t p = RIO_FILE_HEADER_BYTES;
+    int status = RIO_OK;
+    for (;;) {
+        brd r = {f + p, len - p, 0, res->version == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : UINT64_MAX};
+        hdr_t h;
+        memset(&h, 0, sizeof h);
+        e = res->version == RIO_VERSION4 ? read_header_v4(&r, &h) : read_header_v3(&r, &h);
+        if (e) {
+            if (e == RIO_ERR_MAGIC) {
+                /* io.ReadAll of the remainder after the consumed magic varint; all zeros => EOF */
+                int zero = 1;
+                for (uint64_t q = p + h.magic_len; q < len; q++)
+                    if (f[q]) { zero = 0; break; }
+                e = zero ? RIO_EOF_ZERO_TAIL : RIO_ERR_MAGIC;
+            }
+            if (e == RIO_ERR_HEADER_CRC) { res->detail0 = h.exp_crc; res->detail1 = h.act_crc; }
+            status = e;
+            break;
+        }
+        if (h.nil) { /* file_reader.go:96-99: nil ⇒ no payload, whatever c says */
+            arena_push(&a, p, NULL, 0, 1);
+            p += h.hdr_len;
+            continue;
+        }
+        uint64_t plen = res->compression != RIO_COMP_NONE ? h.c : h.u; /* common_reader.go:162-169 */
+        uint64_t avail = len - p - h.hdr_len;
+        if (plen > avail) { /* io.ReadFull: 0 bytes => io.EOF, partial => ErrUnexpectedEOF */
+            status = (avail == 0) ? RIO_EOF_PAYLOAD : RIO_ERR_UNEXPECTED_EOF;
+            break;
+        }
+        const uint8_t* pay = f + p + h.hdr_len;
+        if (res->compression != RIO_COMP_NONE) {
+            uint8_t* dec = NULL;
+            uint64_t dlen = 0;
+            e = decompress(res->compression, pay, plen, &dec, &dlen);
+            if (e) { status = e; break; }
+            arena_push(&a, p, dec, dlen, 0);
+            free(dec);
+        } else {
+            arena_push(&a, p, pay, plen, 0);
+        }
+        p += h.hdr_len + plen;
+    }
+    res->status = status;
+    res->status_offset = p;
+    res->n_records = a.n;
+    res->total_out_bytes = a.out_len;
+    res->out = a.out;
+    res->out_off = a.out_off;
+    res->rec_off = a.rec_off;
+    res->flags = a.flags;
+    return RIO_OK;
+}
+
+void orc_file_result_free(orc_file_result* res) {
+    free(res->out);
+    free(res->out_off);
+    free(res->rec_off);
+    free(res->flags);
+    memset(res, 0, sizeof *res);
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* MMapReader.ReadNextAt (mmap_reader.go:130-203 v4; readNextAtV3 :298-356)                  */
+/* ---------------------------------------------------------------------------------------- */
+int orc_read_next_at(const uint8_t* f, uint64_t len, uint64_t offset, uint8_t** out,
+                     uint64_t* out_len, int* is_nil, uint64_t* detail0, uint64_t* detail1) {
+    uint32_t ver, comp;
+    uint64_t det;
+    *out = NULL;
+    *out_len = 0;
+    *is_nil = 0;
+    *detail0 = *detail1 = 0;
+    int e = orc_file_header(f, len, &ver, &comp, &det);
+    if (e) return e;
+    if (ver < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
+    /* x/exp/mmap ReadAt: off > len => "mmap: invalid ReadAt offset"; 0 bytes => bare io.EOF */
+    if (offset > len) return RIO_ERR_INVALID_OFFSET;
+    uint64_t wmax = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : RIO_RECORD_HEADER_V3_MAX;
+    uint64_t w = len - offset < wmax ? len - offset : wmax;
+    if (w == 0) return RIO_EOF;
+    brd r = {f + offset, w, 0, ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : UINT64_MAX};
+    hdr_t h;
+    memset(&h, 0, sizeof h);
+    e = ver == RIO_VERSION4 ? read_header_v4(&r, &h) : read_header_v3(&r, &h);
+    if (e == RIO_EOF) e = RIO_EOF_HEADER; /* wrapped: "failed reading record header at offset" */
+    if (e == RIO_ERR_HEADER_CRC) { *detail0 = h.exp_crc; *detail1 = h.act_crc; }
+    if (e) return e;
+    if (h.nil) { *is_nil = 1; return RIO_OK; }
+    uint64_t plen = comp != RIO_COMP_NONE ? h.c : h.u;
+    if (plen > len - offset - h.hdr_len) return RIO_EOF_PAYLOAD; /* short ReadAt => io.EOF */
+    const uint8_t* pay = f + offset + h.hdr_len;
+    if (comp != RIO_COMP_NONE) return decompress(comp, pay, plen, out, out_len);
+    *out = (uint8_t*)malloc(plen ? plen : 1);
+    if (plen) memcpy(*out, pay, plen);
+    *out_len = plen;
+    return RIO_OK;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* MMapReader.SeekNext (mmap_reader.go:58-128): windowed scan for the bytes 91 8d 4c, trial    */
+/* ReadNextAt at each hit; header-CRC / magic / io.EOF-class failures continue the scan.      */
+/* ---------------------------------------------------------------------------------------- */
+int orc_seek_next(const uint8_t* f, uint64_t len, uint64_t offset, uint64_t seek_len,
+                  uint64_t* rec_offset, uint8_t** out, uint64_t* out_len, int* is_nil) {
+    static const uint8_t M[3] = {0x91, 0x8D, 0x4C};
+    uint32_t ver, comp;
+    uint64_t det, d0, d1;
+    *out = NULL;
+    *out_len = 0;
+    *is_nil = 0;
+    *rec_offset = 0;
+    int e = orc_file_header(f, len, &ver, &comp, &det);
+    if (e) return e;
+    if (ver < RIO_VERSION2) return RIO_ERR_UNSUPPORTED; /* :62-64 */
+    if (ver < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
+    if (seek_len == 0) seek_len = 4096;
+    uint64_t next = offset;
+    for (;;) {
+        if (next > len) return RIO_ERR_INVALID_OFFSET;
+        uint64_t num = len - next < seek_len ? len - next : seek_len;
+        if (num == 0) return RIO_EOF;
+        const uint8_t* buf = f + next;
+        uint64_t i = 0;
+        int boundary = 0;
+        while (i < num) {
+            uint64_t ix = i;
+            for (int j = 0; j < 3; j++) {
+                if (buf[ix] != M[j]) break;
+                ix++;
+                if (ix >= num) { boundary = 1; break; }
+            }
+            if (boundary) break;
+            if (ix - i < 3) { i = ix + 1; continue; }
+            uint64_t trial = next + i;
+            uint8_t* rec = NULL;
+            uint64_t rl = 0;
+            int nil = 0;
+            e = orc_read_next_at(f, len, trial, &rec, &rl, &nil, &d0, &d1);
+            if (e) {
+                if (e == RIO_ERR_HEADER_CRC || e == RIO_ERR_MAGIC || rio_status_is_eof(e)) {
+                    i = ix;
+                    continue;
+                }
+                return e;
+            }
+            *rec_offset = trial;
+            *out = rec;
+            *out_len = rl;
+            *is_nil = nil;
+            return RIO_OK;
+        }
+        if (i == 0) return RIO_EOF; /* :121-124 */
+        next += i;
+    }
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* CPU baseline helper: record-parallel ReadNextAt over known offsets (pthreads)              */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t* f;
+    uint64_t len;
+    const uint64_t* off;
+    uint64_t lo, hi;
+    uint64_t bytes;
+    int err;
+} par_arg;
+
+static void* par_worker(void* vp) {
+    par_arg* a = (par_arg*)vp;
+    for (uint64_t i = a->lo; i < a->hi; i++) {
+        uint8_t* o = NULL;
+        uint64_t ol = 0, d0, d1;
+        int nil = 0;
+        int e = orc_read_next_at(a->f, a->len, a->off[i], &o, &ol, &nil, &d0, &d1);
+        if (e) a->err = e;
+        a->bytes += ol;
+        free(o);
+    }
+    return NULL;
+}
+
+uint64_t orc_parallel_read_at(const uint8_t* f, uint64_t len, const uint64_t* rec_off, uint64_t n,
+                              int threads) {
+    if (threads <= 0) threads = 1;
+    if (!crc_ready) crc_init();
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    par_arg* args = (par_arg*)calloc((size_t)threads, sizeof(par_arg));
+    for (int t = 0; t < threads; t++) {
+        args[t] = (par_arg){f, len, rec_off, n * (uint64_t)t / threads, n * (uint64_t)(t + 1) / threads, 0, 0};
+        pthread_create(&th[t], NULL, par_worker, &args[t]);
+    }
+    uint64_t total = 0;
+    int err = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        total += args[t].bytes;
+        if (args[t].err) err = 1;
+    }
+    free(th);
+    free(args);
+    return err ? 0 : total;
+}
+
+/* status helpers shared with the product's vocabulary (rio.h); the oracle keeps its own copy so
+ * the library under test is never linked into the checker. */
+int rio_status_is_eof(int s) {
+    return s == RIO_EOF || s == RIO_EOF_ZERO_TAIL || s == RIO_EOF_HEADER || s == RIO_EOF_PAYLOAD;
+}

@@ -1,0 +1,58 @@
+/*
+ * rio_oracle.h — CPU restatement of the reference recordio readers (TEST INFRASTRUCTURE ONLY).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+ * It is the parity checker and the CPU baseline ("kind": "port"); it is never on the product path.
+ *
+ * Parity pinning: checked against every reference fixture under tests/golden/v{3,4}_compat (copied
+ * data files of recordio/test_files) and the expectations the reference's own tests assert
+ * (tests/golden/expectations.json, tests/test_oracle_golden.py). The Go reference cannot be built
+ * here (no Go toolchain), so the fixtures + test assertions are the pin.
+ * Status vocabulary: include/rio.h.
+ */
+#ifndef RIO_ORACLE_H
+#define RIO_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_file_result {
+    uint32_t version, compression;
+    uint64_t n_records;
+    uint64_t total_out_bytes;
+    int32_t status;
+    uint64_t status_offset;
+    uint64_t detail0, detail1;
+    uint8_t* out;       /* malloc'd, total_out_bytes */
+    uint64_t* out_off;  /* malloc'd, n_records + 1 */
+    uint64_t* rec_off;  /* malloc'd, n_records */
+    uint8_t* flags;     /* malloc'd, n_records */
+} orc_file_result;
+
+uint32_t orc_crc32c(const uint8_t* p, uint64_t n);
+/* readFileHeaderFromBuffer (common_reader.go:22-44) on the first 8 bytes */
+int orc_file_header(const uint8_t* f, uint64_t len, uint32_t* version, uint32_t* compression,
+                    uint64_t* detail);
+/* FileReader Open + ReadNext loop until the first non-nil error (file_reader.go:26-131, 389-447) */
+int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res);
+void orc_file_result_free(orc_file_result* res);
+/* MMapReader.ReadNextAt (mmap_reader.go:130-203 v4, 298-356 v3). *out is malloc'd (NULL for nil). */
+int orc_read_next_at(const uint8_t* f, uint64_t len, uint64_t offset, uint8_t** out,
+                     uint64_t* out_len, int* is_nil, uint64_t* detail0, uint64_t* detail1);
+/* MMapReader.SeekNext (mmap_reader.go:58-128) with window seek_len (4096 by default, :370) */
+int orc_seek_next(const uint8_t* f, uint64_t len, uint64_t offset, uint64_t seek_len,
+                  uint64_t* rec_offset, uint8_t** out, uint64_t* out_len, int* is_nil);
+/* snappy.Decode of golang/snappy v1.0.0 (decode.go + decode_other.go). *out malloc'd. */
+int orc_snappy_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len);
+void orc_free(void* p);
+/* multi-threaded CPU baseline: record-parallel ReadNextAt over a known offset table; returns
+ * decoded bytes (0 on error). threads <= 0 => 1. */
+uint64_t orc_parallel_read_at(const uint8_t* f, uint64_t len, const uint64_t* rec_off, uint64_t n,
+                              int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

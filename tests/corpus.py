@@ -1,0 +1,168 @@
+"""Crafted recordio files for parity tests: workloads, edge cases and corruptions.
+
+Every case is decoded by the oracle (the checker) and by the device path; the tests compare the
+two bit-exactly. Builders only produce bytes; nothing here decodes.
+"""
+import random
+import struct
+
+from recordio import encode_file, generate
+
+
+def uvarint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def padded_uvarint(v: int, n: int) -> bytes:
+    """Non-canonical n-byte encoding of v (legal for Go's ReadUvarint)."""
+    b = bytearray()
+    for i in range(n):
+        last = i == n - 1
+        b.append((v & 0x7F) | (0 if last else 0x80))
+        v >>= 7
+    return bytes(b)
+
+
+def crc32c(b: bytes) -> int:
+    c = 0xFFFFFFFF
+    for x in b:
+        c ^= x
+        for _ in range(8):
+            c = (c >> 1) ^ (0x82F63B78 & -(c & 1))
+    return c ^ 0xFFFFFFFF
+
+
+def header_v4(u, c, nil=False, magic=b"\x91\x8d\x4c", u_bytes=None, c_bytes=None, crc_bytes=None):
+    pre = magic + bytes([1 if nil else 0]) + (u_bytes or uvarint(u)) + (c_bytes or uvarint(c))
+    return pre + (crc_bytes if crc_bytes is not None else uvarint(crc32c(pre)))
+
+
+def header_v3(u, c, nil=False, magic=b"\x91\x8d\x4c"):
+    return magic + bytes([1 if nil else 0]) + uvarint(u) + uvarint(c)
+
+
+def file_header(version=4, comp=0):
+    return struct.pack("<II", version, comp)
+
+
+def v3_file(records, comp=0):
+    """v3 image (no CRC) — uncompressed or snappy payloads (file_writer.go writeRecordHeaderV3)."""
+    from recordio import _lib as L
+    import ctypes
+
+    out = bytearray(file_header(3, comp))
+    for r in records:
+        if r is None:
+            c = 1 if comp == 2 else 0
+            out += header_v3(0, c, nil=True)
+            continue
+        if comp == 2:
+            cap = int(L.lib().rio_snappy_max_encoded_len(len(r)))
+            buf = ctypes.create_string_buffer(cap + 1)
+            n = L.lib().rio_snappy_encode(buf, cap, ctypes.c_char_p(bytes(r) or b"\0"), len(r))
+            pay = buf.raw[:n]
+            out += header_v3(len(r), len(pay)) + pay
+        else:
+            out += header_v3(len(r), 0) + bytes(r)
+    return bytes(out)
+
+
+def mixed_records(n, seed, max_len=3000, nil_frac=0.05):
+    rng = random.Random(seed)
+    recs = []
+    for i in range(n):
+        if rng.random() < nil_frac:
+            recs.append(None)
+            continue
+        L = rng.choice([0, 1, 2, 3, 7, 15, 16, 17, 63, 64, 65, rng.randint(0, max_len)])
+        if rng.random() < 0.5:
+            recs.append(bytes(rng.getrandbits(8) for _ in range(L)))
+        else:
+            words = [b"alpha", b"beta", b"gamma", b"delta", b"\x91\x8d\x4c", b"zz"]
+            s = b" ".join(rng.choice(words) for _ in range(L // 4 + 1))
+            recs.append(s[:L])
+    return recs
+
+
+def embedded_file_records(n, seed):
+    """Records whose payloads are themselves valid recordio files: every chunk start inside them
+    finds CRC-valid speculative headers that are not on the true chain (forces repairs)."""
+    rng = random.Random(seed)
+    inner = encode_file([bytes([rng.getrandbits(8)]) * rng.randint(1, 40) for _ in range(600)], 0)
+    return [inner[8:] if i % 2 == 0 else b"x" * rng.randint(0, 50) for i in range(n)]
+
+
+def cases():
+    """(name, image) pairs covering the edge cases the reference's tests and code paths define."""
+    out = []
+    asc = lambda n: bytes(i & 0xFF for i in range(n))  # noqa: E731
+    out.append(("empty_file_header_only", file_header()))
+    out.append(("short_file_4_bytes", b"\x04\x00\x00\x00"))
+    out.append(("asc_none", encode_file([asc(i) for i in range(300)], 0)))
+    out.append(("asc_snappy", encode_file([asc(i) for i in range(300)], 2)))
+    for comp in (0, 2):
+        recs = mixed_records(2500, 11 + comp)
+        img = encode_file(recs, comp)
+        out.append((f"mixed_c{comp}", img))
+        # truncations: inside a header, at a payload start, inside a payload, at a record boundary
+        rng = random.Random(comp)
+        for k in range(6):
+            cut = rng.randint(9, len(img) - 1)
+            out.append((f"mixed_c{comp}_trunc{k}", img[:cut]))
+        # flip one CRC byte of a record in the middle (v4 header CRC mismatch)
+        b = bytearray(img)
+        pos = img.index(b"\x91\x8d\x4c", len(img) // 2)
+        b[pos + 5] ^= 0x01
+        out.append((f"mixed_c{comp}_flip", bytes(b)))
+        # zero tail (DirectIO padding) short and long; non-zero garbage after zeros
+        out.append((f"mixed_c{comp}_zero_tail", img + bytes(4096 * 3 + 5)))
+        out.append((f"mixed_c{comp}_garbage_tail", img + bytes(5000) + b"\xb9\x0a" + bytes(10)))
+        out.append((f"mixed_c{comp}_one_byte_tail", img + b"\x07"))
+        out.append((f"mixed_c{comp}_partial_magic_tail", img + b"\x91\x8d"))
+        out.append((f"mixed_c{comp}_embedded", encode_file(embedded_file_records(40, 5 + comp), comp)))
+    # non-canonical magic / varints in a record on the chain (entry speculation cannot see it)
+    pay = b"hello-noncanonical"
+    h = header_v4(len(pay), 0, magic=b"\x91\x8d\xcc\x00", u_bytes=padded_uvarint(len(pay), 3))
+    body = encode_file([asc(100)] * 60, 0)
+    out.append(("noncanonical_magic", body + h + pay + encode_file([b"after"] * 50, 0)[8:]))
+    # header longer than the 36-byte checksum cache
+    long_pre = padded_uvarint(0x130691, 10) + b"\x00" + padded_uvarint(1, 10) + padded_uvarint(0, 10)
+    long_h = long_pre + padded_uvarint(crc32c(long_pre), 6)
+    out.append(("header_too_long", body + long_h + b"Z"))
+    out.append(("header_36_exact", body + long_pre + padded_uvarint(crc32c(long_pre), 5) + b"Z"))
+    # varint overflow in the magic / size fields
+    out.append(("magic_overflow", body + b"\xff" * 10 + b"\x01" * 20))
+    out.append(("size_overflow", body + b"\x91\x8d\x4c\x00" + b"\xff" * 9 + b"\x02" + b"\x00" * 20))
+    # corrupt snappy: bad copy offset in a record in the middle, and a huge preamble
+    recs = [b"abcdefgh" * 20 for _ in range(50)]
+    img = bytearray(encode_file(recs, 2))
+    p = img.index(b"\x91\x8d\x4c", len(img) // 2)
+    hl = len(header_v4(160, img[p + 6]))  # u = 160 takes two varint bytes; c follows
+    img[p + hl + 2] = 0x01  # first element after preamble/literal tag: turn into a copy with offset 0
+    out.append(("snappy_corrupt_mid", bytes(img)))
+    pre = uvarint(5000) + b"\x00a"
+    out.append(("snappy_huge_preamble", encode_file([b"ok"] * 3, 2) + header_v4(5000, len(pre)) + pre))
+    out.append(("snappy_empty_payload", encode_file([b"ok"] * 3, 2) + header_v4(0, 0)))
+    # nil records in a compressed file with c != 0 (file_writer.go:198-219)
+    out.append(("nil_snappy", encode_file([None, b"a", None, None, b"", b"bb"] * 100, 2)))
+    # payload length beyond the file (the reference would panic in bufferPool.Get; we report EOF)
+    out.append(("huge_u", body + header_v4(1 << 40, 0) + b"abc"))
+    # v3 files
+    out.append(("v3_mixed_none", v3_file(mixed_records(1500, 3), 0)))
+    out.append(("v3_mixed_snappy", v3_file(mixed_records(1500, 4), 2)))
+    v3 = v3_file(mixed_records(800, 9), 0)
+    out.append(("v3_zero_tail", v3 + bytes(9000)))
+    out.append(("v3_trunc", v3[: len(v3) - 7]))
+    # larger synthetic workloads (several chunks / blocks)
+    out.append(("text_snappy_1k", generate(3000, 1024, 2, kind=1, seed=1).tobytes()))
+    out.append(("random_snappy_1k", generate(2000, 1024, 2, kind=2, seed=2).tobytes()))
+    out.append(("refrandom_none_1k", generate(3000, 1024, 0, kind=0, seed=3).tobytes()))
+    out.append(("text_snappy_64", generate(40000, 64, 2, kind=1, seed=4).tobytes()))
+    out.append(("text_snappy_64k", generate(40, 65536, 2, kind=1, seed=5).tobytes()))
+    out.append(("random_none_64k", generate(30, 65536, 0, kind=2, seed=6).tobytes()))
+    return out

@@ -1,0 +1,134 @@
+"""ctypes binding of the oracle (oracle/librio_oracle.so) — test infrastructure only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, byref, c_int, c_uint8, c_uint32, c_uint64, c_void_p
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(REPO, "oracle", "librio_oracle.so")
+
+
+class OrcFileResult(ctypes.Structure):
+    _fields_ = [
+        ("version", c_uint32), ("compression", c_uint32), ("n_records", c_uint64), ("total_out_bytes", c_uint64),
+        ("status", ctypes.c_int32), ("status_offset", c_uint64), ("detail0", c_uint64), ("detail1", c_uint64),
+        ("out", POINTER(c_uint8)), ("out_off", POINTER(c_uint64)), ("rec_off", POINTER(c_uint64)),
+        ("flags", POINTER(c_uint8)),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.check_call(["make", "-C", os.path.join(REPO, "oracle")], stdout=subprocess.DEVNULL)
+        L = ctypes.CDLL(ORACLE_SO)
+        L.orc_crc32c.restype = c_uint32
+        L.orc_crc32c.argtypes = [c_void_p, c_uint64]
+        L.orc_file_reader_decode.argtypes = [c_void_p, c_uint64, POINTER(OrcFileResult)]
+        L.orc_file_result_free.argtypes = [POINTER(OrcFileResult)]
+        L.orc_read_next_at.argtypes = [c_void_p, c_uint64, c_uint64, POINTER(c_void_p), POINTER(c_uint64),
+                                       POINTER(c_int), POINTER(c_uint64), POINTER(c_uint64)]
+        L.orc_seek_next.argtypes = [c_void_p, c_uint64, c_uint64, c_uint64, POINTER(c_uint64), POINTER(c_void_p),
+                                    POINTER(c_uint64), POINTER(c_int)]
+        L.orc_snappy_decode.argtypes = [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]
+        L.orc_free.argtypes = [c_void_p]
+        L.orc_file_header.argtypes = [c_void_p, c_uint64, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint64)]
+        L.orc_parallel_read_at.restype = c_uint64
+        L.orc_parallel_read_at.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, c_int]
+        _lib = L
+    return _lib
+
+
+def _buf(data):
+    b = bytes(data)
+    return ctypes.create_string_buffer(b, len(b) + 1), len(b)
+
+
+def crc32c(data: bytes) -> int:
+    b, n = _buf(data)
+    return lib().orc_crc32c(b, n)
+
+
+def file_reader_decode(data: bytes) -> dict:
+    """FileReader ReadNext loop: records (bytes / None for nil) + terminal status."""
+    b, n = _buf(data)
+    r = OrcFileResult()
+    lib().orc_file_reader_decode(b, n, byref(r))
+    recs, rec_off = [], []
+    for i in range(r.n_records):
+        lo, hi = r.out_off[i], r.out_off[i + 1]
+        if r.flags[i] & 1:
+            recs.append(None)
+        elif hi > lo:
+            recs.append(ctypes.string_at(ctypes.addressof(r.out.contents) + lo, hi - lo))
+        else:
+            recs.append(b"")
+        rec_off.append(r.rec_off[i])
+    res = {"version": r.version, "compression": r.compression, "n_records": r.n_records,
+           "total_out_bytes": r.total_out_bytes, "status": r.status, "status_offset": r.status_offset,
+           "detail0": r.detail0, "detail1": r.detail1, "records": recs, "rec_off": rec_off}
+    lib().orc_file_result_free(byref(r))
+    return res
+
+
+def file_reader_decode_arrays(data) -> dict:
+    """Same as file_reader_decode, numpy arrays instead of per-record bytes (large files)."""
+    import numpy as np
+
+    arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data
+    arr = np.ascontiguousarray(arr)
+    r = OrcFileResult()
+    lib().orc_file_reader_decode(arr.ctypes.data, arr.shape[0], byref(r))
+    n, nb = r.n_records, r.total_out_bytes
+
+    def cp(ptr, count, dt):
+        if count == 0 or not ptr:  # file-header errors leave the arrays unallocated
+            return np.zeros(count, dtype=dt)
+        return np.ctypeslib.as_array(ptr, shape=(count,)).astype(dt, copy=True)
+
+    res = {"status": r.status, "status_offset": r.status_offset, "n_records": n, "total_out_bytes": nb,
+           "detail0": r.detail0, "detail1": r.detail1,
+           "out": cp(r.out, nb, np.uint8), "out_off": cp(r.out_off, n + 1, np.int64),
+           "rec_off": cp(r.rec_off, n, np.int64), "flags": cp(r.flags, n, np.uint8)}
+    lib().orc_file_result_free(byref(r))
+    return res
+
+
+def read_next_at(data: bytes, offset: int):
+    b, n = _buf(data)
+    out, ol, nil, d0, d1 = c_void_p(), c_uint64(), c_int(), c_uint64(), c_uint64()
+    st = lib().orc_read_next_at(b, n, offset, byref(out), byref(ol), byref(nil), byref(d0), byref(d1))
+    rec = None
+    if st == 0 and not nil.value:
+        rec = ctypes.string_at(out.value, ol.value) if ol.value else b""
+    if out.value:
+        lib().orc_free(out)
+    return st, rec
+
+
+def seek_next(data: bytes, offset: int, seek_len: int = 4096):
+    b, n = _buf(data)
+    ro, out, ol, nil = c_uint64(), c_void_p(), c_uint64(), c_int()
+    st = lib().orc_seek_next(b, n, offset, seek_len, byref(ro), byref(out), byref(ol), byref(nil))
+    rec = None
+    if st == 0 and not nil.value:
+        rec = ctypes.string_at(out.value, ol.value) if ol.value else b""
+    if out.value:
+        lib().orc_free(out)
+    return st, ro.value, rec
+
+
+def snappy_decode(data: bytes):
+    b, n = _buf(data)
+    out, ol = c_void_p(), c_uint64()
+    st = lib().orc_snappy_decode(b, n, byref(out), byref(ol))
+    rec = ctypes.string_at(out.value, ol.value) if st == 0 and ol.value else (b"" if st == 0 else None)
+    if out.value:
+        lib().orc_free(out)
+    return st, rec

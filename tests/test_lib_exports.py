@@ -1,0 +1,41 @@
+"""librio.so loads and exports every symbol include/rio.h declares (CPU; no compute calls)."""
+import ctypes
+import os
+import re
+
+from conftest import REPO
+
+from recordio import _lib as L
+
+
+def _declared():
+    src = open(os.path.join(REPO, "include", "rio.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(rio_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
+
+
+def test_every_declared_symbol_exported():
+    lib = ctypes.CDLL(L.LIB_PATH)
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    assert set(_declared()) <= set(L.EXPORTED) | {"rio_device_count"}
+
+
+def test_status_vocabulary():
+    lib = L.lib()
+    assert lib.rio_strerror(L.RIO_ERR_MAGIC) == b"magic number mismatch"
+    assert lib.rio_strerror(L.RIO_ERR_HEADER_CRC) == b"header checksum mismatch"
+    for s in (L.RIO_EOF, L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_HEADER, L.RIO_EOF_PAYLOAD):
+        assert lib.rio_status_is_eof(s)
+    for s in (L.RIO_OK, L.RIO_ERR_UNEXPECTED_EOF, L.RIO_ERR_MAGIC, L.RIO_ERR_HEADER_CRC):
+        assert not lib.rio_status_is_eof(s)
+    assert lib.rio_max_records(8 + 600) == 101
+
+
+def test_code_object_targets_gfx950():
+    data = open(L.LIB_PATH, "rb").read()
+    assert b"gfx950" in data

@@ -1,0 +1,88 @@
+"""The input generator (librio rio_encode_* / FileWriter mirror) against the reference fixtures (CPU).
+
+Byte identity with files the reference FileWriter wrote pins both the v4 header emission
+(fillRecordHeaderV4, file_writer.go:160-176) and the golang/snappy v1.0.0 encoder restatement.
+Host-only code: no GPU needed.
+"""
+import os
+
+import pytest
+
+import oracle_py as orc
+from conftest import read_fixture
+from recordio import FileWriter, encode_file, generate
+
+
+def asc(n):
+    return bytes(i & 0xFF for i in range(n))
+
+
+@pytest.mark.parametrize("name,records,comp", [
+    ("recordio_UncompressedSingleRecord", [asc(13)], 0),
+    ("recordio_UncompressedWriterMultiRecord_asc", [asc(i) for i in range(255)], 0),
+    ("recordio_SnappyWriterMultiRecord_asc", [asc(i) for i in range(255)], 2),
+    ("recordio_UncompressedSingleRecord_comp2", [asc(1337)], 2),
+    ("recordio_UncompressedNilAndEmptyRecord", [None, b""], 0),
+    ("recordio_UncompressedMagicNumberContent", [b"\x91\x8d\x4c", bytes([21, 8, 23]), b"\x91\x8d\x4c"], 0),
+])
+def test_generator_byte_identical_to_reference_writer(name, records, comp):
+    assert encode_file(records, comp) == read_fixture("v4_compat", name)
+
+
+def test_writer_size_kats(tmp_path, expectations):
+    k = expectations["kats"]["writer_sizes"]
+    p = str(tmp_path / "w")
+    w = FileWriter(p)
+    assert w.Open() is None
+    off, err = w.Write(os.urandom(13))
+    assert err is None and off == 8
+    assert w.Size() == k["single_13"]
+    w.Close()
+    w = FileWriter(p)
+    w.Open()
+    for n, want in zip([5, 10, 25], k["seq_5_10_25"]):
+        w.Write(os.urandom(n))
+        assert w.Size() == want
+    w.Close()
+    assert os.path.getsize(p) == 0x51
+    w = FileWriter(p)
+    w.Open()
+    offs = [w.Write(bytes([i]))[0] for i in range(127)]
+    w.Close()
+    assert os.path.getsize(p) == k["seq_127_one_byte"]
+    assert offs[0] == 8 and offs[1] == 8 + 12
+
+
+def test_nil_in_compressed_file_has_header_only():
+    """Write(nil) with snappy: header carries nil=1, u=0, c=1 and no payload (file_writer.go:198-219)."""
+    img = encode_file([None, b"x"], 2)
+    assert img[8:12] == b"\x91\x8d\x4c\x01"
+    assert img[12] == 0 and img[13] == 1  # u = 0, c = len(snappy(nil)) = 1
+    res = orc.file_reader_decode(img)
+    assert res["records"] == [None, b"x"]
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_generated_workloads_decode_on_oracle(kind):
+    img = generate(300, 1024, compression=2, kind=kind, seed=5).tobytes()
+    res = orc.file_reader_decode(img)
+    assert res["status"] == 1 and res["n_records"] == 300
+    assert all(len(r) == 1024 for r in res["records"])
+    if kind == 0:
+        assert len(set(res["records"])) == 1
+        assert max(max(r) for r in res["records"]) <= 254
+    else:
+        assert len(set(res["records"])) == 300
+
+
+def test_text_like_compression_ratio():
+    """The headline workload (C2) targets a snappy ratio of about 0.5-0.6."""
+    img = generate(2000, 1024, compression=2, kind=1, seed=1)
+    ratio = (len(img) - 8) / (2000 * 1024)
+    assert 0.45 < ratio < 0.70, ratio
+
+
+def test_generator_deterministic():
+    a = generate(500, 64, compression=2, kind=1, seed=3, threads=1)
+    b = generate(500, 64, compression=2, kind=1, seed=3, threads=4)
+    assert a.tobytes() == b.tobytes()
