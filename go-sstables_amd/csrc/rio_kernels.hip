@@ -559,24 +559,6 @@ __device__ __forceinline__ uint32_t header_fields_fast(const uint8_t* f, uint64_
     return (uint32_t)(i - p);
 }
 
-// One wave per record: lanes stride the payload bytes (uncompressed files).
-__global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
-    const ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_NONE) return;
-    const uint64_t n = st->n_records;
-    const uint32_t ver = st->version;
-    const int lane = threadIdx.x & 63;
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t i = wave; i < n; i += nwaves) {
-        const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
-        if (o1 == o0) continue;
-        const uint64_t p = P.rec_off[i];
-        uint64_t u, cl;
-        const uint64_t src = p + header_fields_fast(P.file, p, ver, u, cl);
-        for (uint64_t k = lane; k < o1 - o0; k += 64) P.out[o0 + k] = P.file[src + k];
-    }
-}
 
 // golang/snappy v1.0.0 decode (decode_other.go) of one record by one thread.
 __device__ bool snappy_decode_thread(const uint8_t* src, uint64_t slen, uint8_t* dst, uint64_t dlen) {
@@ -626,6 +608,140 @@ __device__ bool snappy_decode_thread(const uint8_t* src, uint64_t slen, uint8_t*
     return d == dlen;
 }
 
+// ---- 16-byte register window helpers (hardware unaligned global access, gfx950) -----------
+typedef uint4 __attribute__((aligned(1))) u4u;
+
+__device__ __forceinline__ uint4 ldu16(const uint8_t* p) { return *reinterpret_cast<const u4u*>(p); }
+__device__ __forceinline__ void stu16(uint8_t* p, uint4 v) { *reinterpret_cast<u4u*>(p) = v; }
+
+// 128-bit value >> 8k bits (k in [0, 16)), zero fill
+__device__ __forceinline__ uint4 shr_bytes(uint4 v, uint32_t k) {
+    uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+    if (k >= 8) {
+        lo = hi >> (8 * (k - 8));
+        hi = 0;
+    } else if (k) {
+        lo = (lo >> (8 * k)) | (hi << (64 - 8 * k));
+        hi >>= 8 * k;
+    }
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+// store the first n (< 16) bytes of v
+__device__ __forceinline__ void st_partial(uint8_t* p, uint4 v, uint32_t n) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+        if (k < n) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+
+// dst[d, d+len) = src[0, len), 16 bytes at a time; whole 16-byte stores may overrun the element
+// (later elements overwrite those bytes) but never the record end `dlen`.
+__device__ __forceinline__ void copy_fwd(uint8_t* dst, uint64_t d, const uint8_t* src, uint64_t len, uint64_t dlen) {
+    for (uint64_t k = 0; k < len; k += 16) {
+        const uint4 v = ldu16(src + k);
+        if (d + k + 16 <= dlen)
+            stu16(dst + d + k, v);
+        else
+            st_partial(dst + d + k, v, (uint32_t)(dlen - d - k));
+    }
+}
+
+// Uncompressed files: 16-lane groups, one record per group; each lane moves 16 bytes per step
+// (unaligned load and store; the record's last piece is stored exactly).
+__global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
+    const ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_NONE) return;
+    const uint64_t n = st->n_records;
+    const uint32_t ver = st->version;
+    const uint32_t lane = threadIdx.x & 15;
+    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
+    for (uint64_t i = grp; i < n; i += ngrp) {
+        const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
+        if (o1 == o0) continue;
+        const uint64_t p = P.rec_off[i];
+        uint64_t u, cl;
+        const uint8_t* src = P.file + p + header_fields_fast(P.file, p, ver, u, cl);
+        uint8_t* dst = P.out + o0;
+        const uint64_t len = o1 - o0;
+        for (uint64_t k = 16 * lane; k < len; k += 256) {
+            const uint4 v = ldu16(src + k);
+            if (k + 16 <= len)
+                stu16(dst + k, v);
+            else
+                st_partial(dst + k, v, (uint32_t)(len - k));
+        }
+    }
+}
+
+// Snappy block decode of one record by one lane (SIMT across the wave's records): the element
+// stream is read through a 16-byte register window that is shifted, not reloaded, while it holds
+// the next tag; literals that fit the window are stored straight from it. Output history reads
+// (copies) go through L1/L2. Same semantics and error checks as golang/snappy decode_other.go.
+__device__ bool snappy_decode_lane(const uint8_t* src, uint64_t slen, uint8_t* dst, uint64_t dlen) {
+    uint64_t s = 0, d = 0;
+    uint4 w = make_uint4(0, 0, 0, 0);
+    uint32_t wv = 0;  // valid bytes in w (w starts at src + s)
+    while (s < slen) {
+        if (wv < 5) {
+            w = ldu16(src + s);
+            wv = 16;
+        }
+        const uint32_t tag = w.x & 0xFF;
+        if ((tag & 3) == 0) {
+            uint32_t x = tag >> 2, hl = 1;
+            if (x >= 60) {
+                hl = x - 58;  // 1 tag + 1..4 length bytes
+                const uint64_t lw = ((uint64_t)w.y << 32 | w.x) >> 8;
+                x = (uint32_t)(lw & ((1ull << (8 * (hl - 1))) - 1));
+                if (s + hl > slen) return false;
+            }
+            const uint64_t len = (uint64_t)x + 1;
+            if (len > dlen - d || len > slen - s - hl) return false;
+            if (hl + len <= wv && d + 16 <= dlen) {
+                stu16(dst + d, shr_bytes(w, hl));
+                const uint32_t adv = (uint32_t)(hl + len);
+                if (adv < 16) w = shr_bytes(w, adv);
+                wv -= adv;
+            } else {
+                copy_fwd(dst, d, src + s + hl, len, dlen);
+                wv = 0;
+            }
+            s += hl + len;
+            d += len;
+            continue;
+        }
+        uint64_t len, off;
+        uint32_t hl;
+        if ((tag & 3) == 1) {
+            hl = 2;
+            len = 4 + ((tag >> 2) & 7);
+            off = ((tag & 0xE0u) << 3) | ((w.x >> 8) & 0xFF);
+        } else if ((tag & 3) == 2) {
+            hl = 3;
+            len = 1 + (tag >> 2);
+            off = (w.x >> 8) & 0xFFFF;
+        } else {
+            hl = 5;
+            len = 1 + (tag >> 2);
+            off = (uint64_t)((w.x >> 8) | (w.y << 24));
+        }
+        if (s + hl > slen) return false;
+        if (off == 0 || d < off || len > dlen - d) return false;
+        if (off >= 16) {
+            copy_fwd(dst, d, dst + d - off, len, dlen);
+        } else {  // overlapping pattern copy (RLE-like): forward bytes
+            for (uint64_t k = 0; k < len; k++) dst[d + k] = dst[d + k - off];
+        }
+        s += hl;
+        d += len;
+        w = shr_bytes(w, hl);
+        wv -= hl;
+    }
+    return d == dlen;
+}
+
 __global__ void __launch_bounds__(256) k_decode_snappy(FrameParams P) {
     ScanState* st = P.state;
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
@@ -641,8 +757,7 @@ __global__ void __launch_bounds__(256) k_decode_snappy(FrameParams P) {
         const uint8_t* pay = P.file + p + hl;
         uint64_t dl = 0;
         const int k = uvarint_buf(pay, cl, dl);
-        if (k <= 0 || dl != o1 - o0 ||
-            !snappy_decode_thread(pay + k, cl - (uint64_t)k, P.out + o0, o1 - o0))
+        if (k <= 0 || dl != o1 - o0 || !snappy_decode_lane(pay + k, cl - (uint64_t)k, P.out + o0, o1 - o0))
             atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)i);
     }
 }
