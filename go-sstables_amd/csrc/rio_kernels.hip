@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rio_device.h"
+#include "rio_dev_util.h"
 
 namespace rio {
 
@@ -65,24 +66,6 @@ __device__ int read_uvarint(Src& s, uint64_t& x) {
         sh += 7;
     }
     return RIO_ERR_VARINT_OVERFLOW;
-}
-
-// encoding/binary.Uvarint semantics: >0 bytes read, 0 buffer too small, <0 overflow
-__device__ int uvarint_buf(const uint8_t* p, uint64_t n, uint64_t& x) {
-    uint64_t v = 0;
-    uint32_t sh = 0;
-    for (uint64_t i = 0; i < n; i++) {
-        if (i == 10) return -(int)(i + 1);
-        uint32_t b = p[i];
-        if (b < 0x80) {
-            if (i == 9 && b > 1) return -(int)(i + 1);
-            x = v | ((uint64_t)b << sh);
-            return (int)(i + 1);
-        }
-        v |= (uint64_t)(b & 0x7F) << sh;
-        sh += 7;
-    }
-    return 0;
 }
 
 struct Hdr {
@@ -536,105 +519,6 @@ __global__ void __launch_bounds__(256) k_zero(FrameParams P) {
 // ------------------------------------------------------------------------------------------
 // Decode
 // ------------------------------------------------------------------------------------------
-// Re-parse an already validated header at a record start: sizes and header length, no checks.
-__device__ __forceinline__ uint64_t vread(const uint8_t* f, uint64_t& i) {
-    uint64_t v = 0;
-    uint32_t sh = 0, b;
-    do {
-        b = f[i++];
-        v |= (uint64_t)(b & 0x7F) << sh;
-        sh += 7;
-    } while ((b & 0x80) && sh < 70);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t header_fields_fast(const uint8_t* f, uint64_t p, uint32_t ver, uint64_t& u,
-                                                       uint64_t& c) {
-    uint64_t i = p;
-    (void)vread(f, i);  // magic
-    i++;                // nil byte
-    u = vread(f, i);
-    c = vread(f, i);
-    if (ver == RIO_VERSION4) (void)vread(f, i);  // crc
-    return (uint32_t)(i - p);
-}
-
-
-// golang/snappy v1.0.0 decode (decode_other.go) of one record by one thread.
-__device__ bool snappy_decode_thread(const uint8_t* src, uint64_t slen, uint8_t* dst, uint64_t dlen) {
-    uint64_t s = 0, d = 0;
-    while (s < slen) {
-        const uint32_t tag = src[s];
-        uint64_t length, offset;
-        if ((tag & 3) == 0) {
-            uint32_t x = tag >> 2;
-            if (x < 60) {
-                s += 1;
-            } else {
-                const uint32_t nb = x - 59;  // 1..4 extra length bytes
-                s += 1 + nb;
-                if (s > slen) return false;
-                x = 0;
-                for (uint32_t k = 0; k < nb; k++) x |= (uint32_t)src[s - nb + k] << (8 * k);
-            }
-            length = (uint64_t)x + 1;
-            if (length > dlen - d || length > slen - s) return false;
-            for (uint64_t k = 0; k < length; k++) dst[d + k] = src[s + k];
-            d += length;
-            s += length;
-            continue;
-        }
-        if ((tag & 3) == 1) {
-            s += 2;
-            if (s > slen) return false;
-            length = 4 + ((tag >> 2) & 7);
-            offset = ((tag & 0xE0u) << 3) | src[s - 1];
-        } else if ((tag & 3) == 2) {
-            s += 3;
-            if (s > slen) return false;
-            length = 1 + (tag >> 2);
-            offset = (uint64_t)src[s - 2] | (uint64_t)src[s - 1] << 8;
-        } else {
-            s += 5;
-            if (s > slen) return false;
-            length = 1 + (tag >> 2);
-            offset = (uint64_t)src[s - 4] | (uint64_t)src[s - 3] << 8 | (uint64_t)src[s - 2] << 16 |
-                     (uint64_t)src[s - 1] << 24;
-        }
-        if (offset == 0 || d < offset || length > dlen - d) return false;
-        for (uint64_t k = 0; k < length; k++) dst[d + k] = dst[d - offset + k];
-        d += length;
-    }
-    return d == dlen;
-}
-
-// ---- 16-byte register window helpers (hardware unaligned global access, gfx950) -----------
-typedef uint4 __attribute__((aligned(1))) u4u;
-
-__device__ __forceinline__ uint4 ldu16(const uint8_t* p) { return *reinterpret_cast<const u4u*>(p); }
-__device__ __forceinline__ void stu16(uint8_t* p, uint4 v) { *reinterpret_cast<u4u*>(p) = v; }
-
-// 128-bit value >> 8k bits (k in [0, 16)), zero fill
-__device__ __forceinline__ uint4 shr_bytes(uint4 v, uint32_t k) {
-    uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
-    if (k >= 8) {
-        lo = hi >> (8 * (k - 8));
-        hi = 0;
-    } else if (k) {
-        lo = (lo >> (8 * k)) | (hi << (64 - 8 * k));
-        hi >>= 8 * k;
-    }
-    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-}
-
-// store the first n (< 16) bytes of v
-__device__ __forceinline__ void st_partial(uint8_t* p, uint4 v, uint32_t n) {
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (uint32_t k = 0; k < 16; k++)
-        if (k < n) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-}
-
 // dst[d, d+len) = src[0, len), 16 bytes at a time; whole 16-byte stores may overrun the element
 // (later elements overwrite those bytes) but never the record end `dlen`.
 __device__ __forceinline__ void copy_fwd(uint8_t* dst, uint64_t d, const uint8_t* src, uint64_t len, uint64_t dlen) {
@@ -672,93 +556,6 @@ __global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
             else
                 st_partial(dst + k, v, (uint32_t)(len - k));
         }
-    }
-}
-
-// Snappy block decode of one record by one lane (SIMT across the wave's records): the element
-// stream is read through a 16-byte register window that is shifted, not reloaded, while it holds
-// the next tag; literals that fit the window are stored straight from it. Output history reads
-// (copies) go through L1/L2. Same semantics and error checks as golang/snappy decode_other.go.
-__device__ bool snappy_decode_lane(const uint8_t* src, uint64_t slen, uint8_t* dst, uint64_t dlen) {
-    uint64_t s = 0, d = 0;
-    uint4 w = make_uint4(0, 0, 0, 0);
-    uint32_t wv = 0;  // valid bytes in w (w starts at src + s)
-    while (s < slen) {
-        if (wv < 5) {
-            w = ldu16(src + s);
-            wv = 16;
-        }
-        const uint32_t tag = w.x & 0xFF;
-        if ((tag & 3) == 0) {
-            uint32_t x = tag >> 2, hl = 1;
-            if (x >= 60) {
-                hl = x - 58;  // 1 tag + 1..4 length bytes
-                const uint64_t lw = ((uint64_t)w.y << 32 | w.x) >> 8;
-                x = (uint32_t)(lw & ((1ull << (8 * (hl - 1))) - 1));
-                if (s + hl > slen) return false;
-            }
-            const uint64_t len = (uint64_t)x + 1;
-            if (len > dlen - d || len > slen - s - hl) return false;
-            if (hl + len <= wv && d + 16 <= dlen) {
-                stu16(dst + d, shr_bytes(w, hl));
-                const uint32_t adv = (uint32_t)(hl + len);
-                if (adv < 16) w = shr_bytes(w, adv);
-                wv -= adv;
-            } else {
-                copy_fwd(dst, d, src + s + hl, len, dlen);
-                wv = 0;
-            }
-            s += hl + len;
-            d += len;
-            continue;
-        }
-        uint64_t len, off;
-        uint32_t hl;
-        if ((tag & 3) == 1) {
-            hl = 2;
-            len = 4 + ((tag >> 2) & 7);
-            off = ((tag & 0xE0u) << 3) | ((w.x >> 8) & 0xFF);
-        } else if ((tag & 3) == 2) {
-            hl = 3;
-            len = 1 + (tag >> 2);
-            off = (w.x >> 8) & 0xFFFF;
-        } else {
-            hl = 5;
-            len = 1 + (tag >> 2);
-            off = (uint64_t)((w.x >> 8) | (w.y << 24));
-        }
-        if (s + hl > slen) return false;
-        if (off == 0 || d < off || len > dlen - d) return false;
-        if (off >= 16) {
-            copy_fwd(dst, d, dst + d - off, len, dlen);
-        } else {  // overlapping pattern copy (RLE-like): forward bytes
-            for (uint64_t k = 0; k < len; k++) dst[d + k] = dst[d + k - off];
-        }
-        s += hl;
-        d += len;
-        w = shr_bytes(w, hl);
-        wv -= hl;
-    }
-    return d == dlen;
-}
-
-__global__ void __launch_bounds__(256) k_decode_snappy(FrameParams P) {
-    ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
-    const uint64_t n = st->n_records;
-    const uint32_t ver = st->version;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (P.flags[i] & RIO_FLAG_NIL) continue;
-        const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
-        const uint64_t p = P.rec_off[i];
-        uint64_t u, cl;
-        const uint32_t hl = header_fields_fast(P.file, p, ver, u, cl);
-        const uint8_t* pay = P.file + p + hl;
-        uint64_t dl = 0;
-        const int k = uvarint_buf(pay, cl, dl);
-        if (k <= 0 || dl != o1 - o0 || !snappy_decode_lane(pay + k, cl - (uint64_t)k, P.out + o0, o1 - o0))
-            atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)i);
     }
 }
 
@@ -969,13 +766,16 @@ hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 }
 
 // Phase B: placement into the caller's arrays, decode, final result.
+hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s);  // rio_snappy.hip
+
+// Phase B: placement into the caller's arrays, decode, final result. Both decoders check the
+// file's compression type on the device and exit at once when it is not theirs.
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
-    const unsigned grid = 2048;
     hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 256)), dim3(256), 0, s, P);
     hipLaunchKernelGGL(k_post_scan, dim3(1), dim3(64), 0, s, P);
     if (ev) (void)hipEventRecord(ev[3], s);
-    hipLaunchKernelGGL(k_decode_copy, dim3(grid), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_decode_snappy, dim3(grid), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);
+    launch_snappy_decode(P, s);
     if (ev) (void)hipEventRecord(ev[4], s);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, P);
     return hipGetLastError();
