@@ -143,7 +143,7 @@ struct rio_ctx {
         ev_cursor = 0;
     }
     // framing arenas
-    DevBuf scratch_off, scratch_len, chunks, block_runs, chunk_excl, place, block_excl, state, info;
+    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, chunks, block_runs, chunk_excl, place, block_excl, state, info;
     // host-API arenas
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
     uint8_t* pinned[2] = {nullptr, nullptr};
@@ -166,6 +166,7 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     const uint64_t nc = std::max<uint64_t>(P.n_chunks, 1), nb = std::max<uint64_t>(P.n_blocks, 1);
     HIP_TRY(ctx->scratch_off.ensure(nc * P.slots * 8));
     HIP_TRY(ctx->scratch_len.ensure(nc * P.slots * 8));
+    HIP_TRY(ctx->scratch_pay.ensure(nc * P.slots * 8));
     HIP_TRY(ctx->chunks.ensure(nc * sizeof(ChunkSum)));
     HIP_TRY(ctx->chunk_excl.ensure(nc * sizeof(RunSum)));
     HIP_TRY(ctx->place.ensure(nc * sizeof(ChunkPlace)));
@@ -175,6 +176,7 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     HIP_TRY(ctx->info.ensure(sizeof(rio_file_info)));
     P.scratch_off = ctx->scratch_off.as<uint64_t>();
     P.scratch_len = ctx->scratch_len.as<uint64_t>();
+    P.scratch_pay = ctx->scratch_pay.as<uint64_t>();
     P.chunks = ctx->chunks.as<ChunkSum>();
     P.chunk_excl = ctx->chunk_excl.as<RunSum>();
     P.place = ctx->place.as<ChunkPlace>();
@@ -216,7 +218,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
+    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
                       &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
                       &c->readat_out, &c->readat_res, &c->seek_off})
         b->release();
@@ -277,6 +279,8 @@ extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t l
     P.flags = d_flags;
     P.rec_cap = rec_cap;
     P.info = d_info;
+    HIP_TRY(ctx->rec_pay.ensure((rec_cap + 1) * 8));
+    P.rec_pay = ctx->rec_pay.as<uint64_t>();
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     hipEvent_t* ev = ctx->next_events();
     HIP_TRY(launch_phase_a(P, s, ev));
@@ -390,6 +394,8 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
     P.rec_off = ctx->rec_off.as<uint64_t>();
     P.flags = ctx->flags.as<uint8_t>();
     P.rec_cap = n;
+    HIP_TRY(ctx->rec_pay.ensure((n + 1) * 8));
+    P.rec_pay = ctx->rec_pay.as<uint64_t>();
     HIP_TRY(launch_phase_b(P, ctx->stream, ctx->same_events()));
     rio_file_info fin{};
     HIP_TRY(hipMemcpyAsync(&fin, P.info, sizeof fin, hipMemcpyDeviceToHost, ctx->stream));

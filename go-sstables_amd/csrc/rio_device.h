@@ -80,6 +80,11 @@ struct FrameParams {
     uint64_t slots;  // scratch slots per chunk
     uint64_t* scratch_off;   // [n_chunks * slots] record header offsets
     uint64_t* scratch_len;   // [n_chunks * slots] decoded length | kNilBit
+    uint64_t* scratch_pay;   // [n_chunks * slots] payload descriptor (see rec_pay)
+    // internal per-record payload descriptor [rec_cap]: bits 0..7 = bytes from the record header
+    // start to the first payload byte the decoder consumes (header + snappy preamble), bits 8..63
+    // = length of the consumed payload stream (snappy element stream / raw payload)
+    uint64_t* rec_pay;
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)
     RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix

@@ -107,32 +107,134 @@ __device__ int parse_header(const uint8_t* f, uint64_t p, uint64_t avail, uint64
     return RIO_OK;
 }
 
+// ---- register-window header parse (fast path) --------------------------------------------
+// 8 bytes starting at byte k (0..24) of a 32-byte window held in 8 dwords
+__device__ __forceinline__ uint64_t win8(const uint32_t (&w)[8], uint32_t k) {
+    const uint32_t j = k >> 2, r = 8 * (k & 3);
+    uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+#pragma unroll
+    for (uint32_t t = 1; t < 6; t++) {
+        d0 = j == t ? w[t] : d0;
+        d1 = j == t ? w[t + 1] : d1;
+        d2 = j == t ? w[t + 2] : d2;
+    }
+    const uint64_t a = ((uint64_t)d1 << 32) | d0, b = d2;
+    return r ? (a >> r) | (b << (64 - r)) : a;
+}
+
+// LEB128 of at most 8 bytes at the bottom of x: returns the byte count (0 if longer than 8)
+__device__ __forceinline__ uint32_t varint8(uint64_t x, uint64_t& v) {
+    const uint64_t stop = ~x & 0x8080808080808080ull;
+    if (!stop) return 0;
+    const uint32_t nb = (__builtin_ctzll(stop) >> 3) + 1;
+    const uint64_t m = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+    const uint64_t y = x & m;
+    uint64_t r = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < 8; g++) r |= ((y >> (8 * g)) & 0x7F) << (7 * g);
+    v = r;
+    return nb;
+}
+
+__device__ __forceinline__ uint32_t crc32c_bytes(uint32_t c, uint64_t x, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) c = crc32c_byte(c, (uint32_t)(x >> (8 * i)) & 0xFF);
+    return c;
+}
+
+// CRC-32C register state after the canonical magic bytes 91 8d 4c (before the final xor)
+__device__ __forceinline__ uint32_t crc_after_magic() {
+    uint32_t c = 0xFFFFFFFFu;
+    c = crc32c_byte(c, 0x91);
+    c = crc32c_byte(c, 0x8D);
+    return crc32c_byte(c, 0x4C);
+}
+
 // FileReader sequential semantics at record start p: header + payload availability + decoded
-// size. next = start of the following record.
+// size. next = start of the following record; pay = rec_pay descriptor (rio_device.h).
+// Common records (canonical magic, header + preamble inside 32 bytes, valid) are parsed from two
+// 16-byte loads; everything else (and every failure, for its exact classification) takes the
+// byte-wise ReadUvarint restatement.
 __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t ver, uint32_t comp,
-                            Hdr& h, uint64_t& next, uint64_t& out_len) {
+                            Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay) {
+    if (p + 32 <= len) {
+        const uint4 a = ldu16(f + p), b = ldu16(f + p + 16);
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        if ((a.x & 0xFFFFFFu) == 0x4C8D91u) {
+            uint64_t u = 0, c = 0, crc = 0;
+            const uint32_t nu = varint8(win8(w, 4), u);
+            const uint32_t nc = nu ? varint8(win8(w, 4 + nu), c) : 0;
+            uint32_t hl = 4 + nu + nc;
+            bool ok = nu && nc;
+            uint32_t act = 0;
+            if (ok && ver == RIO_VERSION4) {
+                const uint32_t ncrc = varint8(win8(w, hl), crc);
+                uint32_t cs = crc32c_byte(crc_after_magic(), (a.x >> 24) & 0xFF);
+                cs = crc32c_bytes(cs, win8(w, 4), nu);
+                cs = crc32c_bytes(cs, win8(w, 4 + nu), nc);
+                act = cs ^ 0xFFFFFFFFu;
+                ok = ncrc && act == crc;
+                hl += ncrc;
+            }
+            if (ok) {
+                const bool nil = ((a.x >> 24) & 0xFF) == 1;
+                const uint64_t plen = comp != RIO_COMP_NONE ? c : u;
+                const uint64_t avail = len - p - hl;
+                uint64_t dl = plen;
+                uint32_t k = 0;
+                if (!nil && comp == RIO_COMP_SNAPPY && hl <= 24) {
+                    k = varint8(win8(w, hl), dl);
+                    ok = k && k <= plen && dl <= 0xFFFFFFFFull && dl <= 22ull * (plen - k) + 64;
+                } else if (!nil && comp == RIO_COMP_SNAPPY) {
+                    ok = false;
+                }
+                if (ok && (nil || plen <= avail)) {
+                    h.u = u;
+                    h.c = c;
+                    h.exp_crc = crc;
+                    h.act_crc = act;
+                    h.hdr_len = hl;
+                    h.magic_len = 3;
+                    h.nil = nil;
+                    if (nil) {  // file_reader.go:96-99: nil => no payload bytes
+                        next = p + hl;
+                        out_len = 0;
+                        pay = hl;
+                    } else {
+                        next = p + hl + plen;
+                        out_len = dl;
+                        pay = ((plen - k) << 8) | (hl + k);
+                    }
+                    return RIO_OK;
+                }
+            }
+        }
+    }
     uint64_t cap = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : ~0ull;
     int e = parse_header(f, p, len - p, cap, ver, h);
     if (e) return e;
     if (h.nil) {  // file_reader.go:96-99: nil => no payload bytes
         next = p + h.hdr_len;
         out_len = 0;
+        pay = h.hdr_len;
         return RIO_OK;
     }
     uint64_t plen = comp != RIO_COMP_NONE ? h.c : h.u;
     uint64_t avail = len - p - h.hdr_len;
     if (plen > avail) return avail == 0 ? RIO_EOF_PAYLOAD : RIO_ERR_UNEXPECTED_EOF;
+    uint64_t k = 0;
     if (comp == RIO_COMP_SNAPPY) {
         uint64_t d = 0;
-        int k = uvarint_buf(f + p + h.hdr_len, plen, d);
+        const int kk = uvarint_buf(f + p + h.hdr_len, plen, d);
         // snappy decodedLen: n<=0 or > 0xffffffff => ErrCorrupt; a preamble above 22x the element
         // bytes cannot be produced (max 64 output bytes per 3-byte tagCopy2) => ErrCorrupt later.
-        if (k <= 0 || d > 0xFFFFFFFFull || d > 22ull * (plen - (uint64_t)k) + 64) return RIO_ERR_DECOMPRESS;
+        if (kk <= 0 || d > 0xFFFFFFFFull || d > 22ull * (plen - (uint64_t)kk) + 64) return RIO_ERR_DECOMPRESS;
         out_len = d;
+        k = (uint64_t)kk;
     } else {
         out_len = plen;
     }
     next = p + h.hdr_len + plen;
+    pay = ((plen - k) << 8) | (h.hdr_len + k);
     return RIO_OK;
 }
 
@@ -205,8 +307,8 @@ __device__ uint64_t find_entry(const FrameParams& P, uint64_t cs, uint64_t ce, u
                 if (p < cs || p >= ce || p + 2 >= P.len) continue;
                 if (f[p + 1] != 0x8D || f[p + 2] != 0x4C) continue;
                 Hdr h;
-                uint64_t nx, ol;
-                if (frame_record(f, P.len, p, ver, comp, h, nx, ol) == RIO_OK) return p;
+                uint64_t nx, ol, pd;
+                if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd) == RIO_OK) return p;
             }
         }
     }
@@ -228,10 +330,11 @@ __device__ void walk_chunk(const FrameParams& P, uint64_t c, uint64_t from, uint
         uint64_t p = from;
         uint64_t* so = P.scratch_off + c * P.slots;
         uint64_t* sl = P.scratch_len + c * P.slots;
+        uint64_t* sp = P.scratch_pay + c * P.slots;
         while (p < ce) {
             Hdr h;
-            uint64_t next = 0, olen = 0;
-            int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen);
+            uint64_t next = 0, olen = 0, pd = 0;
+            int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd);
             if (e) {
                 s.status = e;
                 s.err_off = p;
@@ -248,6 +351,7 @@ __device__ void walk_chunk(const FrameParams& P, uint64_t c, uint64_t from, uint
             if (s.count < P.slots) {
                 so[s.count] = p;
                 sl[s.count] = olen | (h.nil ? kNilBit : 0);
+                sp[s.count] = pd;
             }
             s.count++;
             s.bytes += olen;
@@ -482,11 +586,13 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     if (pl.base_idx + pl.owned > P.rec_cap || st->n_records > P.rec_cap) return;
     const uint64_t* so = P.scratch_off + c * P.slots;
     const uint64_t* sl = P.scratch_len + c * P.slots;
+    const uint64_t* sp = P.scratch_pay + c * P.slots;
     uint64_t ob = pl.base_bytes;
     for (uint64_t k = 0; k < pl.owned; k++) {
         const uint64_t i = pl.base_idx + k;
         const uint64_t l = sl[k];
         P.rec_off[i] = so[k];
+        P.rec_pay[i] = sp[k];
         P.out_off[i] = ob;
         P.flags[i] = (l & kNilBit) ? RIO_FLAG_NIL : 0;
         ob += l & ~kNilBit;
@@ -544,9 +650,7 @@ __global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
     for (uint64_t i = grp; i < n; i += ngrp) {
         const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
         if (o1 == o0) continue;
-        const uint64_t p = P.rec_off[i];
-        uint64_t u, cl;
-        const uint8_t* src = P.file + p + header_fields_fast(P.file, p, ver, u, cl);
+        const uint8_t* src = P.file + P.rec_off[i] + (P.rec_pay[i] & 0xFF);
         uint8_t* dst = P.out + o0;
         const uint64_t len = o1 - o0;
         for (uint64_t k = 16 * lane; k < len; k += 256) {
