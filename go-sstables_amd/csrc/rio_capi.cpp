@@ -143,7 +143,7 @@ struct rio_ctx {
         ev_cursor = 0;
     }
     // framing arenas
-    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, chunks, block_runs, chunk_excl, place, block_excl, state, info;
+    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, sink, chunks, block_runs, chunk_excl, place, block_excl, state, info;
     // host-API arenas
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
     uint8_t* pinned[2] = {nullptr, nullptr};
@@ -174,6 +174,8 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     HIP_TRY(ctx->block_excl.ensure(nb * sizeof(RunSum)));
     HIP_TRY(ctx->state.ensure(sizeof(ScanState)));
     HIP_TRY(ctx->info.ensure(sizeof(rio_file_info)));
+    HIP_TRY(ctx->sink.ensure(kSinkBytes));
+    P.sink = ctx->sink.as<uint8_t>();
     P.scratch_off = ctx->scratch_off.as<uint64_t>();
     P.scratch_len = ctx->scratch_len.as<uint64_t>();
     P.scratch_pay = ctx->scratch_pay.as<uint64_t>();
@@ -218,7 +220,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
+    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->sink, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
                       &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
                       &c->readat_out, &c->readat_res, &c->seek_off})
         b->release();

@@ -10,6 +10,12 @@ namespace rio {
 constexpr uint64_t kNone = ~0ull;       // "no speculative entry found in this chunk"
 constexpr uint64_t kNilBit = 1ull << 63;  // scratch out_len | kNilBit => nil record
 
+// Snappy decode launch shape (k_snappy_pipe): every wave owns one 64-byte sink line that absorbs
+// the pipeline's placeholder loads and stores.
+constexpr unsigned kSnappyBlock = 256;
+constexpr unsigned kSnappyGrid = 512;
+constexpr uint64_t kSinkBytes = (uint64_t)kSnappyBlock / 64 * kSnappyGrid * 64;
+
 // Framing chunk: a byte range [cs, ce) of the file; a chunk OWNS the records whose header starts
 // in its range. Written by the walk kernel, consumed by the scan / place kernels.
 struct ChunkSum {
@@ -85,6 +91,7 @@ struct FrameParams {
     // start to the first payload byte the decoder consumes (header + snappy preamble), bits 8..63
     // = length of the consumed payload stream (snappy element stream / raw payload)
     uint64_t* rec_pay;
+    uint8_t* sink;           // [kSinkBytes] placeholder-store target of the Snappy decode pipeline
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)
     RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix
