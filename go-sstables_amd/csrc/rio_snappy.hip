@@ -13,10 +13,13 @@
 //     in issue order, so a uniform schedule is what lets the compiler wait for exactly the loads
 //     issued kD iterations earlier instead of draining the queue whenever some lane of the wave
 //     touched memory.
+//   * The flush is cooperative (see snappy_wave): 64 contiguous bytes of 16 records per wave
+//     store. Lane-private 16-byte stores to 64 records run at ~1.5 TB/s on MI355X, the 16-record
+//     form at ~4.2 TB/s (scripts/mem_probe.hip); loads do not care (5.5 vs 6.0 TB/s).
 //   * History: the last 256 decoded bytes of each record live in an LDS ring; copies reaching
 //     further back (offset > kFarOff) are loaded from the output arena at PARSE time, kD
 //     iterations before use — the flush schedule guarantees those bytes were stored already
-//     (flush lag < 32 bytes, parser lead <= 16*(kD-1) bytes, kFarOff >= 16*kD + 32).
+//     (flush lag < 128 bytes, parser lead <= 16*(kD-1) bytes: kFarOff >= 16*(kD-1) + 16 + 128).
 //   * Input: aligned 16-byte chunks loaded kD iterations ahead land in a 64-byte LDS ring.
 //   * LDS image per wave is chunk-interleaved ([chunk][lane][16 B]): every 16-byte access by a
 //     wave touches each bank once, whatever positions the lanes are at.
@@ -34,10 +37,35 @@ constexpr uint32_t kOutCh = 16;                  // history ring: 16 chunks = 25
 constexpr uint32_t kInCh = 4;                    // input ring: 4 chunks = 64 bytes per lane
 constexpr uint32_t kWaveLds = (kOutCh + kInCh) * 64 * 16;  // 20 KiB per wave
 constexpr uint32_t kFarOff = kOutCh * 16 - 48;   // copies reaching further back read HBM
-constexpr uint32_t kD = 3;                       // pipeline depth in iterations
+constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
-static_assert(kFarOff >= 16 * kD + 32, "far history must be flushed before the parser reads it");
+static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128, "far history must be flushed before the parser reads it");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
+
+// bytes [r, r + 16) of the 32-byte little-endian concatenation (a, b), r in [0, 16): dword
+// selection by r >> 2 (two select levels) + v_alignbyte_b32 for the byte shift
+__device__ __forceinline__ uint4 funnel16(uint4 a, uint4 b, uint32_t r) {
+    const uint32_t sh = r & 3u;
+    const bool h1 = (r & 4u) != 0, h2 = (r & 8u) != 0;
+    const uint32_t p0 = h1 ? a.y : a.x, p1 = h1 ? a.z : a.y, p2 = h1 ? a.w : a.z, p3 = h1 ? b.x : a.w,
+                   p4 = h1 ? b.y : b.x, p5 = h1 ? b.z : b.y, p6 = h1 ? b.w : b.z;
+    const uint32_t e0 = h2 ? p2 : p0, e1 = h2 ? p3 : p1, e2 = h2 ? p4 : p2, e3 = h2 ? p5 : p3, e4 = h2 ? p6 : p4;
+    return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
+                      __builtin_amdgcn_alignbyte(e3, e2, sh), __builtin_amdgcn_alignbyte(e4, e3, sh));
+}
+
+__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+// place v at byte offset r of a 32-byte window: lo = v << 8r (bytes of the chunk holding the
+// position), hi = v >> 8(16 - r) (bytes spilling into the next chunk)
+__device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& hi) {
+    const uint32_t t = (16u - r) & 15u;
+    const uint4 a = funnel16(zero4(), v, t), b = funnel16(v, zero4(), t);
+    lo = sel4(r != 0, a, b);  // r == 0: a = 0, b = v
+    hi = sel4(r != 0, b, a);
+}
 
 // per-lane view of the wave's chunk-interleaved LDS image
 struct LaneLds {
@@ -45,17 +73,9 @@ struct LaneLds {
     __device__ uint4* out(uint32_t pos) const { return reinterpret_cast<uint4*>(p + ((pos >> 4) & (kOutCh - 1)) * 1024); }
     __device__ uint4* in(uint32_t c) const { return reinterpret_cast<uint4*>(p + (kOutCh + (c & (kInCh - 1))) * 1024); }
     // 16 bytes of history at output position q
-    __device__ uint4 out16(uint32_t q) const {
-        const uint32_t r = q & 15u;
-        const uint4 x0 = *out(q), x1 = *out(q + 16);
-        return or4(shr_bytes(x0, r), shl_bytes(x1, 16 - r));
-    }
+    __device__ uint4 out16(uint32_t q) const { return funnel16(*out(q), *out(q + 16), q & 15u); }
     // 16 bytes of input at aligned-frame position pos
-    __device__ uint4 in16(uint32_t pos) const {
-        const uint32_t r = pos & 15u, c = pos >> 4;
-        const uint4 x0 = *in(c), x1 = *in(c + 1);
-        return or4(shr_bytes(x0, r), shl_bytes(x1, 16 - r));
-    }
+    __device__ uint4 in16(uint32_t pos) const { return funnel16(*in(pos >> 4), *in((pos >> 4) + 1), pos & 15u); }
 };
 
 // one pipeline slot: a parsed piece plus the two loads issued with it
@@ -70,130 +90,133 @@ struct Slot {
 };
 }  // namespace
 
-// Decode one record. src: element stream (after the length preamble) of slen bytes; the decoded
-// length dlen was validated against the preamble by framing.
-__device__ bool snappy_pipe(const uint8_t* src, uint32_t slen, const LaneLds& L, uint8_t* gout, uint32_t dlen,
-                            uint8_t* sink) {
-    if (slen == 0) return dlen == 0;
-    const uint32_t so = (uint32_t)((uintptr_t)src & 15u);
-    const uint4* sa = reinterpret_cast<const uint4*>(src - so);
-    const uint32_t lastc = (so + slen - 1) >> 4;  // last input chunk holding stream bytes
+// Per-lane record state of the pipelined decoder.
+struct Rec {
+    const uint4* sa;  // aligned base of the element stream
+    uint64_t o0;      // output offset of the record in the arena
+    uint32_t so, slen, dlen, lastc;
+};
+
+// Decode the 64 records of one wave batch, one per lane (`live` = the lane holds a record). The
+// loop runs until every lane of the wave is done: finished lanes keep stepping as bubbles because
+// the flush is cooperative — at step j the 16 lanes 16*(j%4) .. +15 are "owners" and every quad of
+// lanes writes one owner's next complete 64-byte block (16 B per lane, 64 contiguous bytes per
+// record): a wave store touches 16 records instead of 64, which the L2 absorbs ~3x faster.
+// Returns the lane's verdict: true = decoded, bytes [0, dlen) written.
+__device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane, uint8_t* out, uint8_t* sink) {
+    const LaneLds L{wl + lane * 16};
+    const uint4* sa = R.sa;
+    const uint32_t so = R.so, slen = R.slen, dlen = R.dlen, lastc = R.lastc;
+    uint8_t* const gout = out + R.o0;  // addresses derive from the arena argument: global, not flat
     // prime the input ring with chunks [0, 4)
-    uint32_t whi = min(kInCh, lastc + 1);  // chunks [0, whi) have landed in LDS
+    const bool has_stream = live && slen != 0;
+    uint32_t whi = has_stream ? min(kInCh, lastc + 1) : 0u;  // chunks [0, whi) have landed
     for (uint32_t c = 0; c < whi; c++) *L.in(c) = sa[c];
-    uint32_t cn = whi;  // next chunk to load
+    // next chunk to load; a lane without a stream never takes one (cn > lastc always)
+    uint32_t cn = has_stream ? whi : 0xFFFFFFFFu;
 
     // parser state
     uint32_t s = 0, pd = 0, rem = 0, eff = 0;
-    bool islit = false, pdone = false, bad = false;
-    // emitter state
-    uint32_t d = 0, fl = 0;
+    bool islit = false, bad = false;
+    bool pdone = !live || slen == 0;
+    // emitter state: d = bytes emitted, fb = flushed bytes (multiple of 64)
+    uint32_t d = 0, fb = 0;
     uint4 stage = zero4();
 
-    Slot S0, S1, S2;
-    {
-        const uint4 c0 = sa[0];
-        for (Slot* S : {&S0, &S1, &S2}) {
-            S->in = c0;
-            S->in_c = kNoChunk;
-            S->far = zero4();
-            S->lit = zero4();
-            S->n = 0;
-            S->q = 0;
-            S->kind = 0;
-        }
+    Slot S0, S1, S2, S3;
+    for (Slot* S : {&S0, &S1, &S2, &S3}) {
+        S->in = zero4();
+        S->in_c = kNoChunk;
+        S->far = zero4();
+        S->lit = zero4();
+        S->n = 0;
+        S->q = 0;
+        S->kind = 1;
     }
     uint32_t drain = 0;
 
-    auto step = [&](Slot& S) {
+    auto step = [&](Slot& S, const uint32_t j) {
+        drain += pdone ? 1u : 0u;
         // 1. land the input chunk loaded kD iterations ago
-        if (S.in_c != kNoChunk) {
-            *L.in(S.in_c) = S.in;
-            whi = S.in_c + 1;
-        }
+        const bool landed = S.in_c != kNoChunk;
+        if (landed) *L.in(S.in_c) = S.in;
+        whi = landed ? S.in_c + 1 : whi;
 
         // 2. emit the piece parsed kD iterations ago (a bubble appends nothing)
         {
-            uint4 v = L.out16(S.q);
-            v = make_uint4(S.kind == 2 ? S.far.x : v.x, S.kind == 2 ? S.far.y : v.y, S.kind == 2 ? S.far.z : v.z,
-                           S.kind == 2 ? S.far.w : v.w);
-            v = make_uint4(S.kind == 0 ? S.lit.x : v.x, S.kind == 0 ? S.lit.y : v.y, S.kind == 0 ? S.lit.z : v.z,
-                           S.kind == 0 ? S.lit.w : v.w);
-            const uint32_t n = S.n, r = d & 15u;
-            v = keep_bytes(v, n);
-            const uint4 lo = or4(stage, shl_bytes(v, r));
-            const uint4 hi = shr_bytes(v, 16 - r);
+            const uint4 h = L.out16(S.q);
+            const uint4 v = keep_bytes(sel4(S.kind == 0, S.lit, sel4(S.kind == 2, S.far, h)), S.n);
+            const uint32_t r = d & 15u;
+            uint4 lo, hi;
+            place16(v, r, lo, hi);
+            lo = or4(stage, lo);
             *L.out(d) = lo;       // chunk holding d: staged head + new bytes
             *L.out(d + 16) = hi;  // next chunk: only bytes not yet final
-            const bool roll = r + n >= 16;
-            stage = make_uint4(roll ? hi.x : lo.x, roll ? hi.y : lo.y, roll ? hi.z : lo.z, roll ? hi.w : lo.w);
-            d += n;
+            stage = sel4(r + S.n >= 16, hi, lo);
+            d += S.n;
         }
 
-        // 3. flush one completed 16-byte chunk (placeholder: the sink line)
+        // 3. cooperative flush: lane writes 16 bytes of owner o's next 64-byte block if complete
         {
-            const bool full = fl + 16 <= d;
-            const uint4 fv = *L.out(fl);
-            stu16(full ? gout + fl : sink, fv);
-            fl += full ? 16u : 0u;
+            const uint32_t o = 16u * (j & 3u) + (lane >> 2), part = lane & 3u;
+            const bool ready = d - fb >= 64;
+            const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
+            const uint32_t glo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)R.o0);
+            const uint32_t ghi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)(R.o0 >> 32));
+            const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
+            const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
+            stu16((ofb >> 31) ? out + ((((uint64_t)ghi << 32) | glo) + pos) : sink, fv);
+            fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
         }
 
-        // 4. parse the next piece into this slot
-        uint32_t n = 0, q = 0, kind = 0;
-        uint4 lit = zero4();
-        if (!pdone) {
-            if (rem == 0) {  // element header: bytes s .. s+4 must have landed
-                const uint32_t pos = so + s;
-                if (min((pos + 4) >> 4, lastc) < whi) {
-                    const uint4 W = L.in16(pos);
-                    const uint32_t tag = W.x & 0xFF, t = tag & 3, x = tag >> 2;
-                    const uint64_t w64 = ((uint64_t)W.y << 32) | W.x;
-                    const uint32_t lit_hl = x < 60 ? 1u : x - 58u;
-                    const uint32_t ext = (uint32_t)((w64 >> 8) & ((1ull << ((8 * (lit_hl - 1)) & 63)) - 1));
-                    const uint32_t len = t == 0 ? (x < 60 ? x : ext) + 1 : (t == 1 ? 4 + (x & 7) : x + 1);
-                    const uint32_t hl = t == 0 ? lit_hl : (t == 1 ? 2u : (t == 2 ? 3u : 5u));
-                    const uint32_t o1 = ((tag & 0xE0u) << 3) | ((W.x >> 8) & 0xFF);
-                    const uint32_t o2 = (W.x >> 8) & 0xFFFF;
-                    const uint32_t o4 = (W.x >> 8) | (W.y << 24);
-                    const uint32_t off = t == 1 ? o1 : (t == 2 ? o2 : o4);
-                    islit = t == 0;
-                    // golang/snappy bounds: header bytes, literal source, copy offset, output room
-                    bad = hl > slen - s || len > dlen - pd ||
-                          (islit ? (len == 0 || len > slen - s - hl) : (off == 0 || off > pd));
-                    if (bad) {
-                        pdone = true;
-                    } else {
-                        s += hl;
-                        rem = len;
-                        eff = off;
-                    }
-                }
-            }
-            if (rem != 0) {
-                if (islit) {  // literal piece: its bytes must have landed
-                    const uint32_t pos = so + s;
-                    if (min((pos + 15) >> 4, lastc) < whi) {
-                        n = min(rem, 16u);
-                        lit = L.in16(pos);
-                        s += n;
-                    }
-                } else {  // copy piece; overlapping copies double their reach (a multiple of the offset)
-                    n = min(min(rem, 16u), eff);
-                    q = pd - eff;
-                    kind = eff > kFarOff ? 2u : 1u;
-                    eff = (eff < 16 && n == eff) ? 2 * eff : eff;
-                }
-                rem -= n;
-                pd += n;
-            }
-            if (rem == 0 && s >= slen) pdone = true;
+        // 4. parse the next piece into this slot (selects only: lanes diverge in data, not flow)
+        {
+            const uint32_t pos = so + s;
+            const uint4 W = L.in16(pos);  // input bytes [s, s + 16)
+            const bool avail = min((pos + 15) >> 4, lastc) < whi;
+            // element header at s (golang/snappy decode_other.go tag forms); every form is computed
+            // and combined with masks, so divergent tags cost no exec-mask branches
+            const uint32_t tag = W.x & 0xFF, t = tag & 3, x = tag >> 2;
+            const uint32_t m0 = 0u - (uint32_t)(t == 0), m1 = 0u - (uint32_t)(t == 1), m2 = 0u - (uint32_t)(t == 2),
+                           m3 = 0u - (uint32_t)(t == 3), mlong = 0u - (uint32_t)(x >= 60);
+            const uint32_t lit_hl = (mlong & (x - 58u)) | (~mlong & 1u);  // 1 + extra length bytes
+            const uint32_t xb = (lit_hl - 1u) * 8u;                        // 0..32 extra length bits
+            const uint32_t ext = __builtin_amdgcn_alignbyte(W.y, W.x, 1) & (xb >= 32 ? ~0u : (1u << xb) - 1u);
+            const uint32_t lit_len = ((mlong & ext) | (~mlong & x)) + 1u;
+            const uint32_t len = (m0 & lit_len) | (m1 & (4u + (x & 7u))) | ((m2 | m3) & (x + 1u));
+            const uint32_t hl = (m0 & lit_hl) | (m1 & 2u) | (m2 & 3u) | (m3 & 5u);
+            const uint32_t o1 = ((tag & 0xE0u) << 3) | ((W.x >> 8) & 0xFF);
+            const uint32_t o2 = (W.x >> 8) & 0xFFFF;
+            const uint32_t o4 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);
+            const uint32_t off = (m1 & o1) | (m2 & o2) | (m3 & o4);
+            // golang/snappy bounds: header bytes, literal source, copy offset, output room
+            const uint32_t sleft = slen - s;
+            const bool lbad = (len == 0) | (len > sleft - hl);
+            const bool cbad = (off == 0) | (off > pd);
+            const bool hbad = (hl > sleft) | (len > dlen - pd) | (t == 0 ? lbad : cbad);
+            const bool hdr = !pdone && rem == 0 && avail;
+            const bool badn = hdr && hbad, ok = hdr && !hbad;
+            bad = bad || badn;
+            const uint32_t sh = ok ? hl : 0u;
+            const uint32_t rem1 = ok ? len : rem, eff1 = ok ? off : eff;
+            const bool lit1 = ok ? t == 0 : islit;
+            // a literal piece takes the window bytes after the header; a copy piece reaches back
+            // at most `eff` bytes (overlapping copies double their reach: a multiple of the offset)
+            const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
+            const uint32_t n = go ? min(rem1, lit1 ? 16u - sh : min(16u, eff1)) : 0u;
+            S.n = n;
+            S.q = pd - eff1;
+            S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
+            S.lit = funnel16(W, zero4(), sh);
+            s += sh + (lit1 ? n : 0u);
+            rem = rem1 - n;
+            pd += n;
+            eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
+            islit = lit1;
+            pdone = pdone || badn || (rem == 0 && s >= slen);
         }
-        S.n = n;
-        S.q = q;
-        S.kind = kind;
-        S.lit = lit;
         // far history (flushed: see header) or a placeholder load
-        S.far = ldu16(kind == 2 ? gout + q : sink);
+        S.far = ldu16(S.kind == 2 ? gout + S.q : sink);
 
         // 5. input prefetch: the next chunk if the ring has room for it when it lands
         {
@@ -205,19 +228,18 @@ __device__ bool snappy_pipe(const uint8_t* src, uint32_t slen, const LaneLds& L,
         }
     };
 
-    // one exit per kD steps: every path around the loop issues the same memory operations, so the
-    // compiler's wait counts stay exact (extra steps after the drain only emit bubbles)
-    static_assert(kD == 3, "unrolled for three slots");
+    // one exit per kD steps, taken by the whole wave: every path around the loop issues the same
+    // memory operations, so the compiler's wait counts stay exact
+    static_assert(kD == 4, "unrolled for four slots");
     do {
-        drain += pdone ? 1u : 0u;
-        step(S0);
-        drain += pdone ? 1u : 0u;
-        step(S1);
-        drain += pdone ? 1u : 0u;
-        step(S2);
-    } while (drain < kD);
+        step(S0, 0);
+        step(S1, 1);
+        step(S2, 2);
+        step(S3, 3);
+    } while (__any(drain < kD));
+    if (!live) return true;
     if (bad || d != dlen || pd != dlen) return false;
-    for (uint32_t k = fl; k < d; k += 16) {
+    for (uint32_t k = fb; k < d; k += 16) {  // the record's tail (< 128 bytes), lane by lane
         const uint4 v = *L.out(k);
         if (k + 16 <= d)
             stu16(gout + k, v);
@@ -233,17 +255,29 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
     const uint64_t n = st->n_records;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const LaneLds L{lds + wave * kWaveLds + lane * 16};
-    const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint8_t* sink = P.sink + (gtid >> 6) * 64;  // the wave's placeholder line
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = gtid; i < n; i += stride) {
-        if (P.flags[i] & RIO_FLAG_NIL) continue;
-        const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
-        if (slen > 0xFFFFFFFFull) continue;  // k_snappy_global
-        const uint64_t o0 = P.out_off[i], olen = P.out_off[i + 1] - o0;
-        const uint8_t* src = P.file + P.rec_off[i] + (pay & 0xFF);
-        if (!snappy_pipe(src, (uint32_t)slen, L, P.out + o0, (uint32_t)olen, sink))
+    uint8_t* const wl = lds + wave * kWaveLds;
+    const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    uint8_t* sink = P.sink + gwave * 64;  // the wave's placeholder line
+    for (uint64_t b = gwave; b * 64 < n; b += nwaves) {  // wave-uniform batches of 64 records
+        const uint64_t i = b * 64 + lane;
+        Rec R{};
+        bool live = false;
+        if (i < n && !(P.flags[i] & RIO_FLAG_NIL)) {
+            const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
+            if (slen <= 0xFFFFFFFFull) {  // longer streams: k_snappy_global
+                const uint64_t o0 = P.out_off[i];
+                const uint8_t* src = P.file + P.rec_off[i] + (pay & 0xFF);
+                R.so = (uint32_t)((uintptr_t)src & 15u);
+                R.sa = reinterpret_cast<const uint4*>(src - R.so);
+                R.slen = (uint32_t)slen;
+                R.dlen = (uint32_t)(P.out_off[i + 1] - o0);
+                R.lastc = slen ? (R.so + R.slen - 1) >> 4 : 0u;
+                R.o0 = o0;
+                live = true;
+            }
+        }
+        if (!snappy_wave(R, live, wl, lane, P.out, sink))
             atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)i);
     }
 }
