@@ -64,7 +64,7 @@ struct ScanState {
     uint64_t n_repairs;
     uint64_t decode_err_rec;  // min record index that failed to decompress (kNone = none)
     uint32_t capacity_fail;
-    uint32_t pad;
+    uint32_t huge_streams;  // a record stream exceeds 32-bit positions: k_snappy_global runs
 };
 
 // Result of the single-record (ReadNextAt) kernel.

@@ -255,6 +255,7 @@ __global__ void k_header(FrameParams P) {
     st->n_repairs = 0;
     st->decode_err_rec = kNone;
     st->capacity_fail = 0;
+    st->huge_streams = 0;
     st->slow = 0;
     if (P.len < RIO_FILE_HEADER_BYTES) {
         st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;

@@ -265,7 +265,9 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
         bool live = false;
         if (i < n && !(P.flags[i] & RIO_FLAG_NIL)) {
             const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
-            if (slen <= 0xFFFFFFFFull) {  // longer streams: k_snappy_global
+            if (slen > 0xFFFFFFFFull) {  // longer streams: k_snappy_global
+                atomicOr(&st->huge_streams, 1u);
+            } else {
                 const uint64_t o0 = P.out_off[i];
                 const uint8_t* src = P.file + P.rec_off[i] + (pay & 0xFF);
                 R.so = (uint32_t)((uintptr_t)src & 15u);
@@ -284,7 +286,8 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
 
 __global__ void __launch_bounds__(256) k_snappy_global(FrameParams P) {
     ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->huge_streams)
+        return;
     const uint64_t n = st->n_records;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {

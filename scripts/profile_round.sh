@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round evidence on one GPU box: GPU tests, smoke, the default bench line, the rocprofv3 kernel-trace
+# summary of the same command, and the FETCH_SIZE / WRITE_SIZE passes that give the decode kernel's
+# HBM traffic (scripts/traffic.py). Every GPU step has its own time limit; a fault, abort or
+# timeout ends the script. usage: scripts/profile_round.sh <tag> [config]
+set -u
+TAG=$1; CFG=${2:-c2}
+OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
+fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
+step() {
+    local name=$1 to=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"; tail -3 "$OUT/$name.log"
+    if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+step tests 900 python -m pytest tests -m gpu -x -q
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py --config "$CFG"
+grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
+step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python bench.py --config "$CFG" --no-cpu-baseline --no-e2e
+find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
+step pmc_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
+    python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
+step pmc_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
+    python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
+python scripts/traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$CFG" k_snappy_pipe "$OUT/traffic.json"
+echo done

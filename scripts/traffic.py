@@ -1,0 +1,49 @@
+"""HBM traffic of the dominant decode kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+Per MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB counted at the L2's
+memory side; on gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads, so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane stores. bench.py's first decode launch is a
+capacity probe that decodes nothing, so the per-launch value is the maximum over dispatches.
+
+usage: python scripts/traffic.py <fetch_pass_dir> <write_pass_dir> <config> <kernel-substring> <out.json>
+"""
+import csv
+import glob
+import json
+import sys
+
+
+def counter(root, name, kernel):
+    vals = []
+    for path in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(path)):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == name:
+                vals.append(float(row["Counter_Value"]))
+    if not vals:
+        raise SystemExit(f"no {name} samples for {kernel} under {root}")
+    return max(vals), len(vals)
+
+
+def main():
+    fdir, wdir, cfg, kernel, out = sys.argv[1:6]
+    fetch_kib, nf = counter(fdir, "FETCH_SIZE", kernel)
+    write_kib, nw = counter(wdir, "WRITE_SIZE", kernel)
+    read_bytes = 2.0 * fetch_kib * 1024  # gfx950: FETCH_SIZE = 1/2 of wide streaming-read bytes
+    write_bytes = write_kib * 1024
+    doc = {
+        "config": cfg,
+        "kernel": kernel,
+        "fetch_size_kib": fetch_kib,
+        "write_size_kib": write_kib,
+        "dispatches": {"fetch": nf, "write": nw},
+        "hbm_read_bytes": read_bytes,
+        "hbm_write_bytes": write_bytes,
+        "decode_kernel_bytes_per_launch": read_bytes + write_bytes,
+        "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), max over dispatches, separate --pmc passes",
+    }
+    json.dump(doc, open(out, "w"), indent=1)
+    print(json.dumps(doc))
+
+
+if __name__ == "__main__":
+    main()
