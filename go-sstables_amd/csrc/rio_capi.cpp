@@ -125,7 +125,7 @@ struct rio_ctx {
     // timing ring: slot i holds the 5 stage events of the i-th decode since rio_ctx_set_timing
     std::vector<std::array<hipEvent_t, 5>> ev;
     uint64_t ev_cursor = 0;
-    uint64_t chunk_bytes = 4096;
+    uint64_t chunk_bytes = 32768;
     hipEvent_t* next_events() {
         if (ev.empty()) return nullptr;
         return ev[ev_cursor++ % ev.size()].data();
@@ -205,8 +205,8 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     HIP_TRY(hipSetDevice(device));
     auto* c = new rio_ctx();
     c->device = device;
-    c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 4096);
-    if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 4096;
+    c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 32768);
+    if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RIO_ERR_HIP;

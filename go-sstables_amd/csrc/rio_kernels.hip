@@ -149,13 +149,48 @@ __device__ __forceinline__ uint32_t crc_after_magic() {
     return crc32c_byte(c, 0x4C);
 }
 
+// CRC-32C slice-by-4 over LDS tables T[0..1023] (T0..T3, reflected polynomial 0x82F63B78):
+// n <= 16 bytes given little-endian in x0 (bytes 0..7) and x1 (bytes 8..15). Register state in/out.
+__device__ __forceinline__ uint32_t crc32c_tab(uint32_t c, uint64_t x0, uint64_t x1, uint32_t n, const uint32_t* T) {
+    uint32_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const uint32_t w = c ^ (uint32_t)((i < 8 ? x0 >> (8 * i) : x1 >> (8 * (i - 8))));
+        c = T[768 + (w & 0xFF)] ^ T[512 + ((w >> 8) & 0xFF)] ^ T[256 + ((w >> 16) & 0xFF)] ^ T[w >> 24];
+    }
+    for (; i < n; i++) {
+        const uint32_t b = (uint32_t)((i < 8 ? x0 >> (8 * i) : x1 >> (8 * (i - 8)))) & 0xFF;
+        c = T[(c ^ b) & 0xFF] ^ (c >> 8);
+    }
+    return c;
+}
+
+// Build the slice-by-4 tables in LDS (blockDim.x >= 256); ends with a workgroup barrier.
+__device__ void crc32c_tab_init(uint32_t* T) {
+    const uint32_t i = threadIdx.x;
+    if (i < 256) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+        T[i] = c;
+    }
+    __syncthreads();
+    if (i < 256) {
+        uint32_t c = T[i];
+        for (int k = 1; k < 4; k++) {
+            c = (c >> 8) ^ T[c & 0xFF];
+            T[256 * k + i] = c;
+        }
+    }
+    __syncthreads();
+}
+
 // FileReader sequential semantics at record start p: header + payload availability + decoded
 // size. next = start of the following record; pay = rec_pay descriptor (rio_device.h).
 // Common records (canonical magic, header + preamble inside 32 bytes, valid) are parsed from two
 // 16-byte loads; everything else (and every failure, for its exact classification) takes the
 // byte-wise ReadUvarint restatement.
 __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t ver, uint32_t comp,
-                            Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay) {
+                            Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay,
+                            const uint32_t* crct = nullptr) {
     if (p + 32 <= len) {
         const uint4 a = ldu16(f + p), b = ldu16(f + p + 16);
         const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -168,9 +203,14 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
             uint32_t act = 0;
             if (ok && ver == RIO_VERSION4) {
                 const uint32_t ncrc = varint8(win8(w, hl), crc);
-                uint32_t cs = crc32c_byte(crc_after_magic(), (a.x >> 24) & 0xFF);
-                cs = crc32c_bytes(cs, win8(w, 4), nu);
-                cs = crc32c_bytes(cs, win8(w, 4 + nu), nc);
+                uint32_t cs;
+                if (crct && nu + nc <= 15) {  // nil byte + both varints: bytes [3, 4 + nu + nc)
+                    cs = crc32c_tab(crc_after_magic(), win8(w, 3), win8(w, 11), 1 + nu + nc, crct);
+                } else {
+                    cs = crc32c_byte(crc_after_magic(), (a.x >> 24) & 0xFF);
+                    cs = crc32c_bytes(cs, win8(w, 4), nu);
+                    cs = crc32c_bytes(cs, win8(w, 4 + nu), nc);
+                }
                 act = cs ^ 0xFFFFFFFFu;
                 ok = ncrc && act == crc;
                 hl += ncrc;
@@ -316,62 +356,266 @@ __device__ uint64_t find_entry(const FrameParams& P, uint64_t cs, uint64_t ce, u
     return kNone;
 }
 
-// Walk chunk c from record start `from` (kNone => nothing to walk), filling its scratch slots.
-__device__ void walk_chunk(const FrameParams& P, uint64_t c, uint64_t from, uint32_t ver, uint32_t comp) {
+// Continue walking chunk c from record start p (count/bytes already in s), filling its scratch
+// slots; sets s.exit / s.status. Serial header-to-header hops (FileReader order).
+__device__ void walk_from(const FrameParams& P, uint64_t c, uint64_t p, uint32_t ver, uint32_t comp, ChunkSum& s) {
     const uint64_t ce = chunk_end(P, c);
+    uint64_t* so = P.scratch_off + c * P.slots;
+    uint64_t* sl = P.scratch_len + c * P.slots;
+    uint64_t* sp = P.scratch_pay + c * P.slots;
+    while (p < ce) {
+        Hdr h;
+        uint64_t next = 0, olen = 0, pd = 0;
+        int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd);
+        if (e) {
+            s.status = e;
+            s.err_off = p;
+            if (e == RIO_ERR_HEADER_CRC) {
+                s.det0 = h.exp_crc;
+                s.det1 = h.act_crc;
+            } else if (e == RIO_ERR_MAGIC) {
+                s.det0 = h.magic_len;
+            } else if (e == RIO_ERR_UNEXPECTED_EOF && h.hdr_len != 0) {
+                s.det0 = 1;  // raised by the payload read, not by a header varint
+            }
+            break;
+        }
+        if (s.count < P.slots) {
+            so[s.count] = p;
+            sl[s.count] = olen | (h.nil ? kNilBit : 0);
+            sp[s.count] = pd;
+        }
+        s.count++;
+        s.bytes += olen;
+        p = next;
+    }
+    s.exit = s.status ? s.err_off : p;
+}
+
+__device__ __forceinline__ ChunkSum chunk_sum_empty(uint64_t entry) {
     ChunkSum s;
-    s.entry = from;
+    s.entry = entry;
     s.exit = kNone;
     s.bytes = 0;
     s.err_off = 0;
     s.det0 = s.det1 = 0;
     s.count = 0;
     s.status = RIO_OK;
-    if (from != kNone) {
-        uint64_t p = from;
-        uint64_t* so = P.scratch_off + c * P.slots;
-        uint64_t* sl = P.scratch_len + c * P.slots;
-        uint64_t* sp = P.scratch_pay + c * P.slots;
-        while (p < ce) {
-            Hdr h;
-            uint64_t next = 0, olen = 0, pd = 0;
-            int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd);
-            if (e) {
-                s.status = e;
-                s.err_off = p;
-                if (e == RIO_ERR_HEADER_CRC) {
-                    s.det0 = h.exp_crc;
-                    s.det1 = h.act_crc;
-                } else if (e == RIO_ERR_MAGIC) {
-                    s.det0 = h.magic_len;
-                } else if (e == RIO_ERR_UNEXPECTED_EOF && h.hdr_len != 0) {
-                    s.det0 = 1;  // raised by the payload read, not by a header varint
-                }
-                break;
-            }
-            if (s.count < P.slots) {
-                so[s.count] = p;
-                sl[s.count] = olen | (h.nil ? kNilBit : 0);
-                sp[s.count] = pd;
-            }
-            s.count++;
-            s.bytes += olen;
-            p = next;
-        }
-        s.exit = s.status ? s.err_off : p;
-    }
+    return s;
+}
+
+// Walk chunk c from record start `from` (kNone => nothing to walk), filling its scratch slots.
+__device__ void walk_chunk(const FrameParams& P, uint64_t c, uint64_t from, uint32_t ver, uint32_t comp) {
+    ChunkSum s = chunk_sum_empty(from);
+    if (from != kNone) walk_from(P, c, from, ver, comp, s);
     P.chunks[c] = s;
 }
 
-__global__ void __launch_bounds__(256) k_walk(FrameParams P) {
-    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= P.n_chunks) return;
+// Wave-wide exclusive prefix sum (64 lanes).
+template <typename T>
+__device__ __forceinline__ T wave_excl_scan(T v, uint32_t lane) {
+    T x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const T y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x - v;
+}
+
+// Cooperative chunk walk: one wave per chunk, processed in windows of up to 64 candidates.
+//   1. fill: the wave reads 4 KiB at a time (four 1 KiB coalesced blocks, loads in flight
+//      together) and compacts the positions of the canonical magic bytes 91 8d 4c (find_entry's
+//      candidates) into LDS in file order, until ~48 are listed or 16 KiB were read; a 65th
+//      candidate ends the window exactly at its position (the next window starts there);
+//   2. every listed candidate is framed at once (frame_record, one lane each, result in registers);
+//   3. the chain is followed with wave votes: the entry is the first candidate that frames
+//      (find_entry); a run of candidates chains while each record's successor is the next
+//      candidate; a record whose successor skips candidates (magic bytes inside its payload)
+//      restarts the vote at its successor. Windows the chain jumps over (long records) are not
+//      read. Wherever the chain leaves the candidates (a header that fails, a non-canonical magic
+//      encoding) lane 0 takes over with the serial walk (walk_from) for the rest of the chunk.
+// Result and slots are identical to find_entry + walk_chunk (the serial thread-per-chunk walk,
+// which paid ~50 dependent global round trips per 4 KiB chunk).
+constexpr uint32_t kWalkWaves = 4;      // chunks per workgroup
+constexpr uint32_t kWalkFill = 48;      // stop filling a window at this many candidates
+constexpr uint32_t kWalkFillMax = 4;    // ... or after this many 4 KiB fill rounds
+
+struct WalkLds {
+    uint64_t pos[64];
+    uint64_t overflow;  // first candidate beyond the 64 listed (kNone if none)
+};
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_ffs(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+
+// exact per-byte equality with a byte value: bit 7 of every byte of the result = (byte == v)
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t d, uint32_t v4) {
+    const uint32_t x = d ^ v4;
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+
+// candidate bits of the 16 positions q .. q+15 in [lo, hi) (91 8d 4c at the position, the magic
+// inside the file); d = the 16 bytes at q plus the next 4
+__device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t q, uint64_t lo, uint64_t hi,
+                                               uint64_t len) {
+    // positions holding 0x91 (SWAR exact byte compare, byte high bits gathered into 16 bits); only
+    // those (~1 in 256 bytes) get the full 3-byte test
+    uint32_t m91 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++)
+        m91 |= (((bytes_eq(d[k], 0x91919191u) & 0x80808080u) * 0x00204081u) >> 28) << (4 * k);
+    const uint32_t a = lo > q ? (uint32_t)min(lo - q, (uint64_t)16) : 0u;
+    const uint32_t b = hi > q ? (uint32_t)min(hi - q, (uint64_t)16) : 0u;
+    m91 &= (b >= 16 ? 0xFFFFu : (1u << b) - 1u) & ~(a >= 16 ? 0xFFFFu : (1u << a) - 1u);
+    uint32_t mask = 0;
+    while (m91) {
+        const uint32_t i = __ffs(m91) - 1;
+        m91 &= m91 - 1;
+        const uint32_t k = i >> 2;  // select, not index: no scratch array
+        const uint32_t d0 = k == 0 ? d[0] : (k == 1 ? d[1] : (k == 2 ? d[2] : d[3]));
+        const uint32_t d1 = k == 0 ? d[1] : (k == 1 ? d[2] : (k == 2 ? d[3] : d[4]));
+        const uint32_t x = __builtin_amdgcn_alignbyte(d1, d0, i & 3) & 0xFFFFFFu;
+        if (x == 0x4C8D91u && q + i + 2 < len) mask |= 1u << i;
+    }
+    return mask;
+}
+
+__global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
+    __shared__ WalkLds W[kWalkWaves];
+    __shared__ uint32_t crct[1024];
+    crc32c_tab_init(crct);
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
     const ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK) return;
+    if (c >= P.n_chunks || st->hdr_status != RIO_OK) return;  // wave-uniform
+    WalkLds& L = W[wv];
     const uint32_t ver = st->version, comp = st->compression;
     const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
-    uint64_t entry = (c == 0) ? (uint64_t)RIO_FILE_HEADER_BYTES : find_entry(P, cs, ce, ver, comp);
-    walk_chunk(P, c, entry, ver, comp);
+    const uint8_t* f = P.file;
+    uint64_t* so = P.scratch_off + c * P.slots;
+    uint64_t* sl = P.scratch_len + c * P.slots;
+    uint64_t* sp = P.scratch_pay + c * P.slots;
+    // wave-uniform chain state
+    uint64_t p = (c == 0) ? (uint64_t)RIO_FILE_HEADER_BYTES : kNone;  // next record start to chain
+    uint32_t mode = (c == 0) ? 1u : 0u;  // 0 entry search, 1 chaining, 2 serial takeover at p
+    uint64_t count = 0, bytes = 0, entry = p;
+    uint64_t ws = cs;  // window start: candidates are positions >= ws
+    while (ws < ce && mode < 2) {
+        if (mode == 1) {
+            if (p >= ce) break;
+            ws = max(ws, p);  // skip what the chain jumped over
+        }
+        // 1. fill the window [ws, we)
+        if (lane == 0) L.overflow = kNone;
+        uint32_t total = 0;
+        uint64_t rd = ws & ~15ull;  // next 16-B aligned read position
+        for (uint32_t r = 0; r < kWalkFillMax && rd < ce && total < kWalkFill && total <= 64; r++) {
+            uint4 blk[4];
+            uint32_t tail[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint64_t q = rd + 1024 * j + 16 * lane;
+                if (q < ce) {  // 16-B aligned; q + 20 <= len + RIO_DEVICE_PAD
+                    blk[j] = *reinterpret_cast<const uint4*>(f + q);
+                    tail[j] = *reinterpret_cast<const uint32_t*>(f + q + 16);
+                }
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint64_t q = rd + 1024 * j + 16 * lane;
+                uint32_t mask = 0;
+                if (q < ce) {
+                    const uint32_t d[5] = {blk[j].x, blk[j].y, blk[j].z, blk[j].w, tail[j]};
+                    mask = magic_mask(d, q, ws, ce, P.len);
+                }
+                const uint32_t cnt = __popc(mask);
+                const uint32_t excl = wave_excl_scan(cnt, lane);
+                uint32_t k = total + excl;
+                while (mask) {
+                    const uint32_t i = __ffs(mask) - 1;
+                    mask &= mask - 1;
+                    if (k < 64)
+                        L.pos[k] = q + i;
+                    else if (k == 64)
+                        L.overflow = q + i;
+                    k++;
+                }
+                total += __shfl(excl + cnt, 63);
+            }
+            rd += 4096;
+        }
+        wave_sync_lds();
+        const uint64_t overflow = L.overflow;
+        const uint64_t we = overflow != kNone ? overflow : min(rd, ce);  // window end
+        // 2. frame one candidate per lane
+        const uint32_t nst = min(total, 64u);
+        const bool have = lane < nst;
+        const uint64_t cpos = have ? L.pos[lane] : kNone;
+        Hdr h;
+        h.nil = false;
+        uint64_t nx = 0, ol = 0, pd = 0;
+        int e = RIO_ERR_MAGIC;
+        if (have) e = frame_record(f, P.len, cpos, ver, comp, h, nx, ol, pd, crct);
+        const bool ok = have && e == RIO_OK;
+        const uint64_t ok_mask = __ballot(ok);
+        const uint64_t succ_pos = __shfl_down(cpos, 1);  // next candidate's position
+        // 3. entry and chain by votes
+        if (mode == 0) {
+            const uint32_t k = lane_ffs(ok_mask);
+            if (k < 64) {
+                p = __shfl(cpos, k);
+                mode = 1;
+            }
+            entry = p;
+        }
+        uint32_t slot = ~0u;
+        while (mode == 1 && p < we) {
+            // the candidate at p, if listed and framed
+            const uint32_t e0 = lane_ffs(__ballot(have && cpos >= p));
+            if (e0 >= nst || __shfl(cpos, e0) != p || !((ok_mask >> e0) & 1)) {
+                mode = 2;  // serial takeover at p
+                break;
+            }
+            // maximal run e0..b where each record's successor is the next candidate
+            const bool link = ok && lane + 1 < nst && nx == succ_pos;
+            const uint64_t brk = ~__ballot(link) & (~0ull << e0);
+            const uint32_t b = lane_ffs(brk);  // first non-linking candidate (< nst: lane nst-1 never links)
+            // b is reached by the chain; if its header fails, the chain stops AT it (serial takeover
+            // classifies the error), else b is the run's last record
+            const bool bok = (ok_mask >> b) & 1;
+            const uint32_t last = bok ? b : b - 1;  // b > e0 when !bok (e0 frames)
+            if (lane >= e0 && lane <= last) slot = (uint32_t)count + (lane - e0);
+            count += last - e0 + 1;
+            p = bok ? __shfl(nx, b) : __shfl(cpos, b);
+        }
+        // 4. scratch slots of the chained candidates + their decoded bytes
+        const uint64_t mylen = slot != ~0u ? ol : 0;
+        if (slot != ~0u && slot < P.slots) {
+            so[slot] = cpos;
+            sl[slot] = ol | (h.nil ? kNilBit : 0);
+            sp[slot] = pd;
+        }
+        bytes += __shfl(wave_excl_scan(mylen, lane) + mylen, 63);
+        wave_sync_lds();
+        ws = we;
+    }
+    // 5. serial takeover where the chain left the candidates; the chunk summary
+    if (lane == 0) {
+        ChunkSum s = chunk_sum_empty(entry);
+        s.count = (uint32_t)count;
+        s.bytes = bytes;
+        if (mode == 2)
+            walk_from(P, c, p, ver, comp, s);
+        else if (entry != kNone)
+            s.exit = p;  // the chain left the chunk (or ended at the file end) cleanly
+        P.chunks[c] = s;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -556,11 +800,14 @@ __global__ void __launch_bounds__(1024) k_scan_top(FrameParams P) {
     if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
 }
 
-// Placement: one thread per chunk copies its owned scratch records to the global index.
+// Placement: one wave per chunk copies its owned scratch records to their global index (64
+// records per step, out_off by a wave prefix sum: coalesced stores instead of one thread's serial
+// record loop).
 __global__ void __launch_bounds__(256) k_place(FrameParams P) {
-    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const ScanState* st = P.state;
-    if (c >= P.n_chunks || st->hdr_status != RIO_OK) return;
+    if (c >= P.n_chunks || st->hdr_status != RIO_OK) return;  // wave-uniform
     ChunkPlace pl;
     if (st->slow) {
         pl = P.place[c];
@@ -581,22 +828,27 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
             const ChunkSum s = P.chunks[c];
             if (s.entry != kNone && y == s.entry) pl.owned = s.count;
         }
-        P.place[c] = pl;
+        if (lane == 0) P.place[c] = pl;
     }
     if (pl.owned == 0) return;
     if (pl.base_idx + pl.owned > P.rec_cap || st->n_records > P.rec_cap) return;
     const uint64_t* so = P.scratch_off + c * P.slots;
     const uint64_t* sl = P.scratch_len + c * P.slots;
     const uint64_t* sp = P.scratch_pay + c * P.slots;
-    uint64_t ob = pl.base_bytes;
-    for (uint64_t k = 0; k < pl.owned; k++) {
-        const uint64_t i = pl.base_idx + k;
-        const uint64_t l = sl[k];
-        P.rec_off[i] = so[k];
-        P.rec_pay[i] = sp[k];
-        P.out_off[i] = ob;
-        P.flags[i] = (l & kNilBit) ? RIO_FLAG_NIL : 0;
-        ob += l & ~kNilBit;
+    uint64_t carry = pl.base_bytes;
+    for (uint64_t k0 = 0; k0 < pl.owned; k0 += 64) {
+        const uint64_t k = k0 + lane;
+        const bool v = k < pl.owned;
+        const uint64_t l = v ? sl[k] : 0, len = l & ~kNilBit;
+        const uint64_t excl = wave_excl_scan(len, lane);
+        if (v) {
+            const uint64_t i = pl.base_idx + k;
+            P.rec_off[i] = so[k];
+            P.rec_pay[i] = sp[k];
+            P.out_off[i] = carry + excl;
+            P.flags[i] = (l & kNilBit) ? RIO_FLAG_NIL : 0;
+        }
+        carry += __shfl(excl + len, 63);
     }
 }
 
@@ -860,7 +1112,7 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], s);
     hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, P);
-    hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, 256)), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, P);
@@ -876,7 +1128,7 @@ hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s);  // rio_sn
 // Phase B: placement into the caller's arrays, decode, final result. Both decoders check the
 // file's compression type on the device and exit at once when it is not theirs.
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
-    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 256)), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
     hipLaunchKernelGGL(k_post_scan, dim3(1), dim3(64), 0, s, P);
     if (ev) (void)hipEventRecord(ev[3], s);
     hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);

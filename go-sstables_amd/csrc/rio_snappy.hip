@@ -67,6 +67,15 @@ __device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& h
     hi = sel4(r != 0, b, a);
 }
 
+// cache policy experiment knob (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads
+#ifndef RIO_NT
+#define RIO_NT 0
+#endif
+__device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
+    if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
+}
+__device__ __forceinline__ uint4 ld_far(const uint8_t* p) { return (RIO_NT & 2) ? ldu16_nt(p) : ldu16(p); }
+
 // per-lane view of the wave's chunk-interleaved LDS image
 struct LaneLds {
     uint8_t* p;  // wave image + lane * 16
@@ -165,7 +174,7 @@ __device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane,
             const uint32_t ghi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)(R.o0 >> 32));
             const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
             const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
-            stu16((ofb >> 31) ? out + ((((uint64_t)ghi << 32) | glo) + pos) : sink, fv);
+            st_out((ofb >> 31) ? out + ((((uint64_t)ghi << 32) | glo) + pos) : sink, fv);
             fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
         }
 
@@ -216,7 +225,7 @@ __device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane,
             pdone = pdone || badn || (rem == 0 && s >= slen);
         }
         // far history (flushed: see header) or a placeholder load
-        S.far = ldu16(S.kind == 2 ? gout + S.q : sink);
+        S.far = ld_far(S.kind == 2 ? gout + S.q : sink);
 
         // 5. input prefetch: the next chunk if the ring has room for it when it lands
         {

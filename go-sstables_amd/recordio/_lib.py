@@ -11,7 +11,8 @@ import os
 from ctypes import POINTER, c_char_p, c_float, c_int, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "librio.so"))
+# RIO_LIB_PATH: load an experiment build (csrc/Makefile `variant`) instead of the in-tree library
+LIB_PATH = os.environ.get("RIO_LIB_PATH") or os.path.normpath(os.path.join(_HERE, "..", "librio.so"))
 
 # status codes (rio.h rio_status)
 RIO_OK = 0

@@ -64,7 +64,7 @@ def test_repairs_happen_and_stay_exact():
     assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), "embedded")
 
 
-@pytest.mark.parametrize("chunk", [64, 256, 1024, 65536])
+@pytest.mark.parametrize("chunk", [64, 256, 1024, 4096, 65536])
 def test_chunk_size_independent(chunk, monkeypatch):
     """The result does not depend on the framing chunk size (speculation granularity)."""
     import ctypes
