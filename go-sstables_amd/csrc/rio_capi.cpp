@@ -143,7 +143,7 @@ struct rio_ctx {
         ev_cursor = 0;
     }
     // framing arenas
-    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, sink, chunks, block_runs, chunk_excl, place, block_excl, state, info;
+    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, sink, chunks, block_runs, chunk_excl, place, block_excl, state, info;
     // host-API arenas
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
     uint8_t* pinned[2] = {nullptr, nullptr};
@@ -220,7 +220,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->sink, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
+    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->rec_desc, &c->sink, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
                       &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
                       &c->readat_out, &c->readat_res, &c->seek_off})
         b->release();
@@ -283,6 +283,8 @@ extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t l
     P.info = d_info;
     HIP_TRY(ctx->rec_pay.ensure((rec_cap + 1) * 8));
     P.rec_pay = ctx->rec_pay.as<uint64_t>();
+    HIP_TRY(ctx->rec_desc.ensure((rec_cap + 1) * 16));
+    P.rec_desc = ctx->rec_desc.as<uint4>();
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     hipEvent_t* ev = ctx->next_events();
     HIP_TRY(launch_phase_a(P, s, ev));
@@ -398,6 +400,8 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
     P.rec_cap = n;
     HIP_TRY(ctx->rec_pay.ensure((n + 1) * 8));
     P.rec_pay = ctx->rec_pay.as<uint64_t>();
+    HIP_TRY(ctx->rec_desc.ensure((n + 1) * 16));
+    P.rec_desc = ctx->rec_desc.as<uint4>();
     HIP_TRY(launch_phase_b(P, ctx->stream, ctx->same_events()));
     rio_file_info fin{};
     HIP_TRY(hipMemcpyAsync(&fin, P.info, sizeof fin, hipMemcpyDeviceToHost, ctx->stream));

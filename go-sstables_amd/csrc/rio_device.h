@@ -91,6 +91,9 @@ struct FrameParams {
     // start to the first payload byte the decoder consumes (header + snappy preamble), bits 8..63
     // = length of the consumed payload stream (snappy element stream / raw payload)
     uint64_t* rec_pay;
+    // internal per-record decode descriptor [rec_cap] (Snappy decode): x,y = file offset of the
+    // element stream (lo, hi), z = stream length, w = decoded length
+    uint4* rec_desc;
     uint8_t* sink;           // [kSinkBytes] placeholder-store target of the Snappy decode pipeline
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)

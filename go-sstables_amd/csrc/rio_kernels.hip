@@ -843,10 +843,13 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
         const uint64_t excl = wave_excl_scan(len, lane);
         if (v) {
             const uint64_t i = pl.base_idx + k;
-            P.rec_off[i] = so[k];
-            P.rec_pay[i] = sp[k];
+            const uint64_t ro = so[k], pay = sp[k], start = ro + (pay & 0xFF), slen = pay >> 8;
+            P.rec_off[i] = ro;
+            P.rec_pay[i] = pay;
             P.out_off[i] = carry + excl;
             P.flags[i] = (l & kNilBit) ? RIO_FLAG_NIL : 0;
+            P.rec_desc[i] = make_uint4((uint32_t)start, (uint32_t)(start >> 32), (uint32_t)slen, (uint32_t)len);
+            if ((slen | len) > 0xFFFFFFFFull) atomicOr(&P.state->huge_streams, 1u);
         }
         carry += __shfl(excl + len, 63);
     }

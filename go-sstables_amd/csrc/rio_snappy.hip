@@ -90,71 +90,91 @@ struct LaneLds {
 // one pipeline slot: a parsed piece plus the two loads issued with it
 struct Slot {
     uint4 in;       // input chunk in_c (load in flight; sink bytes when in_c == kNoChunk)
-    uint4 far;      // far-history bytes (load in flight; placeholder unless kind == 2)
+    uint4 aux;      // far-history bytes (kind 2) or the next record's descriptor (desc): in flight
     uint4 lit;      // literal bytes (kind == 0)
     uint32_t in_c;  // chunk index of `in`
     uint32_t n;     // piece length, 0 = bubble
     uint32_t q;     // source output position (kind 1)
     uint32_t kind;  // 0 literal, 1 ring copy, 2 far copy
+    uint32_t desc;  // aux carries the next record's descriptor
 };
+__device__ __forceinline__ Slot empty_slot() {
+    Slot S;
+    S.in = zero4();
+    S.in_c = kNoChunk;
+    S.aux = zero4();
+    S.lit = zero4();
+    S.n = 0;
+    S.q = 0;
+    S.kind = 1;
+    S.desc = 0;
+    return S;
+}
 }  // namespace
 
-// Per-lane record state of the pipelined decoder.
-struct Rec {
-    const uint4* sa;  // aligned base of the element stream
-    uint64_t o0;      // output offset of the record in the arena
-    uint32_t so, slen, dlen, lastc;
-};
+// Files the 32-bit lane-stream positions cannot cover take k_snappy_global.
+__device__ __forceinline__ bool snappy_wide(const FrameParams& P, const ScanState* st) {
+    return st->huge_streams || P.len >= 0xFFFFFF00ull || st->total_bytes >= 0xFFFFFF00ull;
+}
 
-// Decode the 64 records of one wave batch, one per lane (`live` = the lane holds a record). The
-// loop runs until every lane of the wave is done: finished lanes keep stepping as bubbles because
+// Decode the contiguous record range [r0, r1) of this lane as ONE stream: consecutive records are
+// contiguous in the output arena and separated only by their headers in the file, so the lane's
+// pipeline never drains between records; positions are relative to the lane's aligned input base
+// and to its output base out_off[r0]. Copy offsets stay record-relative (golang/snappy bounds per
+// record); the next record's descriptor travels in the far-load slot of a step without a far copy.
+// The loop runs until every lane of the wave is done: finished lanes keep stepping as bubbles because
 // the flush is cooperative — at step j the 16 lanes 16*(j%4) .. +15 are "owners" and every quad of
-// lanes writes one owner's next complete 64-byte block (16 B per lane, 64 contiguous bytes per
-// record): a wave store touches 16 records instead of 64, which the L2 absorbs ~3x faster.
-// Returns the lane's verdict: true = decoded, bytes [0, dlen) written.
-__device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane, uint8_t* out, uint8_t* sink) {
+// lanes writes one owner's next complete 64-byte block (16 B per lane, 64 contiguous bytes of one
+// stream): a wave store touches 16 streams instead of 64, which the L2 absorbs ~3x faster.
+// Returns false with *bad_rec = the failing record if a record does not decode.
+__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint32_t lane,
+                            uint8_t* sink, uint64_t* bad_rec) {
     const LaneLds L{wl + lane * 16};
-    const uint4* sa = R.sa;
-    const uint32_t so = R.so, slen = R.slen, dlen = R.dlen, lastc = R.lastc;
-    uint8_t* const gout = out + R.o0;  // addresses derive from the arena argument: global, not flat
+    const bool live = r0 < r1;
+    uint8_t* const out = P.out;
+    const uint4 d0 = live ? P.rec_desc[r0] : zero4();
+    const uint64_t o0 = live ? P.out_off[r0] : 0;  // lane output base (arena offset)
+    uint8_t* const gout = out + o0;
+    const uint64_t start0 = ((uint64_t)d0.y << 32) | d0.x;
+    const uint64_t base = start0 & ~15ull;  // lane input base (file offset, 16-B aligned)
+    const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
+    // chunks the prefetcher may read: up to the file end (+pad), never more than the lane needs
+    const uint32_t lastc = live && base < P.len ? (uint32_t)min((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
     // prime the input ring with chunks [0, 4)
-    const bool has_stream = live && slen != 0;
-    uint32_t whi = has_stream ? min(kInCh, lastc + 1) : 0u;  // chunks [0, whi) have landed
+    uint32_t whi = live ? min(kInCh, lastc + 1) : 0u;  // chunks [0, whi) have landed
     for (uint32_t c = 0; c < whi; c++) *L.in(c) = sa[c];
-    // next chunk to load; a lane without a stream never takes one (cn > lastc always)
-    uint32_t cn = has_stream ? whi : 0xFFFFFFFFu;
+    uint32_t cn = live ? whi : 0xFFFFFFFFu;  // next chunk to load (never for an idle lane)
 
-    // parser state
-    uint32_t s = 0, pd = 0, rem = 0, eff = 0;
-    bool islit = false, bad = false;
-    bool pdone = !live || slen == 0;
+    // record state: current record k, its input [s, s_end) and output [rd_start, rd_end)
+    uint64_t k = r0;
+    uint32_t s = (uint32_t)(start0 - base), s_end = s + d0.z;
+    uint32_t pd = 0, rd_start = 0, rd_end = d0.w;
+    uint32_t rem = 0, eff = 0;
+    bool islit = false, bad = false, pdone = !live;
+    // next record's descriptor: 0 needed, 1 in flight, 2 landed, 3 none (last record)
+    uint4 nd = zero4();
+    uint32_t nds = (live && r0 + 1 < r1) ? 0u : 3u;
     // emitter state: d = bytes emitted, fb = flushed bytes (multiple of 64)
     uint32_t d = 0, fb = 0;
     uint4 stage = zero4();
 
-    Slot S0, S1, S2, S3;
-    for (Slot* S : {&S0, &S1, &S2, &S3}) {
-        S->in = zero4();
-        S->in_c = kNoChunk;
-        S->far = zero4();
-        S->lit = zero4();
-        S->n = 0;
-        S->q = 0;
-        S->kind = 1;
-    }
+    Slot S0 = empty_slot(), S1 = empty_slot(), S2 = empty_slot(), S3 = empty_slot();
     uint32_t drain = 0;
 
-    auto step = [&](Slot& S, const uint32_t j) {
+    auto step = [&](Slot& S, const uint32_t j) __attribute__((always_inline)) {
         drain += pdone ? 1u : 0u;
         // 1. land the input chunk loaded kD iterations ago
         const bool landed = S.in_c != kNoChunk;
         if (landed) *L.in(S.in_c) = S.in;
         whi = landed ? S.in_c + 1 : whi;
+        // ... and the next record's descriptor, if this slot fetched it
+        nd = sel4(S.desc != 0, S.aux, nd);
+        nds = S.desc ? 2u : nds;
 
         // 2. emit the piece parsed kD iterations ago (a bubble appends nothing)
         {
             const uint4 h = L.out16(S.q);
-            const uint4 v = keep_bytes(sel4(S.kind == 0, S.lit, sel4(S.kind == 2, S.far, h)), S.n);
+            const uint4 v = keep_bytes(sel4(S.kind == 0, S.lit, sel4(S.kind == 2, S.aux, h)), S.n);
             const uint32_t r = d & 15u;
             uint4 lo, hi;
             place16(v, r, lo, hi);
@@ -170,8 +190,8 @@ __device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane,
             const uint32_t o = 16u * (j & 3u) + (lane >> 2), part = lane & 3u;
             const bool ready = d - fb >= 64;
             const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
-            const uint32_t glo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)R.o0);
-            const uint32_t ghi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)(R.o0 >> 32));
+            const uint32_t glo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)o0);
+            const uint32_t ghi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)(o0 >> 32));
             const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
             const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
             st_out((ofb >> 31) ? out + ((((uint64_t)ghi << 32) | glo) + pos) : sink, fv);
@@ -180,7 +200,7 @@ __device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane,
 
         // 4. parse the next piece into this slot (selects only: lanes diverge in data, not flow)
         {
-            const uint32_t pos = so + s;
+            const uint32_t pos = s;
             const uint4 W = L.in16(pos);  // input bytes [s, s + 16)
             const bool avail = min((pos + 15) >> 4, lastc) < whi;
             // element header at s (golang/snappy decode_other.go tag forms); every form is computed
@@ -198,12 +218,12 @@ __device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane,
             const uint32_t o2 = (W.x >> 8) & 0xFFFF;
             const uint32_t o4 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);
             const uint32_t off = (m1 & o1) | (m2 & o2) | (m3 & o4);
-            // golang/snappy bounds: header bytes, literal source, copy offset, output room
-            const uint32_t sleft = slen - s;
+            // golang/snappy bounds, per record: header bytes, literal source, copy offset, output room
+            const uint32_t sleft = s_end - s;
             const bool lbad = (len == 0) | (len > sleft - hl);
-            const bool cbad = (off == 0) | (off > pd);
-            const bool hbad = (hl > sleft) | (len > dlen - pd) | (t == 0 ? lbad : cbad);
-            const bool hdr = !pdone && rem == 0 && avail;
+            const bool cbad = (off == 0) | (off > pd - rd_start);
+            const bool hbad = (hl > sleft) | (len > rd_end - pd) | (t == 0 ? lbad : cbad);
+            const bool hdr = !pdone && rem == 0 && s < s_end && avail;
             const bool badn = hdr && hbad, ok = hdr && !hbad;
             bad = bad || badn;
             const uint32_t sh = ok ? hl : 0u;
@@ -222,14 +242,36 @@ __device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane,
             pd += n;
             eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
             islit = lit1;
-            pdone = pdone || badn || (rem == 0 && s >= slen);
+            pdone = pdone || badn;
+            // record boundary: stream consumed -> the record must be complete; switch to the next
+            // (its descriptor landed) or finish the range
+            const bool at_end = !pdone && rem == 0 && s == s_end;
+            const bool bad_len = at_end && pd != rd_end;  // snappy: d != len(dst) => ErrCorrupt
+            const bool more = k + 1 < r1;
+            const bool sw = at_end && !bad_len && more && nds == 2;
+            bad = bad || bad_len;
+            pdone = pdone || bad_len || (at_end && !more);
+            k += sw ? 1u : 0u;
+            const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
+            s = sw ? (uint32_t)(nstart - base) : s;
+            s_end = sw ? s + nd.z : s_end;
+            rd_start = sw ? pd : rd_start;
+            rd_end = sw ? pd + nd.w : rd_end;
+            nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
         }
-        // far history (flushed: see header) or a placeholder load
-        S.far = ld_far(S.kind == 2 ? gout + S.q : sink);
+        // far history (flushed: see header), or the next record's descriptor, or a placeholder load
+        {
+            const bool want_desc = S.kind != 2 && nds == 0;
+            S.desc = want_desc ? 1u : 0u;
+            nds = want_desc ? 1u : nds;
+            const uint8_t* ap = S.kind == 2 ? gout + S.q
+                                            : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
+            S.aux = ld_far(ap);
+        }
 
         // 5. input prefetch: the next chunk if the ring has room for it when it lands
         {
-            const uint32_t a = (so + s) >> 4;
+            const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn < a + kInCh;
             S.in = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
             S.in_c = take ? cn : kNoChunk;
@@ -246,63 +288,52 @@ __device__ bool snappy_wave(const Rec& R, bool live, uint8_t* wl, uint32_t lane,
         step(S2, 2);
         step(S3, 3);
     } while (__any(drain < kD));
-    if (!live) return true;
-    if (bad || d != dlen || pd != dlen) return false;
-    for (uint32_t k = fb; k < d; k += 16) {  // the record's tail (< 128 bytes), lane by lane
-        const uint4 v = *L.out(k);
-        if (k + 16 <= d)
-            stu16(gout + k, v);
+    // the stream's tail (< 128 bytes), lane by lane; written even after a failure: the bytes of
+    // the records before the failing one must be complete
+    for (uint32_t q = fb; q < d; q += 16) {
+        const uint4 v = *L.out(q);
+        if (q + 16 <= d)
+            stu16(gout + q, v);
         else
-            st_partial(gout + k, v, d - k);
+            st_partial(gout + q, v, d - q);
     }
-    return true;
+    *bad_rec = k;
+    return !bad;
 }
 
 __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || snappy_wide(P, st))
+        return;
     const uint64_t n = st->n_records;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint8_t* const wl = lds + wave * kWaveLds;
-    const uint64_t gwave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    uint8_t* sink = P.sink + gwave * 64;  // the wave's placeholder line
-    for (uint64_t b = gwave; b * 64 < n; b += nwaves) {  // wave-uniform batches of 64 records
-        const uint64_t i = b * 64 + lane;
-        Rec R{};
-        bool live = false;
-        if (i < n && !(P.flags[i] & RIO_FLAG_NIL)) {
-            const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
-            if (slen > 0xFFFFFFFFull) {  // longer streams: k_snappy_global
-                atomicOr(&st->huge_streams, 1u);
-            } else {
-                const uint64_t o0 = P.out_off[i];
-                const uint8_t* src = P.file + P.rec_off[i] + (pay & 0xFF);
-                R.so = (uint32_t)((uintptr_t)src & 15u);
-                R.sa = reinterpret_cast<const uint4*>(src - R.so);
-                R.slen = (uint32_t)slen;
-                R.dlen = (uint32_t)(P.out_off[i + 1] - o0);
-                R.lastc = slen ? (R.so + R.slen - 1) >> 4 : 0u;
-                R.o0 = o0;
-                live = true;
-            }
-        }
-        if (!snappy_wave(R, live, wl, lane, P.out, sink))
-            atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)i);
-    }
+    // lane number: waves are numbered across workgroups first, so that a file with few records
+    // (fewer than lanes) spreads its active waves over every CU
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (((uint64_t)wave * gridDim.x + blockIdx.x) << 6) | lane;
+    // contiguous record ranges of ceil(n / T) records: lanes of a wave cover consecutive ranges,
+    // and a file with fewer records than lanes fills whole waves (the rest exit at once)
+    const uint64_t rpl = (n + T - 1) / T;
+    const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
+    if ((t & ~63ull) * rpl >= n) return;  // the whole wave is idle (wave-uniform exit)
+    uint8_t* sink = P.sink + (t >> 6) * 64;  // the wave's placeholder line
+    uint64_t bad_rec = 0;
+    if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec))
+        atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)bad_rec);
 }
 
+// Files beyond the lane-stream kernel's 32-bit positions (>= 4 GiB of input or output, or a
+// stream over 4 GiB): every record decoded by one thread with byte loops straight to HBM.
 __global__ void __launch_bounds__(256) k_snappy_global(FrameParams P) {
     ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->huge_streams)
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !snappy_wide(P, st))
         return;
     const uint64_t n = st->n_records;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (P.flags[i] & RIO_FLAG_NIL) continue;
         const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
-        if (slen <= 0xFFFFFFFFull) continue;  // k_snappy_pipe
         const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
         if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), slen, P.out + o0, o1 - o0))
             atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)i);
