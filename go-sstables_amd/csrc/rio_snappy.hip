@@ -54,6 +54,16 @@ __device__ __forceinline__ uint4 funnel16(uint4 a, uint4 b, uint32_t r) {
                       __builtin_amdgcn_alignbyte(e3, e2, sh), __builtin_amdgcn_alignbyte(e4, e3, sh));
 }
 
+// bytes [sh, sh + 16) of the 32-byte concatenation (w, 0) for sh in [0, 7] (a literal's header
+// length): one select level instead of funnel16's two
+__device__ __forceinline__ uint4 shift_small(uint4 w, uint32_t sh) {
+    const uint32_t b = sh & 3u;
+    const bool h = (sh & 4u) != 0;
+    const uint32_t e0 = h ? w.y : w.x, e1 = h ? w.z : w.y, e2 = h ? w.w : w.z, e3 = h ? 0u : w.w;
+    return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, b), __builtin_amdgcn_alignbyte(e2, e1, b),
+                      __builtin_amdgcn_alignbyte(e3, e2, b), __builtin_amdgcn_alignbyte(0u, e3, b));
+}
+
 __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
     return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
@@ -71,6 +81,11 @@ __device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& h
 #ifndef RIO_NT
 #define RIO_NT 0
 #endif
+// timing-only experiment knobs (wrong output): 1 = no out16 funnel, 2 = no place16, 4 = no in16 funnel,
+// 8 = no flush bpermutes of the owner base
+#ifndef RIO_EXP
+#define RIO_EXP 0
+#endif
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
 }
@@ -82,9 +97,13 @@ struct LaneLds {
     __device__ uint4* out(uint32_t pos) const { return reinterpret_cast<uint4*>(p + ((pos >> 4) & (kOutCh - 1)) * 1024); }
     __device__ uint4* in(uint32_t c) const { return reinterpret_cast<uint4*>(p + (kOutCh + (c & (kInCh - 1))) * 1024); }
     // 16 bytes of history at output position q
-    __device__ uint4 out16(uint32_t q) const { return funnel16(*out(q), *out(q + 16), q & 15u); }
+    __device__ uint4 out16(uint32_t q) const {
+        return (RIO_EXP & 1) ? *out(q) : funnel16(*out(q), *out(q + 16), q & 15u);
+    }
     // 16 bytes of input at aligned-frame position pos
-    __device__ uint4 in16(uint32_t pos) const { return funnel16(*in(pos >> 4), *in((pos >> 4) + 1), pos & 15u); }
+    __device__ uint4 in16(uint32_t pos) const {
+        return (RIO_EXP & 4) ? *in(pos >> 4) : funnel16(*in(pos >> 4), *in((pos >> 4) + 1), pos & 15u);
+    }
 };
 
 // one pipeline slot: a parsed piece plus the two loads issued with it
@@ -158,6 +177,17 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     uint32_t d = 0, fb = 0;
     uint4 stage = zero4();
 
+    // output base of the owner each lane flushes for at step j (owner = 16 (j % 4) + lane / 4): the
+    // owners never change, so their bases are exchanged once instead of every step
+    uint8_t* obase[4];
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++) {
+        const int src = (int)((16u * jj + (lane >> 2)) * 4);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
+        obase[jj] = out + (((uint64_t)hi << 32) | lo);
+    }
+
     Slot S0 = empty_slot(), S1 = empty_slot(), S2 = empty_slot(), S3 = empty_slot();
     uint32_t drain = 0;
 
@@ -177,7 +207,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint4 v = keep_bytes(sel4(S.kind == 0, S.lit, sel4(S.kind == 2, S.aux, h)), S.n);
             const uint32_t r = d & 15u;
             uint4 lo, hi;
-            place16(v, r, lo, hi);
+            if (RIO_EXP & 2) { lo = v; hi = v; } else place16(v, r, lo, hi);
             lo = or4(stage, lo);
             *L.out(d) = lo;       // chunk holding d: staged head + new bytes
             *L.out(d + 16) = hi;  // next chunk: only bytes not yet final
@@ -190,11 +220,9 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t o = 16u * (j & 3u) + (lane >> 2), part = lane & 3u;
             const bool ready = d - fb >= 64;
             const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
-            const uint32_t glo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)o0);
-            const uint32_t ghi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(uint32_t)(o0 >> 32));
             const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
             const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
-            st_out((ofb >> 31) ? out + ((((uint64_t)ghi << 32) | glo) + pos) : sink, fv);
+            st_out((ofb >> 31) ? obase[j & 3u] + pos : sink, fv);
             fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
         }
 
@@ -203,26 +231,24 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t pos = s;
             const uint4 W = L.in16(pos);  // input bytes [s, s + 16)
             const bool avail = min((pos + 15) >> 4, lastc) < whi;
-            // element header at s (golang/snappy decode_other.go tag forms); every form is computed
-            // and combined with masks, so divergent tags cost no exec-mask branches
-            const uint32_t tag = W.x & 0xFF, t = tag & 3, x = tag >> 2;
-            const uint32_t m0 = 0u - (uint32_t)(t == 0), m1 = 0u - (uint32_t)(t == 1), m2 = 0u - (uint32_t)(t == 2),
-                           m3 = 0u - (uint32_t)(t == 3), mlong = 0u - (uint32_t)(x >= 60);
-            const uint32_t lit_hl = (mlong & (x - 58u)) | (~mlong & 1u);  // 1 + extra length bytes
-            const uint32_t xb = (lit_hl - 1u) * 8u;                        // 0..32 extra length bits
-            const uint32_t ext = __builtin_amdgcn_alignbyte(W.y, W.x, 1) & (xb >= 32 ? ~0u : (1u << xb) - 1u);
-            const uint32_t lit_len = ((mlong & ext) | (~mlong & x)) + 1u;
-            const uint32_t len = (m0 & lit_len) | (m1 & (4u + (x & 7u))) | ((m2 | m3) & (x + 1u));
-            const uint32_t hl = (m0 & lit_hl) | (m1 & 2u) | (m2 & 3u) | (m3 & 5u);
-            const uint32_t o1 = ((tag & 0xE0u) << 3) | ((W.x >> 8) & 0xFF);
-            const uint32_t o2 = (W.x >> 8) & 0xFFFF;
-            const uint32_t o4 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);
-            const uint32_t off = (m1 & o1) | (m2 & o2) | (m3 & o4);
-            // golang/snappy bounds, per record: header bytes, literal source, copy offset, output room
+            // element header at s (golang/snappy decode_other.go tag forms): every form is computed
+            // and combined with selects, so divergent tags cost no exec-mask branches
+            const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);  // the 4 bytes after the tag
+            const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
+            const bool is0 = t == 0, is1 = t == 1, is2 = t == 2;
+            // literal: x < 60 -> length x + 1; x in [60, 63] -> x - 59 little-endian length bytes follow
+            const bool lng = x >= 60;
+            const uint32_t lmask = 0xFFFFFFFFu >> (((63u - x) << 3) & 31u);
+            const uint32_t lit_len = (lng ? (W1 & lmask) : x) + 1u;
+            const uint32_t len = is0 ? lit_len : (is1 ? (x & 7u) + 4u : x + 1u);
+            const uint32_t hl = is0 ? (lng ? x - 58u : 1u) : (is1 ? 2u : (is2 ? 3u : 5u));
+            const uint32_t off = is1 ? (((tag & 0xE0u) << 3) | (W1 & 0xFFu)) : (is2 ? (W1 & 0xFFFFu) : W1);
+            // golang/snappy bounds, per record: header bytes present; literal source room or copy
+            // offset in [1, bytes produced] (length / offset 0 wrap to the maximum key); output room
             const uint32_t sleft = s_end - s;
-            const bool lbad = (len == 0) | (len > sleft - hl);
-            const bool cbad = (off == 0) | (off > pd - rd_start);
-            const bool hbad = (hl > sleft) | (len > rd_end - pd) | (t == 0 ? lbad : cbad);
+            const uint32_t lim = is0 ? sleft - hl : pd - rd_start;
+            const uint32_t key = (is0 ? len : off) - 1u;
+            const bool hbad = (hl > sleft) | (key >= lim) | (len > rd_end - pd);
             const bool hdr = !pdone && rem == 0 && s < s_end && avail;
             const bool badn = hdr && hbad, ok = hdr && !hbad;
             bad = bad || badn;
@@ -236,7 +262,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.n = n;
             S.q = pd - eff1;
             S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
-            S.lit = funnel16(W, zero4(), sh);
+            S.lit = shift_small(W, sh);
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
