@@ -62,7 +62,7 @@ struct ScanState {
     uint64_t det0, det1;
     uint64_t zero_from;     // zero-tail check range start (kNone = no check)
     uint64_t n_repairs;
-    uint64_t decode_err_rec;  // min record index that failed to decompress (kNone = none)
+    uint64_t decode_err_rec;  // min 2 * record + (1: cannot be placed -> unsupported) that failed (kNone = none)
     uint32_t capacity_fail;
     uint32_t huge_streams;  // a record stream exceeds 32-bit positions: k_snappy_global runs
 };

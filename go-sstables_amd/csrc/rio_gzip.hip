@@ -1,0 +1,516 @@
+// rio_gzip.hip — gzip-compressed records decoded on the device (GzipCompressor.DecompressWithBuf,
+// recordio/compressor/gzip_compression.go:54-69: Go compress/gzip Reader over compress/flate,
+// called per record by FileReader.ReadNext, file_reader.go:115-125).
+//
+// Semantics restated from the published formats and Go's reader rules:
+//   * RFC 1952 member: ID 1f 8b, CM 8, FLG with FEXTRA / FNAME / FCOMMENT (NUL-terminated, Go's
+//     512-byte buffer limit) / FHCRC (low 16 bits of the header's CRC-32), 8-byte trailer
+//     CRC-32/IEEE + ISIZE of the member's output.
+//   * RFC 1951 blocks: stored (LEN / NLEN), fixed and dynamic Huffman. Go's Huffman acceptance:
+//     HLIT <= 286, HDIST <= 30, every code complete except a single 1-bit code, empty distance
+//     codes allowed until used; symbols 286/287 and distance codes 30/31 are corrupt; a distance
+//     beyond the member's output so far is corrupt.
+// Every failure is the codec-error class (RIO_ERR_DECOMPRESS). Where this path cannot follow the
+// reader it hands the file back: a record holding more than one gzip member (Go's multistream
+// reader would go on reading), or a record announced as <= 2 KiB that decodes past the small
+// window, ends the sequence with RIO_ERR_UNSUPPORTED and the adapter keeps the reference reader.
+// Bytes decoded past the announced size are never stored; the member then fails its ISIZE check
+// exactly like Go's (gzip.ErrChecksum).
+//
+// The framing sized each record from the last four payload bytes (ISIZE of its only member).
+//
+// k_gzip_inflate<kWin>: one wavefront per record (grid-stride over records). Huffman decoding is
+// inherently serial, so the whole wave runs the decoder in lock step on wave-uniform state (bit
+// buffer, tables read from LDS as broadcasts); the lanes split the wide work: loading the input
+// into an LDS ring 1 KiB at a time, building the decode tables (ballot-based counting and
+// sorting), match copies (64 bytes per round, `k mod dist` for overlapping copies) and flushing
+// the LDS output window to HBM 1 KiB at a time. Two instantiations: records decoding to <= 2 KiB
+// keep the whole record in a 2 KiB window (many waves per CU), larger ones use the 32 KiB DEFLATE
+// window.
+// k_gzip_crc: one lane per record, CRC-32/IEEE of the decoded bytes against the trailer.
+#include <hip/hip_runtime.h>
+
+#include "rio_device.h"
+#include "rio_dev_util.h"
+
+namespace rio {
+
+namespace {
+constexpr uint32_t kGzWaves = 4;          // waves per workgroup
+constexpr uint32_t kGzIn = 2048;          // LDS input ring per wave (two 1 KiB refill blocks)
+constexpr uint32_t kGzSmallWin = 2048;    // records with decoded size <= this: whole record in LDS
+constexpr uint32_t kGzLargeWin = 32768;   // DEFLATE window (maximum distance)
+constexpr uint32_t kFastBits = 9;         // decode-table bits
+constexpr uint32_t kFastSize = 1u << kFastBits;
+constexpr uint64_t kPayFail = 1ull << 63;  // rec_pay marker: inflate failed, no CRC check
+
+// per-wave decode tables
+struct GzTables {
+    uint16_t lfast[kFastSize];  // litlen (also the code-length code): sym | len << 9, 0 = longer code
+    uint16_t dfast[kFastSize];  // distance
+    uint16_t lsym[288];         // symbols sorted by (code length, symbol)
+    uint16_t dsym[32];
+    uint16_t lcnt[16];          // codes per length
+    uint16_t dcnt[16];
+    uint8_t lens[288 + 32 + 8];  // code lengths being read (litlen then distance)
+};
+
+template <uint32_t kWin>
+struct GzLds {
+    GzTables t;
+    uint8_t in[kGzIn] __attribute__((aligned(16)));
+    uint8_t win[kWin] __attribute__((aligned(16)));
+};
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint32_t lane_mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Wave-uniform bit reader over the record's DEFLATE stream [0, slen), staged through the LDS ring.
+struct BitIn {
+    const uint8_t* src;  // stream start in HBM
+    uint8_t* ring;
+    uint32_t slen;
+    uint32_t loaded;  // stream bytes [loaded - kGzIn, loaded) are in the ring
+    uint32_t pos;     // next stream byte pulled into bb
+    uint64_t bb;
+    uint32_t nb;
+
+    // bits consumed so far (read-ahead past slen is zero-filled; overrun is checked by the caller)
+    __device__ __forceinline__ uint64_t consumed() const { return 8ull * pos - nb; }
+
+    // make stream bytes [p, p + 8) resident (1 KiB blocks, every lane loads 16 bytes)
+    __device__ void stage(uint32_t p, uint32_t lane) {
+        if (p >= loaded || p + kGzIn < loaded) loaded = p & ~1023u;  // jump (stored block skip)
+        while (loaded < p + 8 && loaded < slen) {
+            const uint32_t off = loaded + lane * 16;
+            if (off < slen) *reinterpret_cast<uint4*>(ring + (off & (kGzIn - 1))) = ldu16(src + off);
+            loaded += 1024;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    __device__ void refill(uint32_t lane) {
+        while (nb <= 32) {
+            stage(pos, lane);
+            const uint32_t a = pos & ~3u;
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(ring + (a & (kGzIn - 1)));
+            const uint32_t w1 = *reinterpret_cast<const uint32_t*>(ring + ((a + 4) & (kGzIn - 1)));
+            uint32_t v = uni(__builtin_amdgcn_alignbyte(w1, w0, pos & 3u));
+            const uint32_t valid = pos < slen ? slen - pos : 0u;
+            if (valid < 4) v &= valid == 0 ? 0u : (0xFFFFFFFFu >> (32u - 8u * valid));
+            bb |= (uint64_t)v << nb;
+            nb += 32;
+            pos += 4;
+        }
+    }
+    __device__ __forceinline__ uint32_t bits(uint32_t n) {  // n <= 32
+        const uint32_t v = (uint32_t)(bb & ((1ull << n) - 1ull));
+        bb >>= n;
+        nb -= n;
+        return v;
+    }
+    __device__ __forceinline__ bool overrun() const { return consumed() > 8ull * slen; }
+};
+
+// Canonical Huffman tables from code lengths lens[0..n) (Go huffmanDecoder.init acceptance).
+// Returns false for an invalid (over-subscribed or incomplete) code; an all-zero code is accepted
+// and fails when used.
+__device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_t* sym, uint16_t* fast,
+                         uint32_t lane) {
+    uint32_t c[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) c[l] = 0;
+    for (uint32_t g = 0; g < n; g += 64) {
+        const uint32_t s = g + lane;
+        const uint32_t L = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (int l = 1; l < 16; l++) c[l] += (uint32_t)__builtin_popcountll(__ballot(L == (uint32_t)l));
+    }
+    uint32_t maxl = 0;
+#pragma unroll
+    for (int l = 1; l < 16; l++) maxl = c[l] ? (uint32_t)l : maxl;
+    uint32_t code = 0, next[16], idx[16], acc = 0;
+#pragma unroll
+    for (int l = 1; l < 16; l++) {
+        code <<= 1;
+        next[l] = code;
+        idx[l] = acc;
+        if ((uint32_t)l <= maxl) code += c[l];
+        acc += c[l];
+    }
+    if (lane < 16) cnt[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int l = 1; l < 16; l++)
+        if (lane == (uint32_t)l) cnt[l] = (uint16_t)c[l];
+    if (maxl == 0) {
+        for (uint32_t e = lane; e < kFastSize; e += 64) fast[e] = 0;
+        __builtin_amdgcn_wave_barrier();
+        return true;
+    }
+    // complete code, or Go's exception: a single code of length 1
+    const uint32_t full = code >> (15 - maxl);  // codes counted at length maxl
+    if (full != (1u << maxl) && !(full == 1 && maxl == 1)) return false;
+    // symbols sorted by (length, symbol): rank of each symbol among equal lengths via ballots
+    uint32_t off[16];
+#pragma unroll
+    for (int l = 1; l < 16; l++) off[l] = idx[l];
+    for (uint32_t g = 0; g < n; g += 64) {
+        const uint32_t s = g + lane;
+        const uint32_t L = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (int l = 1; l < 16; l++) {
+            const uint64_t m = __ballot(L == (uint32_t)l);
+            if (L == (uint32_t)l) sym[off[l] + lane_mbcnt(m)] = (uint16_t)s;
+            off[l] += (uint32_t)__builtin_popcountll(m);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // fast table: entry e = the next kFastBits stream bits (first bit = code MSB)
+    for (uint32_t e = lane; e < kFastSize; e += 64) {
+        uint32_t v = 0, ent = 0;
+#pragma unroll
+        for (int l = 1; l <= (int)kFastBits; l++) {
+            v = (v << 1) | ((e >> (l - 1)) & 1u);
+            if (ent == 0 && v - next[l] < c[l]) ent = (uint32_t)sym[idx[l] + v - next[l]] | ((uint32_t)l << 9);
+        }
+        fast[e] = (uint16_t)ent;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
+// One symbol; -1 if the bits match no code (incomplete / empty code).
+__device__ __forceinline__ int gz_sym(BitIn& B, const uint16_t* fast, const uint16_t* cnt, const uint16_t* sym) {
+    const uint32_t e = uni(fast[(uint32_t)B.bb & (kFastSize - 1)]);
+    if (e) {
+        B.bits(e >> 9);
+        return (int)(e & 511u);
+    }
+    uint32_t code = 0, first = 0, index = 0;
+    for (uint32_t l = 1; l < 16; l++) {
+        code |= (uint32_t)(B.bb >> (l - 1)) & 1u;
+        const uint32_t c = uni(cnt[l]);
+        if (code - first < c) {
+            B.bits(l);
+            return (int)uni(sym[index + code - first]);
+        }
+        index += c;
+        first = (first + c) << 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+// DEFLATE length / distance bases (RFC 1951 3.2.5)
+__device__ __forceinline__ uint32_t len_base(uint32_t s, uint32_t& eb) {  // s in [257, 285]
+    const uint32_t i = s - 257;
+    if (i < 8) { eb = 0; return 3 + i; }
+    if (i == 28) { eb = 0; return 258; }
+    eb = (i - 4) >> 2;
+    return ((4u + (i & 3u)) << eb) + 3u;
+}
+__device__ __forceinline__ uint32_t dist_base(uint32_t s, uint32_t& eb) {  // s in [0, 29]
+    if (s < 4) { eb = 0; return s + 1; }
+    eb = (s - 2) >> 1;
+    return ((2u + (s & 1u)) << eb) + 1u;
+}
+
+enum : int { kGzOk = 0, kGzCorrupt = 1, kGzUnsupported = 2 };
+
+// Inflate one record's single gzip member into `out` (exactly dlen bytes announced by ISIZE).
+template <uint32_t kWin>
+__device__ int gz_record(GzLds<kWin>& S, const uint8_t* src, uint32_t slen, uint8_t* out, uint32_t dlen,
+                         uint32_t lane) {
+    GzTables& T = S.t;
+    BitIn B{src, S.in, slen, 0, 0, 0ull, 0};
+    B.refill(lane);
+    // ---- member header (gzip reader.go readHeader) ----
+    if (slen < 10) return kGzCorrupt;
+    const uint32_t id = B.bits(16), cm = B.bits(8), flg = B.bits(8);
+    if (id != 0x8B1Fu || cm != 8u) return kGzCorrupt;
+    B.refill(lane);
+    const uint32_t mt = B.bits(32);
+    B.refill(lane);
+    const uint32_t xo = B.bits(16);  // XFL, OS
+    // header CRC-32 (FHCRC) over every header byte read so far
+    uint32_t hcrc = 0xFFFFFFFFu;
+    auto hbyte = [&](uint32_t b) {
+        hcrc ^= b;
+#pragma unroll
+        for (int k = 0; k < 8; k++) hcrc = (hcrc >> 1) ^ (0xEDB88320u & (0u - (hcrc & 1u)));
+    };
+    hbyte(0x1F); hbyte(0x8B); hbyte(8); hbyte(flg);
+    for (int k = 0; k < 4; k++) hbyte((mt >> (8 * k)) & 0xFF);
+    hbyte(xo & 0xFF); hbyte(xo >> 8);
+    if (flg & 4u) {  // FEXTRA: XLEN + data
+        B.refill(lane);
+        const uint32_t xlen = B.bits(16);
+        hbyte(xlen & 0xFF); hbyte(xlen >> 8);
+        for (uint32_t k = 0; k < xlen; k++) {
+            B.refill(lane);
+            hbyte(B.bits(8));
+        }
+        if (B.overrun()) return kGzCorrupt;
+    }
+    for (uint32_t f = 8; f <= 16; f <<= 1) {  // FNAME, FCOMMENT: NUL-terminated, < 512 bytes
+        if (!(flg & f)) continue;
+        for (uint32_t k = 0;; k++) {
+            if (k >= 512) return kGzCorrupt;
+            B.refill(lane);
+            const uint32_t b = B.bits(8);
+            if (B.overrun()) return kGzCorrupt;
+            hbyte(b);
+            if (b == 0) break;
+        }
+    }
+    if (flg & 2u) {  // FHCRC
+        B.refill(lane);
+        const uint32_t h16 = B.bits(16);
+        if (h16 != ((hcrc ^ 0xFFFFFFFFu) & 0xFFFFu)) return kGzCorrupt;
+    }
+    if (B.overrun()) return kGzCorrupt;
+
+    // ---- DEFLATE blocks (flate inflate.go) ----
+    uint32_t d = 0, flushed = 0;
+    bool fin = false;
+    auto flush = [&](uint32_t upto) {  // window bytes [flushed, upto) -> HBM, 16 per lane
+        while (flushed < upto) {
+            const uint32_t q = flushed + lane * 16;
+            if (q < upto) {
+                const uint4 v = *reinterpret_cast<const uint4*>(S.win + (q & (kWin - 1)));
+                if (q + 16 <= upto)
+                    stu16(out + q, v);
+                else
+                    st_partial(out + q, v, upto - q);
+            }
+            flushed = min(upto, flushed + 1024);
+        }
+    };
+    while (!fin) {
+        B.refill(lane);
+        fin = B.bits(1) != 0;
+        const uint32_t type = B.bits(2);
+        if (B.overrun()) return kGzCorrupt;
+        if (type == 0) {  // stored: byte-align, LEN, NLEN, raw bytes
+            const uint32_t p = (uint32_t)((B.consumed() + 7) >> 3);
+            B.pos = p;
+            B.nb = 0;
+            B.bb = 0;
+            B.refill(lane);
+            const uint32_t ln = B.bits(16), nl = B.bits(16);
+            if (B.overrun() || (ln ^ 0xFFFFu) != nl) return kGzCorrupt;
+            const uint32_t p0 = p + 4;
+            if (ln > slen - min(slen, p0)) return kGzCorrupt;
+            if (kWin == kGzSmallWin && d + ln > kWin) return kGzUnsupported;
+            // 1 KiB at a time, flushing in between: the window never overruns unflushed bytes
+            for (uint32_t k0 = 0; k0 < ln; k0 += 1024) {
+                const uint32_t m = min(1024u, ln - k0);
+                for (uint32_t k = lane; k < m; k += 64) S.win[(d + k) & (kWin - 1)] = src[p0 + k0 + k];
+                __builtin_amdgcn_wave_barrier();
+                d += m;
+                if (kWin != kGzSmallWin && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
+            }
+            B.pos = p0 + ln;
+            B.nb = 0;
+            B.bb = 0;
+            continue;
+        }
+        if (type == 3) return kGzCorrupt;
+        if (type == 1) {  // fixed Huffman (RFC 1951 3.2.6)
+            for (uint32_t s = lane; s < 288 + 32; s += 64)
+                T.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+            __builtin_amdgcn_wave_barrier();
+            gz_build(T.lens, 288, T.lcnt, T.lsym, T.lfast, lane);
+            gz_build(T.lens + 288, 32, T.dcnt, T.dsym, T.dfast, lane);
+        } else {  // dynamic (readHuffman)
+            B.refill(lane);
+            const uint32_t nlit = B.bits(5) + 257, ndist = B.bits(5) + 1, nclen = B.bits(4) + 4;
+            if (nlit > 286 || ndist > 30) return kGzCorrupt;
+            // code-length code lengths, in the RFC's order, into lens[0..19)
+            if (lane < 19) T.lens[lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+            for (uint32_t k = 0; k < nclen; k++) {
+                B.refill(lane);
+                const uint32_t v = B.bits(3);
+                if (lane == 0) T.lens[order[k]] = (uint8_t)v;
+            }
+            if (B.overrun()) return kGzCorrupt;
+            __builtin_amdgcn_wave_barrier();
+            if (!gz_build(T.lens, 19, T.lcnt, T.lsym, T.lfast, lane)) return kGzCorrupt;
+            // litlen + distance code lengths with the code-length code (runs 16 / 17 / 18); they
+            // overwrite lens[0..19), whose code now lives in lfast / lcnt / lsym
+            uint32_t i = 0, prev = 0;
+            const uint32_t total = nlit + ndist;
+            uint8_t* L = T.lens;
+            while (i < total) {
+                B.refill(lane);
+                const int x = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+                if (x < 0 || B.overrun()) return kGzCorrupt;
+                uint32_t rep = 1, val = (uint32_t)x;
+                if (x == 16) {
+                    if (i == 0) return kGzCorrupt;
+                    rep = 3 + B.bits(2);
+                    val = prev;
+                } else if (x == 17) {
+                    rep = 3 + B.bits(3);
+                    val = 0;
+                } else if (x == 18) {
+                    rep = 11 + B.bits(7);
+                    val = 0;
+                }
+                if (B.overrun() || i + rep > total) return kGzCorrupt;
+                for (uint32_t k = lane; k < rep; k += 64) L[i + k] = (uint8_t)val;
+                __builtin_amdgcn_wave_barrier();
+                i += rep;
+                prev = val;
+            }
+            // distance lengths live at lens[nlit..): move them behind the 288 litlen slots
+            for (uint32_t k = lane; k < 32; k += 64) {
+                const uint8_t v = k < ndist ? L[nlit + k] : 0;
+                __builtin_amdgcn_wave_barrier();
+                L[288 + k] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (!gz_build(L, nlit, T.lcnt, T.lsym, T.lfast, lane)) return kGzCorrupt;
+            if (!gz_build(L + 288, ndist, T.dcnt, T.dsym, T.dfast, lane)) return kGzCorrupt;
+        }
+        // ---- compressed data (huffmanBlock) ----
+        for (;;) {
+            B.refill(lane);
+            const int s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+            if (s < 0 || B.overrun()) return kGzCorrupt;
+            if (s < 256) {
+                if (kWin == kGzSmallWin && d >= kWin) return kGzUnsupported;
+                if (lane == 0) S.win[d & (kWin - 1)] = (uint8_t)s;
+                d++;
+            } else if (s == 256) {
+                break;
+            } else {
+                if (s > 285) return kGzCorrupt;
+                uint32_t eb;
+                const uint32_t len = len_base((uint32_t)s, eb) + B.bits(eb);
+                B.refill(lane);
+                const int ds = gz_sym(B, T.dfast, T.dcnt, T.dsym);
+                if (ds < 0 || ds >= 30) return kGzCorrupt;
+                uint32_t deb;
+                const uint32_t dist = dist_base((uint32_t)ds, deb) + B.bits(deb);
+                if (B.overrun() || dist > d) return kGzCorrupt;
+                if (kWin == kGzSmallWin && d + len > kWin) return kGzUnsupported;
+                // source bytes all precede d: k mod dist repeats the last `dist` bytes
+                const float rc = 1.0f / (float)dist;
+                for (uint32_t k0 = 0; k0 < len; k0 += 64) {
+                    const uint32_t k = k0 + lane;
+                    if (k < len) {
+                        int q = (int)((float)k * rc);
+                        int r = (int)k - q * (int)dist;
+                        r += r < 0 ? (int)dist : 0;
+                        r -= r >= (int)dist ? (int)dist : 0;
+                        const uint8_t b = S.win[(d - dist + (uint32_t)r) & (kWin - 1)];
+                        S.win[(d + k) & (kWin - 1)] = b;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+                d += len;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (kWin != kGzSmallWin && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
+        }
+    }
+    // ---- trailer: byte-aligned CRC-32 + ISIZE ending the payload (one member per record) ----
+    const uint32_t tp = (uint32_t)((B.consumed() + 7) >> 3);
+    if (tp + 8 > slen) return kGzCorrupt;           // truncated trailer (io.ErrUnexpectedEOF)
+    if (tp + 8 < slen) return kGzUnsupported;        // another member follows (multistream)
+    if (d != dlen) return kGzCorrupt;                // ISIZE mismatch (gzip.ErrChecksum)
+    __builtin_amdgcn_wave_barrier();
+    flush(d);
+    return kGzOk;  // CRC-32: k_gzip_crc
+}
+
+__device__ __forceinline__ bool gzip_active(const FrameParams& P, const ScanState* st) {
+    return st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_GZIP;
+}
+
+__device__ __forceinline__ void gz_fail(const FrameParams& P, uint64_t i, int rc) {
+    P.rec_pay[i] |= kPayFail;
+    atomicMin((unsigned long long*)&P.state->decode_err_rec,
+              (unsigned long long)(2 * i + (rc == kGzUnsupported ? 1u : 0u)));
+}
+}  // namespace
+
+template <uint32_t kWin>
+__global__ void __launch_bounds__(64 * kGzWaves) k_gzip_inflate(FrameParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const ScanState* st = P.state;
+    if (!gzip_active(P, st)) return;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    GzLds<kWin>& S = *reinterpret_cast<GzLds<kWin>*>(lds + wv * sizeof(GzLds<kWin>));
+    const uint64_t n = st->n_records;
+    const uint64_t waves = (uint64_t)gridDim.x * kGzWaves;
+    for (uint64_t i = (uint64_t)blockIdx.x * kGzWaves + wv; i < n; i += waves) {
+        if (P.flags[i] & RIO_FLAG_NIL) continue;
+        const uint64_t o0 = P.out_off[i], dlen = P.out_off[i + 1] - o0;
+        // size classes: the small window takes records it holds whole
+        if ((kWin == kGzSmallWin) != (dlen <= kGzSmallWin)) continue;
+        const uint64_t pay = P.rec_pay[i];
+        const uint64_t slen = pay >> 8;
+        if (slen >= 0xFFFFFFF0ull || dlen >= 0xFFFFFFF0ull) {
+            if (lane == 0) gz_fail(P, i, kGzUnsupported);
+            continue;
+        }
+        const int rc = gz_record<kWin>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen, P.out + o0,
+                                       (uint32_t)dlen, lane);
+        if (rc != kGzOk && lane == 0) gz_fail(P, i, rc);
+    }
+}
+
+// CRC-32/IEEE of every inflated record against its trailer (gzip reader.go Read: ErrChecksum).
+__global__ void __launch_bounds__(256) k_gzip_crc(FrameParams P) {
+    __shared__ uint32_t tab[256];
+    for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
+        uint32_t c = k;
+        for (int j = 0; j < 8; j++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+        tab[k] = c;
+    }
+    __syncthreads();
+    const ScanState* st = P.state;
+    if (!gzip_active(P, st)) return;
+    const uint64_t n = st->n_records;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (P.flags[i] & RIO_FLAG_NIL) continue;
+        const uint64_t pay = P.rec_pay[i];
+        if (pay & kPayFail) continue;
+        const uint64_t slen = (pay & ~kPayFail) >> 8;
+        const uint8_t* t = P.file + P.rec_off[i] + (pay & 0xFF) + slen - 8;
+        const uint32_t want = t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
+        const uint8_t* o = P.out + P.out_off[i];
+        const uint64_t len = P.out_off[i + 1] - P.out_off[i];
+        uint32_t c = 0xFFFFFFFFu;
+        uint64_t k = 0;
+        for (; k < len && ((uintptr_t)(o + k) & 15u); k++) c = tab[(c ^ o[k]) & 0xFFu] ^ (c >> 8);
+        for (; k + 16 <= len; k += 16) {
+            const uint4 v = *reinterpret_cast<const uint4*>(o + k);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) c = tab[(c ^ (w[j >> 2] >> (8 * (j & 3)))) & 0xFFu] ^ (c >> 8);
+        }
+        for (; k < len; k++) c = tab[(c ^ o[k]) & 0xFFu] ^ (c >> 8);
+        if ((c ^ 0xFFFFFFFFu) != want)
+            atomicMin((unsigned long long*)&P.state->decode_err_rec, (unsigned long long)(2 * i));
+    }
+}
+
+hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_gzip_inflate<kGzSmallWin>, dim3(1280), dim3(64 * kGzWaves),
+                       kGzWaves * sizeof(GzLds<kGzSmallWin>), s, P);
+    hipLaunchKernelGGL(k_gzip_inflate<kGzLargeWin>, dim3(256), dim3(64 * kGzWaves),
+                       kGzWaves * sizeof(GzLds<kGzLargeWin>), s, P);
+    hipLaunchKernelGGL(k_gzip_crc, dim3(512), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+}  // namespace rio

@@ -224,8 +224,8 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
                 if (!nil && comp == RIO_COMP_SNAPPY && hl <= 24) {
                     k = varint8(win8(w, hl), dl);
                     ok = k && k <= plen && dl <= 0xFFFFFFFFull && dl <= 22ull * (plen - k) + 64;
-                } else if (!nil && comp == RIO_COMP_SNAPPY) {
-                    ok = false;
+                } else if (!nil && comp != RIO_COMP_NONE) {
+                    ok = false;  // snappy preamble outside the window; gzip: sized by its trailer
                 }
                 if (ok && (nil || plen <= avail)) {
                     h.u = u;
@@ -270,6 +270,20 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
         if (kk <= 0 || d > 0xFFFFFFFFull || d > 22ull * (plen - (uint64_t)kk) + 64) return RIO_ERR_DECOMPRESS;
         out_len = d;
         k = (uint64_t)kk;
+    } else if (comp == RIO_COMP_GZIP) {
+        // gzip.NewReader on an empty payload returns a bare io.EOF, which ReadNext passes through
+        // unwrapped (file_reader.go:118-121, gzip_compression.go:56-59)
+        if (plen == 0) return RIO_EOF_PAYLOAD;
+        // decoded size = ISIZE, the payload's last four bytes (trailer of its only member; more
+        // members -> RIO_ERR_UNSUPPORTED at decode). Above DEFLATE's maximum ratio (258 bytes per
+        // 2 bits) no valid stream ends this way: the reader fails on it => codec error here.
+        uint64_t isz = 0;
+        if (plen >= 18) {
+            const uint8_t* t = f + p + h.hdr_len + plen - 4;
+            isz = t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
+            if (isz > 1032ull * plen + 64) return RIO_ERR_DECOMPRESS;
+        }
+        out_len = isz;
     } else {
         out_len = plen;
     }
@@ -313,7 +327,7 @@ __global__ void k_header(FrameParams P) {
     } else if (c > RIO_COMP_LZW) {
         hs = RIO_ERR_COMPRESSION_TYPE;
         st->det0 = c;
-    } else if (v < RIO_VERSION3 || c == RIO_COMP_GZIP || c == RIO_COMP_LZW) {
+    } else if (v < RIO_VERSION3 || c == RIO_COMP_LZW) {
         hs = RIO_ERR_UNSUPPORTED;  // reference reader keeps these
     }
     st->hdr_status = hs;
@@ -951,11 +965,11 @@ __global__ void k_finalize(FrameParams P) {
     }
     if (st->capacity_fail) {
         info.status = RIO_ERR_CAPACITY;
-    } else if (st->decode_err_rec != kNone && st->decode_err_rec < st->n_records) {
-        const uint64_t r = st->decode_err_rec;
+    } else if (st->decode_err_rec != kNone && (st->decode_err_rec >> 1) < st->n_records) {
+        const uint64_t r = st->decode_err_rec >> 1;
         info.n_records = r;
         info.total_out_bytes = P.out_off[r];
-        info.status = RIO_ERR_DECOMPRESS;
+        info.status = (st->decode_err_rec & 1) ? RIO_ERR_UNSUPPORTED : RIO_ERR_DECOMPRESS;
         info.status_offset = P.rec_off[r];
         info.detail0 = info.detail1 = 0;
     }
@@ -1127,6 +1141,7 @@ hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 
 // Phase B: placement into the caller's arrays, decode, final result.
 hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s);  // rio_snappy.hip
+hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s);    // rio_gzip.hip
 
 // Phase B: placement into the caller's arrays, decode, final result. Both decoders check the
 // file's compression type on the device and exit at once when it is not theirs.
@@ -1136,6 +1151,7 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[3], s);
     hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);
     launch_snappy_decode(P, s);
+    launch_gzip_decode(P, s);
     if (ev) (void)hipEventRecord(ev[4], s);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, P);
     return hipGetLastError();

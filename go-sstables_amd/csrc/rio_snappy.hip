@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     uint8_t* sink = P.sink + (t >> 6) * 64;  // the wave's placeholder line
     uint64_t bad_rec = 0;
     if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec))
-        atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)bad_rec);
+        atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)(2 * bad_rec));
 }
 
 // Files beyond the lane-stream kernel's 32-bit positions (>= 4 GiB of input or output, or a
@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(256) k_snappy_global(FrameParams P) {
         const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
         const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
         if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), slen, P.out + o0, o1 - o0))
-            atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)i);
+            atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)(2 * i));
     }
 }
 

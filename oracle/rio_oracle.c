@@ -246,7 +246,9 @@ corrupt:
 static int gzip_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len) {
     *out = NULL;
     *out_len = 0;
-    if (n == 0) return RIO_ERR_DECOMPRESS; /* gzip.NewReader(empty) -> io.EOF */
+    /* gzip.NewReader(empty) returns a bare io.EOF (gzip_compression.go:56-59), which ReadNext
+     * passes through unwrapped (file_reader.go:118-121) and ReadNextAt wraps once: io.EOF class */
+    if (n == 0) return RIO_EOF_PAYLOAD;
     uint64_t cap = n * 4 + 64, used = 0;
     uint8_t* dst = (uint8_t*)malloc(cap);
     z_stream z;

@@ -166,3 +166,119 @@ def cases():
     out.append(("text_snappy_64k", generate(40, 65536, 2, kind=1, seed=5).tobytes()))
     out.append(("random_none_64k", generate(30, 65536, 0, kind=2, seed=6).tobytes()))
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# gzip-compressed files (compType 1, GzipCompressor: one gzip member per record)
+# ---------------------------------------------------------------------------------------------
+def gzip_member(data: bytes, level: int = 6, strategy: int = 0, header: bytes = None) -> bytes:
+    """One gzip member. header=None: zlib's own 10-byte header; else `header` + raw DEFLATE + trailer."""
+    import zlib
+
+    if header is None:
+        co = zlib.compressobj(level, zlib.DEFLATED, 31, 9, strategy)
+        return co.compress(data) + co.flush()
+    co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+    body = co.compress(data) + co.flush()
+    return header + body + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data) & 0xFFFFFFFF)
+
+
+def gzip_header(flg=0, extra=b"", name=b"", comment=b"", hcrc=None) -> bytes:
+    """RFC 1952 header with optional FEXTRA / FNAME / FCOMMENT / FHCRC (hcrc=None: the right one)."""
+    import zlib
+
+    h = bytearray(b"\x1f\x8b\x08" + bytes([flg]) + b"\x00\x00\x00\x00\x00\xff")
+    if flg & 4:
+        h += struct.pack("<H", len(extra)) + extra
+    if flg & 8:
+        h += name + b"\x00"
+    if flg & 16:
+        h += comment + b"\x00"
+    if flg & 2:
+        v = (zlib.crc32(bytes(h)) & 0xFFFF) if hcrc is None else hcrc
+        h += struct.pack("<H", v)
+    return bytes(h)
+
+
+def gz_file(payloads, version=4):
+    """recordio image with explicit gzip payloads: (uncompressed_len, payload) or None (nil)."""
+    out = bytearray(file_header(version, 1))
+    for p in payloads:
+        if p is None:
+            out += header_v4(0, 0, nil=True) if version == 4 else header_v3(0, 0, nil=True)
+            continue
+        u, pay = p
+        out += (header_v4(u, len(pay)) if version == 4 else header_v3(u, len(pay))) + pay
+    return bytes(out)
+
+
+def text_records(n, seed, lo=1, hi=1500):
+    rng = random.Random(seed)
+    words = ["".join(rng.choice("abcdefghijklmnopqrstuvwxyz") for _ in range(rng.randint(2, 9)))
+             for _ in range(300)]
+    out = []
+    for _ in range(n):
+        k = rng.randint(lo, hi)
+        s = b""
+        while len(s) < k:
+            s += (rng.choice(words) + rng.choice([" ", " ", ", ", ".\n"])).encode()
+        out.append(s[:k])
+    return out
+
+
+def gzip_cases():
+    """(name, image, may_fall_back) gzip files. may_fall_back marks inputs the device path may hand
+    back to the reference reader (RIO_ERR_UNSUPPORTED: a record with more than one member, or one
+    decoding past the small window)."""
+    import zlib
+
+    rng = random.Random(11)
+    cases = []
+    text = text_records(200, 5)
+    cases.append(("gz_text_small", gz_file([(len(r), gzip_member(r)) for r in text]), False))
+    for lvl in (0, 1, 9):
+        cases.append((f"gz_level{lvl}", gz_file([(len(r), gzip_member(r, lvl)) for r in text[:60]]), False))
+    for st, nm in ((zlib.Z_FIXED, "fixed"), (zlib.Z_HUFFMAN_ONLY, "huffonly"), (zlib.Z_RLE, "rle")):
+        cases.append((f"gz_{nm}", gz_file([(len(r), gzip_member(r, 6, st)) for r in text[:60]]), False))
+    big = [b"".join(text_records(40, 7 + i, 200, 1500)) for i in range(4)]
+    rnd = [bytes(rng.getrandbits(8) for _ in range(n)) for n in (3000, 40000, 70000)]
+    runs = [b"a" * 5000, b"ab" * 20000, bytes(range(256)) * 300]
+    large = big + rnd + runs
+    cases.append(("gz_large", gz_file([(len(r), gzip_member(r)) for r in large]), False))
+    cases.append(("gz_large_stored", gz_file([(len(r), gzip_member(r, 0)) for r in large[:5]]), False))
+    cases.append(("gz_mixed_nil_empty", gz_file([None, (0, gzip_member(b"")), (len(text[0]), gzip_member(text[0])),
+                                                None, (0, gzip_member(b"", 0))]), False))
+    hdrs = [gzip_header(8, name=b"record.txt"), gzip_header(16, comment=b"a comment"),
+            gzip_header(4, extra=b"\x01\x02\x03"), gzip_header(2), gzip_header(2 | 4 | 8 | 16, b"xy", b"n", b"c")]
+    cases.append(("gz_header_fields", gz_file([(len(text[i]), gzip_member(text[i], header=h))
+                                              for i, h in enumerate(hdrs)]), False))
+    good = [(len(r), gzip_member(r)) for r in text[:20]]
+
+    def corrupt(name, k, pay, may=False):
+        recs = list(good)
+        recs[k] = (recs[k][0], pay)
+        cases.append((name, gz_file(recs), may))
+
+    p = good[7][1]
+    corrupt("gz_bad_hcrc", 7, gzip_member(text[7], header=gzip_header(2, hcrc=0x1234)))
+    corrupt("gz_bad_magic", 7, b"\x1f\x8c" + p[2:])
+    corrupt("gz_bad_cm", 7, p[:2] + b"\x07" + p[3:])
+    corrupt("gz_bad_crc", 7, p[:-8] + bytes([p[-8] ^ 1]) + p[-7:])
+    corrupt("gz_isize_plus1", 7, p[:-4] + struct.pack("<I", good[7][0] + 1))
+    corrupt("gz_isize_minus1", 7, p[:-4] + struct.pack("<I", good[7][0] - 1), may=True)
+    corrupt("gz_isize_huge", 7, p[:-4] + struct.pack("<I", 0xFFFFFFF0))
+    corrupt("gz_truncated_trailer", 7, p[:-3], may=True)
+    corrupt("gz_truncated_body", 7, p[:len(p) // 2], may=True)
+    corrupt("gz_tiny", 7, p[:5], may=True)
+    corrupt("gz_empty_payload", 7, b"")
+    corrupt("gz_btype3", 7, p[:10] + bytes([p[10] | 6]) + p[11:])
+    corrupt("gz_two_members", 7, gzip_member(text[7][:100]) + gzip_member(text[7][100:]), may=True)
+    corrupt("gz_trailing_garbage", 7, p + b"\x00\x01", may=True)
+    # bit flips inside the DEFLATE body (header and trailer intact)
+    for j in range(12):
+        q = bytearray(p)
+        pos = 10 + rng.randrange(len(p) - 18)
+        q[pos] ^= 1 << rng.randrange(8)
+        corrupt(f"gz_flip{j}", 7, bytes(q), may=True)
+    cases.append(("gz_v3", gz_file([(len(r), gzip_member(r)) for r in text[:30]], version=3), False))
+    return cases

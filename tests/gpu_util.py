@@ -21,8 +21,8 @@ def gpu_decode_arrays(image) -> dict:
     b, info = decoder().decode(d_file, n)
     k, nb = info["n_records"], info["total_out_bytes"]
     res = dict(info)
-    if info["status"] in (L.RIO_ERR_VERSION, L.RIO_ERR_COMPRESSION_TYPE, L.RIO_ERR_UNSUPPORTED,
-                          L.RIO_ERR_SHORT_FILE_HEADER):
+    if info["status"] in (L.RIO_ERR_VERSION, L.RIO_ERR_COMPRESSION_TYPE, L.RIO_ERR_SHORT_FILE_HEADER) or (
+            info["status"] == L.RIO_ERR_UNSUPPORTED and k == 0):
         return res
     res["out"] = b.out[:nb].cpu().numpy()
     res["out_off"] = b.out_off[:k + 1].cpu().numpy()

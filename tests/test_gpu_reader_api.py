@@ -95,6 +95,14 @@ def test_reader_compression_headers(vd):  # :113-134
 
 
 @pytest.mark.parametrize("vd", VDS)
+def test_reader_comp1_content(vd):  # file_reader_test.go:114-122: gzip payload of ascending(1337)
+    r = opened(vd, "recordio_UncompressedSingleRecord_comp1")
+    buf, err = r.ReadNext()
+    assert err is None and buf == asc(1337)
+    expect_eof(r)
+
+
+@pytest.mark.parametrize("vd", VDS)
 def test_reader_comp2_content(vd):
     r = opened(vd, "recordio_UncompressedSingleRecord_comp2")
     buf, err = r.ReadNext()

@@ -1,0 +1,58 @@
+"""Oracle (CPU checker) on the gzip corpus: valid files decode to exactly the records they were
+built from; corruptions end the ReadNext loop at the damaged record with the codec-error class.
+Parity for gzip is pinned by the reference's _comp1 fixture (test_oracle_golden.py); this test pins
+the oracle's gzip restatement against the source records of the crafted corpus."""
+import pytest
+
+import corpus
+import oracle_py as orc
+from conftest import STATUS
+
+
+def _records(name):
+    return {n: img for n, img, _ in corpus.gzip_cases()}[name]
+
+
+@pytest.mark.parametrize("name", ["gz_text_small", "gz_level0", "gz_level9", "gz_fixed", "gz_rle",
+                                  "gz_large", "gz_large_stored", "gz_header_fields", "gz_v3"])
+def test_valid_gzip_files_decode_to_sources(name):
+    img = _records(name)
+    o = orc.file_reader_decode_arrays(img)
+    assert o["status"] == STATUS["EOF"], o["status"]
+    # rebuild the payloads and compare record by record with zlib's own decode of each member
+    import zlib
+
+    out, off = o["out"], o["out_off"]
+    pos, k = 8, 0
+    while pos < len(img):
+        pos += 4  # magic + nil byte
+        vals = []
+        for _ in range(3 if img[:4] == b"\x04\x00\x00\x00" else 2):
+            v, sh = 0, 0
+            while True:
+                b = img[pos]
+                pos += 1
+                v |= (b & 0x7F) << sh
+                sh += 7
+                if b < 0x80:
+                    break
+            vals.append(v)
+        c = vals[1]
+        want = zlib.decompress(img[pos:pos + c], 31)
+        assert bytes(out[off[k]:off[k + 1]]) == want, (name, k)
+        pos += c
+        k += 1
+    assert k == o["n_records"]
+
+
+@pytest.mark.parametrize("name", ["gz_bad_hcrc", "gz_bad_magic", "gz_bad_cm", "gz_bad_crc", "gz_isize_plus1",
+                                  "gz_isize_huge", "gz_btype3", "gz_trailing_garbage"])
+def test_gzip_corruption_ends_at_record(name):
+    o = orc.file_reader_decode_arrays(_records(name))
+    assert o["status"] == STATUS["DECOMPRESS"] and o["n_records"] == 7
+
+
+def test_gzip_empty_payload_is_eof_class():
+    # gzip.NewReader(empty) -> bare io.EOF, returned unwrapped by ReadNext (file_reader.go:118-121)
+    o = orc.file_reader_decode_arrays(_records("gz_empty_payload"))
+    assert o["status"] == STATUS["EOF_PAYLOAD"] and o["n_records"] == 7
