@@ -34,7 +34,9 @@ CONFIGS = {
     "c1": (100_000, 1024, 0, 0, "C1: recordio v4, 100k x 1 KiB uncompressed records (ref generator)"),
     "c3": (10_000_000, 64, 2, 1, "C3: recordio v4, 10M x 64 B snappy records (header-bound)"),
     "c4": (16_384, 65536, 2, 1, "C4: recordio v4, 16384 x 64 KiB snappy records (decompress-bound), one file per GPU"),
+    "c2g": (1_000_000, 1024, 1, 1, "C2-gzip: recordio v4, 1M x 1 KiB gzip records (text-like), one file per GPU"),
 }
+DECODE_KERNEL = {0: "k_decode_copy", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
 
 
 def dist_env():
@@ -243,11 +245,11 @@ def main():
         "dtype": "u8",
         "data": "synthetic: seeded text-like Zipf-word records (snappy ratio ~0.55), one file per rank",
         "config": {"workload": desc, "records": n, "record_bytes": rec_len, "file_bytes": length,
-                   "decoded_bytes": nb, "compression": {0: "none", 2: "snappy"}[comp],
+                   "decoded_bytes": nb, "compression": {0: "none", 1: "gzip", 2: "snappy"}[comp],
                    "parallelism": f"file-sharded x{world}, no data-path collectives"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": "k_snappy_pipe" if comp == 2 else "k_decode_copy",
+                     "kernel": DECODE_KERNEL[comp],
                      "kernel_ms": round(decode_ms, 4), "alg_bytes_per_launch": alg_bytes},
         "stages_ms": {"walk": round(stage[0], 4), "scan": round(stage[1], 4), "place": round(stage[2], 4),
                       "decode": round(stage[3], 4)} if len(stage) == 4 else None,

@@ -442,7 +442,7 @@ __device__ __forceinline__ void gz_fail(const FrameParams& P, uint64_t i, int rc
 }  // namespace
 
 template <uint32_t kWin>
-__global__ void __launch_bounds__(64 * kGzWaves) k_gzip_inflate(FrameParams P) {
+__global__ void __launch_bounds__(64 * kGzWaves, kWin == kGzSmallWin ? 5 : 1) k_gzip_inflate(FrameParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const ScanState* st = P.state;
     if (!gzip_active(P, st)) return;
