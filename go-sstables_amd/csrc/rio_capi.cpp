@@ -28,6 +28,12 @@
 namespace rio {
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* key_off,
+                            uint64_t* key_len, uint64_t* value_off, uint64_t* checksum, uint64_t* result,
+                            hipStream_t s);
+hipError_t launch_sst_validate(const uint8_t* data, const uint64_t* data_off, const uint64_t* data_rec_off,
+                               uint64_t n_data, const uint64_t* value_off, const uint64_t* checksum,
+                               uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s);
 hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t* out, uint64_t out_cap,
                           ReadAtResult* res, hipStream_t s);
 hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
@@ -727,5 +733,32 @@ extern "C" int rio_reader_set_seek_len(rio_reader* r, uint64_t seek_len) {
     if (!r || seek_len == 0) return RIO_ERR_ARG;
     std::lock_guard<std::mutex> g(r->mu);
     r->seek_len = seek_len;
+    return RIO_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// sstables: index parse + value validation on decoded arenas (rio_sstable.hip)
+// ------------------------------------------------------------------------------------------
+extern "C" int rio_sst_index_parse(rio_ctx* ctx, const uint8_t* d_index_out, const uint64_t* d_index_off, uint64_t n,
+                                   uint64_t* d_key_off, uint64_t* d_key_len, uint64_t* d_value_off,
+                                   uint64_t* d_checksum, uint64_t* d_result, void* stream) {
+    if (!ctx || !d_index_off || !d_result || (n && (!d_index_out || !d_key_off || !d_key_len || !d_value_off || !d_checksum)))
+        return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(launch_sst_index(d_index_out, d_index_off, n, d_key_off, d_key_len, d_value_off, d_checksum, d_result, s));
+    return RIO_OK;
+}
+
+extern "C" int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_data_off,
+                                const uint64_t* d_data_rec_off, uint64_t n_data, const uint64_t* d_value_off,
+                                const uint64_t* d_checksum, uint64_t n_index, uint64_t* d_crc_out, uint64_t* d_result,
+                                void* stream) {
+    if (!ctx || !d_result || (n_index && (!d_value_off || !d_checksum || !d_crc_out || !d_data_off || !d_data_rec_off)))
+        return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(launch_sst_validate(d_data_out, d_data_off, d_data_rec_off, n_data, d_value_off, d_checksum, n_index,
+                                d_crc_out, d_result, s));
     return RIO_OK;
 }

@@ -1,0 +1,214 @@
+// rio_sstable.hip — device side of an SSTable's load, validation and full scan on top of the
+// recordio decode (sstables/sstable_reader.go, sstable_iterator.go, slice_key_index.go).
+//
+// An SSTable is data.rio (values: one recordio record per value, Snappy by default,
+// sstable_writer.go:50-56,219-220) + index.rio (one protobuf IndexEntry {key = 1, valueOffset = 2,
+// checksum = 3} per record, sstables/proto/sstable.proto:5-9, uncompressed by default). Both files
+// are decoded by the recordio path (rio_device_decode); these kernels work on the decoded arenas:
+//
+// k_sst_index    one lane per index record: proto.Unmarshal into a reset IndexEntry
+//                (SliceKeyIndexLoader.Load, slice_key_index.go:91-131): wire format restated from
+//                protowire (varints <= 10 bytes, field numbers 1 .. 2^29-1, last occurrence wins,
+//                known fields with another wire type and unknown fields skipped, groups skipped to
+//                their end tag). Outputs key (offset / length into the index arena), valueOffset,
+//                checksum; the first malformed record is reported.
+// k_sst_validate one lane per index entry: the value is the data record whose file offset is the
+//                entry's valueOffset (MMapReader.ReadNextAt, sstable_reader.go:85-92) — record i
+//                for every table the writer produced (valueOffset = the offset its data write
+//                returned, sstable_writer.go:126-132) — then CRC-64/ISO of the value
+//                (checksumValue, :240-248) against the stored checksum, 0 meaning "no checksum"
+//                (:100-108). Outputs every entry's CRC-64, the first mismatching entry, and the
+//                first entry not in the writer's layout (valueOffset is not data record i's offset:
+//                the scan's positional pairing and validation would diverge; the adapter keeps the
+//                reference reader).
+#include <hip/hip_runtime.h>
+
+#include "rio_device.h"
+#include "rio_dev_util.h"
+
+namespace rio {
+
+namespace {
+// protowire.ConsumeVarint over b[0, n): <= 10 bytes, the 10th <= 1
+__device__ __forceinline__ bool pb_varint(const uint8_t* b, uint64_t n, uint64_t& pos, uint64_t& v) {
+    uint64_t x = 0;
+    for (int i = 0; i < 10; i++) {
+        if (pos >= n) return false;
+        const uint32_t c = b[pos++];
+        if (i == 9 && c > 1) return false;
+        x |= (uint64_t)(c & 0x7F) << (7 * i);
+        if (c < 0x80) {
+            v = x;
+            return true;
+        }
+    }
+    return false;
+}
+
+// skip one field value (protowire.ConsumeFieldValue); groups iteratively to their matching end tag
+__device__ bool pb_skip(const uint8_t* b, uint64_t n, uint64_t& pos, uint64_t num, uint32_t wt) {
+    uint64_t v;
+    if (wt == 0) return pb_varint(b, n, pos, v);
+    if (wt == 1) {
+        if (n - pos < 8) return false;
+        pos += 8;
+        return true;
+    }
+    if (wt == 5) {
+        if (n - pos < 4) return false;
+        pos += 4;
+        return true;
+    }
+    if (wt == 2) {
+        if (!pb_varint(b, n, pos, v) || v > n - pos) return false;
+        pos += v;
+        return true;
+    }
+    if (wt != 3) return false;  // 4 unmatched end group, 6, 7 invalid
+    // group: nested start / end tags must match; a stack of field numbers would be exact, the depth
+    // plus the outermost number suffices for wire-valid input and rejects the rest
+    uint32_t depth = 1;
+    uint64_t stack[16];
+    stack[0] = num;
+    while (depth) {
+        uint64_t tag;
+        if (!pb_varint(b, n, pos, tag)) return false;
+        const uint64_t fn = tag >> 3;
+        const uint32_t t = (uint32_t)(tag & 7);
+        if (fn < 1 || fn > 0x1FFFFFFFull) return false;
+        if (t == 4) {
+            if (stack[depth - 1] != fn) return false;
+            depth--;
+        } else if (t == 3) {
+            if (depth == 16) return false;
+            stack[depth++] = fn;
+        } else if (t == 0) {
+            if (!pb_varint(b, n, pos, v)) return false;
+        } else if (t == 1 || t == 5) {
+            const uint64_t w = t == 1 ? 8 : 4;
+            if (n - pos < w) return false;
+            pos += w;
+        } else if (t == 2) {
+            if (!pb_varint(b, n, pos, v) || v > n - pos) return false;
+            pos += v;
+        } else {
+            return false;
+        }
+    }
+    return true;
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n,
+                                                   uint64_t* key_off, uint64_t* key_len, uint64_t* value_off,
+                                                   uint64_t* checksum, unsigned long long* first_bad) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t base = off[i], len = off[i + 1] - base;
+        const uint8_t* b = arena + base;
+        uint64_t pos = 0, ko = 0, kl = 0, vo = 0, cs = 0;
+        bool ok = true;
+        while (ok && pos < len) {
+            uint64_t tag, v;
+            if (!pb_varint(b, len, pos, tag)) { ok = false; break; }
+            const uint64_t fn = tag >> 3;
+            const uint32_t wt = (uint32_t)(tag & 7);
+            if (fn < 1 || fn > 0x1FFFFFFFull) { ok = false; break; }
+            if (fn == 1 && wt == 2) {
+                if (!pb_varint(b, len, pos, v) || v > len - pos) { ok = false; break; }
+                ko = pos;
+                kl = v;
+                pos += v;
+            } else if ((fn == 2 || fn == 3) && wt == 0) {
+                if (!pb_varint(b, len, pos, v)) { ok = false; break; }
+                if (fn == 2) vo = v; else cs = v;
+            } else {
+                ok = pb_skip(b, len, pos, fn, wt);
+            }
+        }
+        key_off[i] = base + ko;
+        key_len[i] = kl;
+        value_off[i] = vo;
+        checksum[i] = cs;
+        if (!ok) atomicMin(first_bad, (unsigned long long)i);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sst_validate(const uint8_t* data, const uint64_t* data_off,
+                                                      const uint64_t* data_rec_off, uint64_t n_data,
+                                                      const uint64_t* value_off, const uint64_t* checksum,
+                                                      uint64_t n_index, uint64_t* crc_out,
+                                                      unsigned long long* result) {
+    __shared__ uint64_t tab[256];
+    for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
+        uint64_t c = k;
+        for (int j = 0; j < 8; j++) c = (c >> 1) ^ (0xD800000000000000ull & (0ull - (c & 1ull)));
+        tab[k] = c;
+    }
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_index; i += stride) {
+        const uint64_t want = value_off[i];
+        uint64_t j = i;
+        if (!(i < n_data && data_rec_off[i] == want)) {
+            // not the writer's layout (entry i <-> data record i): the full scan pairs entries and
+            // records by position while validation follows valueOffset, so the device path hands
+            // the table back; the search still gives validation its value
+            uint64_t lo = 0, hi = n_data;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (data_rec_off[mid] < want) lo = mid + 1; else hi = mid;
+            }
+            if (lo >= n_data || data_rec_off[lo] != want) {
+                crc_out[i] = 0;
+                atomicMin(&result[1], (unsigned long long)i);
+                continue;
+            }
+            j = lo;
+            atomicMin(&result[1], (unsigned long long)i);
+        }
+        const uint8_t* v = data + data_off[j];
+        const uint64_t len = data_off[j + 1] - data_off[j];
+        uint64_t c = ~0ull, k = 0;
+        for (; k < len && ((uintptr_t)(v + k) & 15u); k++) c = tab[(c ^ v[k]) & 0xFFu] ^ (c >> 8);
+        for (; k + 16 <= len; k += 16) {
+            const uint4 w = *reinterpret_cast<const uint4*>(v + k);
+            const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int q = 0; q < 16; q++) c = tab[(c ^ (d[q >> 2] >> (8 * (q & 3)))) & 0xFFu] ^ (c >> 8);
+        }
+        for (; k < len; k++) c = tab[(c ^ v[k]) & 0xFFu] ^ (c >> 8);
+        c = ~c;
+        crc_out[i] = c;
+        if (checksum[i] != 0 && c != checksum[i]) atomicMin(&result[0], (unsigned long long)i);
+    }
+}
+
+__global__ void k_sst_init(unsigned long long* r, int n) {
+    if (threadIdx.x < (unsigned)n) r[threadIdx.x] = ~0ull;
+}
+
+hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* key_off,
+                            uint64_t* key_len, uint64_t* value_off, uint64_t* checksum, uint64_t* result,
+                            hipStream_t s) {
+    unsigned long long* r = reinterpret_cast<unsigned long long*>(result);
+    hipLaunchKernelGGL(k_sst_init, dim3(1), dim3(64), 0, s, r, 1);
+    const uint64_t blocks = (n + 255) / 256;
+    if (n) hipLaunchKernelGGL(k_sst_index, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, arena, off,
+                              n, key_off, key_len, value_off, checksum, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_sst_validate(const uint8_t* data, const uint64_t* data_off, const uint64_t* data_rec_off,
+                               uint64_t n_data, const uint64_t* value_off, const uint64_t* checksum,
+                               uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s) {
+    unsigned long long* r = reinterpret_cast<unsigned long long*>(result);
+    hipLaunchKernelGGL(k_sst_init, dim3(1), dim3(64), 0, s, r, 2);
+    const uint64_t blocks = (n_index + 255) / 256;
+    if (n_index)
+        hipLaunchKernelGGL(k_sst_validate, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, data,
+                           data_off, data_rec_off, n_data, value_off, checksum, n_index, crc_out, r);
+    return hipGetLastError();
+}
+
+}  // namespace rio

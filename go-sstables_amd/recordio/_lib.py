@@ -110,6 +110,11 @@ _SIGS = {
     "rio_snappy_encode": (c_uint64, [c_void_p, c_uint64, c_void_p, c_uint64]),
     "rio_generate": (c_uint64, [c_void_p, c_uint64, c_uint32, c_uint64, c_uint64, c_int, c_uint64, c_int]),
     "rio_generate_bound": (c_uint64, [c_uint32, c_uint64, c_uint64]),
+    "rio_sst_index_parse": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rio_sst_validate": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)
@@ -125,6 +130,14 @@ def lib():
             raise RuntimeError(
                 f"librio.so not built at {LIB_PATH}: run `make -C go-sstables_amd/csrc` "
                 "(or __graft_entry__.build()); the recordio GPU path has no CPU fallback")
+        # One HIP runtime per process: torch bundles its own libamdhip64 under the same soname as
+        # the ROCm one librio.so links. Whichever loads first is used by both; if librio's loads
+        # first, torch later finds no GPU. So when torch is present (the Python mirror uses it for
+        # device buffers), it is imported before the library.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)

@@ -1,0 +1,272 @@
+"""MI355X-native SSTable load / validation / full scan — Python mirror of
+github.com/thomasjungblut/go-sstables/sstables (sstable_reader.go, sstable_iterator.go,
+slice_key_index.go, sstable_writer.go).
+
+The device does the byte work: both files are decoded by the recordio path (rio_device_decode),
+the index records are parsed and every value's CRC-64/ISO is computed by the kernels of
+rio_sstable.hip (rio_sst_index_parse / rio_sst_validate). This module keeps the reference's API
+shape: NewSSTableReader(options...) -> (reader, err), reader.Scan() -> iterator whose Next()
+returns (key, value, err) with the Done sentinel, MetaData(), Get, Contains, Close; errors carry
+the reference's message texts. Tables the device path does not handle (v0 protobuf values,
+recordio v1/v2 files, an index not in the writer's layout) return UnsupportedError: the adapter
+keeps the reference reader for them. There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+from recordio import _lib as L
+from recordio.errors import GoError
+
+from . import proto
+from .writer import NewSSTableStreamWriter, SSTableStreamWriter, write_sstable  # noqa: F401
+
+IndexFileName = "index.rio"
+DataFileName = "data.rio"
+BloomFileName = "bloom.bf.gz"
+MetaFileName = "meta.pb.bin"
+Version = 1
+
+Done = GoError("no more items in iterator")  # sstable.go:18
+NotFound = GoError("key was not found")  # sstable.go:19
+_NONE = 0xFFFFFFFFFFFFFFFF
+
+
+class ChecksumError(GoError):
+    """sstable_reader.go:22-35"""
+
+    def __init__(self, checksum: int, expected: int):
+        super().__init__(f"Checksum mismatch: expected {expected:x}, got {checksum:x}")
+        self.checksum = checksum
+        self.expectedChecksum = expected
+
+    def __eq__(self, other):
+        return isinstance(other, ChecksumError) and (self.checksum, self.expectedChecksum) == (
+            other.checksum, other.expectedChecksum)
+
+    __hash__ = GoError.__hash__
+
+
+class UnsupportedError(GoError):
+    """The device path hands this table back to the reference reader (RIO_ERR_UNSUPPORTED)."""
+
+
+@dataclass
+class _Opts:
+    basePath: str = ""
+    skipHashCheckOnLoad: bool = False  # sstable_reader.go:255-258: validate on load by default
+    skipHashCheckOnRead: bool = True
+    device: int = 0
+
+
+def ReadBasePath(p: str):  # noqa: N802
+    def f(o): o.basePath = p
+    return f
+
+
+def SkipHashCheckOnLoad():  # noqa: N802
+    def f(o): o.skipHashCheckOnLoad = True
+    return f
+
+
+def EnableHashCheckOnReads():  # noqa: N802
+    def f(o): o.skipHashCheckOnRead = False
+    return f
+
+
+def ReadWithKeyComparator(_cmp=None):  # noqa: N802
+    """Bytes comparator only (skiplist.BytesComparator, the reference's default)."""
+    def f(o): pass
+    return f
+
+
+def ReadOnDevice(device: int):  # noqa: N802
+    def f(o): o.device = device
+    return f
+
+
+def _fmt_key(k: bytes) -> str:
+    return "[" + " ".join(str(b) for b in k) + "]"  # Go's %v of a []byte
+
+
+class _DeviceTable:
+    """Both files decoded on the device, index parsed, every value's CRC-64 computed."""
+
+    def __init__(self, base: str, device: int, need_crc: bool):
+        import torch
+
+        from recordio.device import DeviceDecoder, to_device_file
+
+        self.dec = DeviceDecoder(device)
+        dev = f"cuda:{device}"
+        lib = L.lib()
+
+        def decode(name):
+            with open(os.path.join(base, name), "rb") as fh:
+                img = fh.read()
+            d, n = to_device_file(img, device)
+            b, info = self.dec.decode(d, n)
+            return img, b, info
+
+        self.index_img, self.ib, ii = decode(IndexFileName)
+        self.data_img, self.db, di = decode(DataFileName)
+        for what, info in (("index", ii), ("data", di)):
+            if info["status"] == L.RIO_ERR_UNSUPPORTED:
+                raise UnsupportedError(f"{what} file of '{base}' is not decoded on the device (recordio v"
+                                       f"{info['version']}, compression {info['compression']})")
+        self.index_info, self.data_info = ii, di
+        n = self.n_index = ii["n_records"]
+        self.n_data = di["n_records"]
+        self.key_off = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        self.key_len = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        self.value_off = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        self.checksum = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        res = torch.empty(2, dtype=torch.int64, device=dev)
+        stream = torch.cuda.current_stream(device)
+        rc = lib.rio_sst_index_parse(self.dec.ctx, self.ib.out.data_ptr(), self.ib.out_off.data_ptr(), n,
+                                     self.key_off.data_ptr(), self.key_len.data_ptr(), self.value_off.data_ptr(),
+                                     self.checksum.data_ptr(), res.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+        if rc:
+            raise GoError(f"rio_sst_index_parse: {L.strerror(rc)}")
+        self.crc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        vres = torch.empty(2, dtype=torch.int64, device=dev)
+        rc = lib.rio_sst_validate(self.dec.ctx, self.db.out.data_ptr(), self.db.out_off.data_ptr(),
+                                  self.db.rec_off.data_ptr(), self.n_data, self.value_off.data_ptr(),
+                                  self.checksum.data_ptr(), n, self.crc.data_ptr(), vres.data_ptr(),
+                                  ctypes.c_void_p(stream.cuda_stream))
+        if rc:
+            raise GoError(f"rio_sst_validate: {L.strerror(rc)}")
+        torch.cuda.synchronize(device)
+        self.bad_proto = int(res[0].item()) & _NONE
+        self.bad_crc, self.unplaced = (int(v) & _NONE for v in vres.cpu().tolist())
+        # host views for the Python iterator (the device arrays stay resident)
+        u = lambda t, k: [x & _NONE for x in t[:k].cpu().tolist()]  # noqa: E731
+        self.h_key_off, self.h_key_len = u(self.key_off, n), u(self.key_len, n)
+        self.h_value_off, self.h_checksum, self.h_crc = u(self.value_off, n), u(self.checksum, n), u(self.crc, n)
+        nb_i, nb_d = ii["total_out_bytes"], di["total_out_bytes"]
+        self.h_index = bytes(self.ib.out[:nb_i].cpu().numpy())
+        self.h_data = bytes(self.db.out[:nb_d].cpu().numpy())
+        self.h_data_off = u(self.db.out_off, self.n_data + 1)
+        self.h_data_flags = self.db.flags[:self.n_data].cpu().tolist()
+
+    def key(self, i) -> bytes:
+        o = self.h_key_off[i]
+        return self.h_index[o:o + self.h_key_len[i]]
+
+    def value(self, j):
+        if self.h_data_flags[j] & L.RIO_FLAG_NIL:
+            return None
+        return self.h_data[self.h_data_off[j]:self.h_data_off[j + 1]]
+
+
+class SSTableReader:
+    def __init__(self, opts: _Opts, meta: proto.MetaData, table: _DeviceTable):
+        self.opts, self.meta, self.t = opts, meta, table
+        self._keys = None
+
+    def MetaData(self) -> proto.MetaData:  # noqa: N802
+        return self.meta
+
+    def BasePath(self) -> str:  # noqa: N802
+        return self.opts.basePath
+
+    def Scan(self):  # noqa: N802
+        """SSTableFullScanIterator (sstable_iterator.go:68-111): index entries in file order paired
+        with data records read sequentially."""
+        return _FullScanIterator(self, self.opts.skipHashCheckOnRead), None
+
+    def _value_at(self, i, skip_check):
+        """getValueAtOffset (sstable_reader.go:80-117) for index entry i (the writer's layout)."""
+        t = self.t
+        v = t.value(i)
+        if skip_check:
+            return v, None
+        if t.h_crc[i] != t.h_checksum[i] and t.h_checksum[i] != 0:
+            return v, GoError(f"error in sstable '{self.opts.basePath}' while hashing value at offset "
+                              f"[{t.h_value_off[i]}]: {ChecksumError(t.h_crc[i], t.h_checksum[i])}",
+                              wrapped=ChecksumError(t.h_crc[i], t.h_checksum[i]))
+        return v, None
+
+    def _index_keys(self):
+        if self._keys is None:
+            self._keys = [self.t.key(i) for i in range(self.t.n_index)]
+        return self._keys
+
+    def Get(self, key: bytes):  # noqa: N802
+        """SliceKeyIndex.Get (sort.Search over the entries, slice_key_index.go:19-35)."""
+        import bisect
+
+        ks = self._index_keys()
+        i = bisect.bisect_left(ks, bytes(key))
+        if i >= len(ks) or ks[i] != bytes(key):
+            return None, NotFound
+        return self._value_at(i, self.opts.skipHashCheckOnRead)
+
+    def Contains(self, key: bytes):  # noqa: N802
+        import bisect
+
+        ks = self._index_keys()
+        i = bisect.bisect_left(ks, bytes(key))
+        return i < len(ks) and ks[i] == bytes(key), None
+
+    def Close(self):  # noqa: N802
+        self.t = None
+        return None
+
+
+class _FullScanIterator:
+    def __init__(self, r: SSTableReader, skip_check: bool):
+        self.r, self.skip, self.i = r, skip_check, 0
+
+    def Next(self):  # noqa: N802
+        t = self.r.t
+        i = self.i
+        if i >= t.n_index:
+            return None, None, Done
+        self.i += 1
+        key = t.key(i)
+        if i >= t.n_data:  # dataReader.ReadNext error (end of data file before end of index)
+            return None, None, GoError(f"data file of '{self.r.opts.basePath}' ended at record {i}: "
+                                       f"{L.strerror(t.data_info['status'])}")
+        v = t.value(i)
+        if self.skip:
+            return key, v, None
+        if t.h_checksum[i] != 0 and t.h_crc[i] != t.h_checksum[i]:
+            return key, v, ChecksumError(t.h_crc[i], t.h_checksum[i])
+        return key, v, None
+
+
+def NewSSTableReader(*options):  # noqa: N802
+    """sstable_reader.go:250-345: metadata, index (SliceKeyIndexLoader), data reader, then
+    validateDataFile unless SkipHashCheckOnLoad."""
+    o = _Opts()
+    for f in options:
+        f(o)
+    if not o.basePath:
+        return None, GoError("SSTableReader: basePath was not supplied")
+    meta, err = proto.read_metadata_if_exists(os.path.join(o.basePath, MetaFileName))
+    if err is not None:
+        return None, GoError(f"error while reading metadata of sstable in '{o.basePath}': {err}", wrapped=err)
+    if meta.version == 0:
+        return None, UnsupportedError(f"sstable '{o.basePath}' has v0 (protobuf DataEntry) values")
+    try:
+        t = _DeviceTable(o.basePath, o.device, True)
+    except UnsupportedError as e:
+        return None, e
+    if t.index_info["status"] not in L.EOF_CLASS:
+        return None, GoError(f"error while reading index of sstable in '{o.basePath}': "
+                             f"{L.strerror(t.index_info['status'])}")
+    if t.bad_proto != _NONE:
+        return None, GoError(f"error while reading index of sstable in '{o.basePath}': proto: cannot parse "
+                             f"invalid wire-format data (record {t.bad_proto})")
+    if t.unplaced != _NONE:
+        return None, UnsupportedError(f"sstable '{o.basePath}': index entry {t.unplaced} is not in the writer's layout")
+    r = SSTableReader(o, meta, t)
+    if not o.skipHashCheckOnLoad and t.bad_crc != _NONE:
+        i = t.bad_crc
+        _, e = r._value_at(i, False)
+        return None, GoError(f"validateDataFile error loading value '{o.basePath}' at key "
+                             f"[{_fmt_key(t.key(i))}]: {e}", wrapped=e)
+    return r, None

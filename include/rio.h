@@ -152,6 +152,29 @@ uint64_t rio_max_records(uint64_t len);
 int rio_ctx_last_stage_ms(rio_ctx* ctx, float* ms, int n);
 int rio_ctx_set_timing(rio_ctx* ctx, int enable);
 
+/* ---- sstables on the device (sstables/sstable_reader.go). Both calls work on arenas produced by
+ * rio_device_decode of index.rio / data.rio, run on `stream` (NULL = ctx stream), no host sync.
+ *
+ * rio_sst_index_parse replaces SliceKeyIndexLoader.Load's per-record proto.Unmarshal into an
+ * IndexEntry (slice_key_index.go:91-131, sstables/proto/sstable.proto:5-9). Record i of the index
+ * arena (d_index_out[d_index_off[i] .. d_index_off[i+1])) -> key bytes at
+ * d_index_out[d_key_off[i] .. + d_key_len[i]), valueOffset, checksum (absent fields = 0).
+ * d_result[0] = first malformed record (proto error: the reference's Load fails there) or ~0.
+ *
+ * rio_sst_validate replaces validateDataFile (sstable_reader.go:205-238) and the
+ * SSTableFullScanIterator's optional hash check (sstable_iterator.go:77-111): for every index entry,
+ * the value is the data record whose file offset is valueOffset (getValueAtOffset, :85-92), its
+ * CRC-64/ISO (checksumValue, :240-248) goes to d_crc_out[i]. d_result[0] = first entry whose
+ * non-zero checksum mismatches (ChecksumError), d_result[1] = first entry not in the writer's
+ * layout (valueOffset != data record i's offset: keep the reference reader); ~0 = none. */
+int rio_sst_index_parse(rio_ctx* ctx, const uint8_t* d_index_out, const uint64_t* d_index_off, uint64_t n,
+                        uint64_t* d_key_off, uint64_t* d_key_len, uint64_t* d_value_off, uint64_t* d_checksum,
+                        uint64_t* d_result, void* stream);
+int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_data_off,
+                     const uint64_t* d_data_rec_off, uint64_t n_data, const uint64_t* d_value_off,
+                     const uint64_t* d_checksum, uint64_t n_index, uint64_t* d_crc_out, uint64_t* d_result,
+                     void* stream);
+
 /* ---- single-record decode at an arbitrary offset (MMapReader.ReadNextAt semantics) on the
  * device; `d_file` device-resident. The decoded record is written to `d_out` (capacity out_cap);
  * *len_out / *nil_out / status go to host memory (this call synchronises). */

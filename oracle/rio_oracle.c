@@ -159,6 +159,39 @@ static int read_header_v3(brd* r, hdr_t* h) {
     return RIO_OK;
 }
 
+/* readRecordHeaderV2 (common_reader.go:62-81): uvarint magic, u, c (no nil byte, no CRC) */
+static int read_header_v2(brd* r, hdr_t* h) {
+    uint64_t m = 0;
+    int e = go_read_uvarint(r, &m);
+    h->magic_len = r->pos;
+    if (e) return e;
+    if (m != RIO_MAGIC) return RIO_ERR_MAGIC;
+    e = go_read_uvarint(r, &h->u);
+    if (e) return later_field(e);
+    e = go_read_uvarint(r, &h->c);
+    if (e) return later_field(e);
+    h->nil = 0;
+    h->hdr_len = r->pos;
+    return RIO_OK;
+}
+
+/* readNextV1 header (file_reader.go:282-300 + readRecordHeaderV1, common_reader.go:46-60): a
+ * fixed 20-byte header read with io.ReadFull (0 bytes: io.EOF, partial: io.ErrUnexpectedEOF),
+ * LE u32 magic 0x130691, LE u64 u, LE u64 c. No zero-tail rule in v1. */
+static int read_header_v1(const uint8_t* f, uint64_t avail, hdr_t* h) {
+    h->magic_len = 0;
+    if (avail == 0) return RIO_EOF;
+    if (avail < 20) return RIO_ERR_UNEXPECTED_EOF;
+    uint32_t m = (uint32_t)f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+    if (m != RIO_MAGIC) return RIO_ERR_MAGIC;
+    h->u = h->c = 0;
+    for (int k = 7; k >= 0; k--) h->u = (h->u << 8) | f[4 + k];
+    for (int k = 7; k >= 0; k--) h->c = (h->c << 8) | f[12 + k];
+    h->nil = 0;
+    h->hdr_len = 20;
+    return RIO_OK;
+}
+
 /* ---------------------------------------------------------------------------------------- */
 /* golang/snappy v1.0.0 Decode(dst, src): decodedLen (binary.Uvarint, >0xffffffff => ErrCorrupt) */
 /* then decode() with its bounds checks; output length = the preamble, not the header's u.     */
@@ -342,7 +375,6 @@ int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res)
     memset(res, 0, sizeof *res);
     int e = orc_file_header(f, len, &res->version, &res->compression, &res->detail0);
     if (e) { res->status = e; return e; }
-    if (res->version < RIO_VERSION3) { res->status = RIO_ERR_UNSUPPORTED; return RIO_ERR_UNSUPPORTED; }
     arena_t a;
     memset(&a, 0, sizeof a);
     a.out_off = (uint64_t*)calloc(1, sizeof(uint64_t));
@@ -352,9 +384,14 @@ int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res)
         brd r = {f + p, len - p, 0, res->version == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : UINT64_MAX};
         hdr_t h;
         memset(&h, 0, sizeof h);
-        e = res->version == RIO_VERSION4 ? read_header_v4(&r, &h) : read_header_v3(&r, &h);
+        switch (res->version) { /* ReadNext dispatch, file_reader.go:66-73 */
+        case RIO_VERSION1: e = read_header_v1(f + p, len - p, &h); break;
+        case RIO_VERSION2: e = read_header_v2(&r, &h); break;
+        case RIO_VERSION3: e = read_header_v3(&r, &h); break;
+        default: e = read_header_v4(&r, &h); break;
+        }
         if (e) {
-            if (e == RIO_ERR_MAGIC) {
+            if (e == RIO_ERR_MAGIC && res->version != RIO_VERSION1) {
                 /* io.ReadAll of the remainder after the consumed magic varint; all zeros => EOF */
                 int zero = 1;
                 for (uint64_t q = p + h.magic_len; q < len; q++)
@@ -555,4 +592,91 @@ uint64_t orc_parallel_read_at(const uint8_t* f, uint64_t len, const uint64_t* re
  * the library under test is never linked into the checker. */
 int rio_status_is_eof(int s) {
     return s == RIO_EOF || s == RIO_EOF_ZERO_TAIL || s == RIO_EOF_HEADER || s == RIO_EOF_PAYLOAD;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* sstables: checksumValue (sstable_reader.go:240-248) = Go hash/crc64 with crc64.ISO           */
+/* (reflected poly 0xD800000000000000, init/xorout all ones)                                 */
+/* ---------------------------------------------------------------------------------------- */
+uint64_t orc_crc64_iso(const uint8_t* p, uint64_t n) {
+    static uint64_t tab[256];
+    static int init = 0;
+    if (!init) {
+        for (int i = 0; i < 256; i++) {
+            uint64_t c = (uint64_t)i;
+            for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xD800000000000000ull & (0ull - (c & 1)));
+            tab[i] = c;
+        }
+        init = 1;
+    }
+    uint64_t c = ~0ull;
+    for (uint64_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    return ~c;
+}
+
+/* protowire.ConsumeVarint: <= 10 bytes, the 10th <= 1 */
+static int pb_varint(const uint8_t* b, uint64_t n, uint64_t* pos, uint64_t* v) {
+    uint64_t x = 0;
+    for (int i = 0; i < 10; i++) {
+        if (*pos >= n) return -1;
+        uint8_t c = b[(*pos)++];
+        if (i == 9 && c > 1) return -1;
+        x |= (uint64_t)(c & 0x7F) << (7 * i);
+        if (c < 0x80) { *v = x; return 0; }
+    }
+    return -1;
+}
+
+/* skip one field value of wire type wt (protowire.ConsumeFieldValue); groups to their end tag */
+static int pb_skip(const uint8_t* b, uint64_t n, uint64_t* pos, uint64_t num, int wt, int depth) {
+    uint64_t v;
+    switch (wt) {
+    case 0: return pb_varint(b, n, pos, &v);
+    case 1: if (n - *pos < 8) return -1; *pos += 8; return 0;
+    case 5: if (n - *pos < 4) return -1; *pos += 4; return 0;
+    case 2:
+        if (pb_varint(b, n, pos, &v) || v > n - *pos) return -1;
+        *pos += v;
+        return 0;
+    case 3: /* groups nest at most 16 deep here and on the device (protowire allows 10000) */
+        if (depth >= 16) return -1;
+        for (;;) {
+            uint64_t tag;
+            if (pb_varint(b, n, pos, &tag)) return -1;
+            uint64_t fn = tag >> 3;
+            int t = (int)(tag & 7);
+            if (fn < 1 || fn > 0x1FFFFFFFull) return -1;
+            if (t == 4) return fn == num ? 0 : -1;
+            if (pb_skip(b, n, pos, fn, t, depth + 1)) return -1;
+        }
+    default: return -1; /* 4 (unmatched end group), 6, 7 */
+    }
+}
+
+/* proto.Unmarshal into a reset IndexEntry (sstables/proto/sstable.proto:5-9): key = 1 (bytes),
+ * valueOffset = 2 (varint), checksum = 3 (varint); last occurrence wins; a known field with
+ * another wire type and unknown fields are skipped. Returns 0, or -1 for malformed input. */
+int orc_index_entry(const uint8_t* b, uint64_t n, uint64_t* key_off, uint64_t* key_len, uint64_t* value_off,
+                    uint64_t* checksum) {
+    uint64_t pos = 0;
+    *key_off = *key_len = *value_off = *checksum = 0;
+    while (pos < n) {
+        uint64_t tag, v;
+        if (pb_varint(b, n, &pos, &tag)) return -1;
+        uint64_t fn = tag >> 3;
+        int wt = (int)(tag & 7);
+        if (fn < 1 || fn > 0x1FFFFFFFull) return -1;
+        if (fn == 1 && wt == 2) {
+            if (pb_varint(b, n, &pos, &v) || v > n - pos) return -1;
+            *key_off = pos;
+            *key_len = v;
+            pos += v;
+        } else if ((fn == 2 || fn == 3) && wt == 0) {
+            if (pb_varint(b, n, &pos, &v)) return -1;
+            if (fn == 2) *value_off = v; else *checksum = v;
+        } else if (pb_skip(b, n, &pos, fn, wt, 0)) {
+            return -1;
+        }
+    }
+    return 0;
 }

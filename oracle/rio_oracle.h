@@ -35,7 +35,8 @@ uint32_t orc_crc32c(const uint8_t* p, uint64_t n);
 /* readFileHeaderFromBuffer (common_reader.go:22-44) on the first 8 bytes */
 int orc_file_header(const uint8_t* f, uint64_t len, uint32_t* version, uint32_t* compression,
                     uint64_t* detail);
-/* FileReader Open + ReadNext loop until the first non-nil error (file_reader.go:26-131, 389-447) */
+/* FileReader Open + ReadNext loop until the first non-nil error (file_reader.go:26-131, 389-447;
+ * v1/v2 legacy paths :282-360, read only so the reference's SSTable fixtures can pin the checker) */
 int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res);
 void orc_file_result_free(orc_file_result* res);
 /* MMapReader.ReadNextAt (mmap_reader.go:130-203 v4, 298-356 v3). *out is malloc'd (NULL for nil). */
@@ -51,6 +52,13 @@ void orc_free(void* p);
  * decoded bytes (0 on error). threads <= 0 => 1. */
 uint64_t orc_parallel_read_at(const uint8_t* f, uint64_t len, const uint64_t* rec_off, uint64_t n,
                               int threads);
+
+/* sstables: CRC-64/ISO of a value (checksumValue, sstable_reader.go:240-248) */
+uint64_t orc_crc64_iso(const uint8_t* p, uint64_t n);
+/* sstables: proto.Unmarshal of an IndexEntry record (sstables/proto/sstable.proto:5-9); the key is
+ * b[key_off, key_off + key_len). 0 ok, -1 malformed. */
+int orc_index_entry(const uint8_t* b, uint64_t n, uint64_t* key_off, uint64_t* key_len, uint64_t* value_off,
+                    uint64_t* checksum);
 
 #ifdef __cplusplus
 }

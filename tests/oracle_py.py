@@ -41,6 +41,10 @@ def lib():
         L.orc_file_header.argtypes = [c_void_p, c_uint64, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint64)]
         L.orc_parallel_read_at.restype = c_uint64
         L.orc_parallel_read_at.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, c_int]
+        L.orc_crc64_iso.restype = c_uint64
+        L.orc_crc64_iso.argtypes = [c_void_p, c_uint64]
+        L.orc_index_entry.argtypes = [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
+                                      POINTER(c_uint64)]
         _lib = L
     return _lib
 
@@ -132,3 +136,53 @@ def snappy_decode(data: bytes):
     if out.value:
         lib().orc_free(out)
     return st, rec
+
+
+# ---------------------------------------------------------------------------------------------
+# sstables (checker for the device scan): oracle recordio decode + proto.Unmarshal + CRC-64/ISO
+# ---------------------------------------------------------------------------------------------
+def crc64_iso(data: bytes) -> int:
+    b, n = _buf(data)
+    return lib().orc_crc64_iso(b, n)
+
+
+def index_entry(rec: bytes):
+    """proto.Unmarshal of one IndexEntry record -> (key, valueOffset, checksum), None if malformed."""
+    b, n = _buf(rec or b"")
+    ko, kl, vo, cs = c_uint64(), c_uint64(), c_uint64(), c_uint64()
+    if lib().orc_index_entry(b, n, byref(ko), byref(kl), byref(vo), byref(cs)):
+        return None
+    r = bytes(rec or b"")
+    return r[ko.value:ko.value + kl.value], vo.value, cs.value
+
+
+def sstable_oracle(base: str) -> dict:
+    """NewSSTableReader + validateDataFile + Scan restated on the host: index entries in file order
+    (SliceKeyIndexLoader.Load, slice_key_index.go:91-131), value at valueOffset via ReadNextAt
+    (sstable_reader.go:80-117), CRC-64/ISO vs the stored checksum (0 = unchecked), and the scan's
+    positional pairing of index entries with data records (sstable_iterator.go:77-111)."""
+    idx = file_reader_decode(open(os.path.join(base, "index.rio"), "rb").read())
+    data_img = open(os.path.join(base, "data.rio"), "rb").read()
+    dat = file_reader_decode(data_img)
+    entries, bad_proto = [], None
+    for i, r in enumerate(idx["records"]):
+        e = index_entry(r)
+        if e is None:
+            bad_proto = i
+            break
+        entries.append(e)
+    first_bad = unplaced = None
+    crcs = []
+    at = {o: j for j, o in enumerate(dat["rec_off"])}  # ReadNextAt at a record start = that record
+    for i, (k, vo, cs) in enumerate(entries):
+        j = at.get(vo)
+        if j != i and unplaced is None:
+            unplaced = i
+        val = dat["records"][j] if j is not None else None
+        c = crc64_iso(val or b"")
+        crcs.append(c)
+        if first_bad is None and cs != 0 and c != cs:
+            first_bad = i
+    return {"index_status": idx["status"], "data_status": dat["status"], "entries": entries,
+            "bad_proto": bad_proto, "values": dat["records"], "crcs": crcs, "first_bad": first_bad,
+            "unplaced": unplaced}
