@@ -35,7 +35,10 @@ CONFIGS = {
     "c3": (10_000_000, 64, 2, 1, "C3: recordio v4, 10M x 64 B snappy records (header-bound)"),
     "c4": (16_384, 65536, 2, 1, "C4: recordio v4, 16384 x 64 KiB snappy records (decompress-bound), one file per GPU"),
     "c2g": (1_000_000, 1024, 1, 1, "C2-gzip: recordio v4, 1M x 1 KiB gzip records (text-like), one file per GPU"),
+    "c5": (1_250_000, 1024, 2, 0, "C5: SSTable load + validateDataFile + full scan, 1.25M SHA1 keys x 1 KiB values "
+                                  "(data.rio snappy v4 + index.rio v4), one table per GPU (10M keys over 8 GPUs)"),
 }
+SST_METRIC = "sstable full scan GiB/s (device-resident: index load + CRC-64 validation + data decode)"
 DECODE_KERNEL = {0: "k_decode_copy", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
 
 
@@ -150,6 +153,146 @@ def e2e_rate(image, n_out_bytes: int) -> dict:
             "note": "host image -> pinned-staged H2D -> decode -> D2H of records+offsets+flags"}
 
 
+def sstable_images(n: int, rank: int):
+    """Config 5 (benchmark/sstable_read_test.go:134-158): keys = SHA1 of the big-endian u32 index,
+    sorted (the memstore flush), every value the same random 1 KiB record; data.rio Snappy v4 and
+    index.rio uncompressed v4 as sstable_writer.go writes them. One table per rank (disjoint keys)."""
+    import hashlib
+    import struct
+
+    import numpy as np
+
+    from sstables.proto import encode_index_entry
+    from sstables.writer import _Image, crc64_iso
+
+    keys = sorted(hashlib.sha1(struct.pack(">I", rank * n + i)).digest() for i in range(n))
+    value = np.random.default_rng(rank_seed(rank)).integers(0, 256, 1024, dtype=np.uint8).tobytes()
+    one = _Image(2)
+    one.write(value)
+    img = one.bytes()
+    rec = img[8:]
+    data = np.frombuffer(img[:8] + rec * n, dtype=np.uint8)
+    cs = crc64_iso(value)
+    # an uncompressed v4 record's header depends only on its length: encode it once per length
+    hdr = {}
+    parts = [_Image(0).bytes()]
+    for i, k in enumerate(keys):
+        e = encode_index_entry(k, 8 + i * len(rec), cs)
+        h = hdr.get(len(e))
+        if h is None:
+            one = _Image(0)
+            one.write(e)
+            h = hdr[len(e)] = one.bytes()[8:-len(e)]
+        parts.append(h)
+        parts.append(e)
+    return np.frombuffer(b"".join(parts), dtype=np.uint8), data
+
+
+def run_sstable(args, world, rank, local, device):
+    """One step = the device work of NewSSTableReader + Scan on one table: decode index.rio, parse
+    every IndexEntry, decode data.rio, CRC-64 every value against its entry (rio_sst_*)."""
+    import numpy as np
+    import torch
+
+    from recordio import _lib as L
+    from recordio.device import DeviceDecoder, to_device_file
+
+    n = CONFIGS["c5"][0]
+    index_img, data_img = sstable_images(n, rank)
+    d_index, li = to_device_file(index_img, local)
+    d_data, ld = to_device_file(data_img, local)
+    dec = DeviceDecoder(local)
+    ib, ii = dec.decode(d_index, li)
+    db, di = dec.decode(d_data, ld)
+    if ii["n_records"] != n or di["n_records"] != n:
+        raise RuntimeError(f"sstable decode failed: {ii} {di}")
+    lib = L.lib()
+    i64 = dict(dtype=torch.int64, device=device)
+    key_off, key_len, value_off, checksum, crc = (torch.empty(n, **i64) for _ in range(5))
+    pres, vres = torch.empty(2, **i64), torch.empty(2, **i64)
+    # a real stream: the null stream's handle (0) would send the calls to the ctx's own stream and
+    # the stage events would not bracket them
+    stream = torch.cuda.Stream(device=device)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    torch.cuda.synchronize(device)
+
+    def step(ev=None):
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if ev is not None else None
+        if marks: marks[0].record(stream)
+        dec.launch(d_index, li, ib, stream)
+        if marks: marks[1].record(stream)
+        lib.rio_sst_index_parse(dec.ctx, ib.out.data_ptr(), ib.out_off.data_ptr(), n, key_off.data_ptr(),
+                                key_len.data_ptr(), value_off.data_ptr(), checksum.data_ptr(), pres.data_ptr(), sp)
+        if marks: marks[2].record(stream)
+        dec.launch(d_data, ld, db, stream)
+        if marks: marks[3].record(stream)
+        lib.rio_sst_validate(dec.ctx, db.out.data_ptr(), db.out_off.data_ptr(), db.rec_off.data_ptr(), n,
+                             value_off.data_ptr(), checksum.data_ptr(), n, crc.data_ptr(), vres.data_ptr(), sp)
+        if marks:
+            marks[4].record(stream)
+            ev.append(marks)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if int(pres[0].item()) != -1 or int(vres[0].item()) != -1 or int(vres[1].item()) != -1:
+        raise RuntimeError(f"sstable validation failed: {pres.tolist()} {vres.tolist()}")
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    ev = []
+    for _ in range(3):
+        step(ev)
+    torch.cuda.synchronize(device)
+    names = ("decode_index", "parse_index", "decode_data", "validate")
+    stage = {nm: float(np.mean([m[k].elapsed_time(m[k + 1]) for m in ev])) for k, nm in enumerate(names)}
+    total_in = li + ld
+    value, ms_per_step, _ = job_throughput(dt, total_in, args.steps, world, device)
+    nb_d = di["total_out_bytes"]
+    # dominant stage: the data decode (C2-ref-random shape) or the CRC-64 pass over the values
+    alg = {"decode_data": ld + nb_d + 17 * n + 8, "validate": nb_d + 8 * 5 * n}
+    dom = max(alg, key=lambda k: stage[k])
+    achieved = alg[dom] / (stage[dom] * 1e-3) / 1e9
+    line = {
+        "metric": SST_METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: SHA1 keys, one random 1 KiB value (benchmark/sstable_read_test.go shape), one table per rank",
+        "config": {"workload": CONFIGS["c5"][4], "entries": n, "index_bytes": li, "data_bytes": ld,
+                   "decoded_value_bytes": nb_d, "parallelism": f"table-sharded x{world}, no data-path collectives"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": dom,
+                     "kernel_ms": round(stage[dom], 4), "alg_bytes_per_launch": alg[dom]},
+        "stages_ms": {k: round(v, 4) for k, v in stage.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        import oracle_py as orc
+
+        olib = orc.lib()
+        bad = ctypes.c_uint64()
+        runs, t_total = 0, 0.0
+        while runs < 3 and t_total < 20.0:
+            t1 = time.perf_counter()
+            got = olib.orc_sst_scan(index_img.ctypes.data, li, data_img.ctypes.data, ld, ctypes.byref(bad))
+            t_total += time.perf_counter() - t1
+            runs += 1
+            if got != n:
+                raise RuntimeError("oracle sstable scan disagreed")
+        line["cpu_baseline"] = {"value": round(total_in / 2**30 * runs / t_total, 4), "unit": "GiB/s", "cores": 1,
+                                "kind": "port", "sample": f"full table ({n} entries, {total_in} B) x{runs} runs: "
+                                f"oracle index load + CRC-64 validation + data decode, {_cpu_model()}"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,6 +314,12 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group(backend="nccl", device_id=device)
+
+    if args.config == "c5":
+        run_sstable(args, world, rank, local, device)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
 
     from recordio import _lib as L
     from recordio import generate

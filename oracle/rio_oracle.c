@@ -680,3 +680,30 @@ int orc_index_entry(const uint8_t* b, uint64_t n, uint64_t* key_off, uint64_t* k
     }
     return 0;
 }
+
+/* NewSSTableReader (index load + validateDataFile) + Scan over in-memory data.rio / index.rio
+ * images, for the CPU baseline: returns the entries scanned (0 on a decode / proto failure),
+ * *first_bad = first checksum mismatch or UINT64_MAX. Values pair with entries by position after
+ * checking valueOffset against the record offset (the writer's layout). */
+uint64_t orc_sst_scan(const uint8_t* index, uint64_t ilen, const uint8_t* data, uint64_t dlen, uint64_t* first_bad) {
+    orc_file_result ri, rd;
+    *first_bad = UINT64_MAX;
+    orc_file_reader_decode(index, ilen, &ri);
+    orc_file_reader_decode(data, dlen, &rd);
+    uint64_t n = 0;
+    if (ri.status == RIO_EOF && rd.status == RIO_EOF && ri.n_records <= rd.n_records) {
+        for (n = 0; n < ri.n_records; n++) {
+            uint64_t ko, kl, vo, cs;
+            const uint8_t* rec = ri.out + ri.out_off[n];
+            if (orc_index_entry(rec, ri.out_off[n + 1] - ri.out_off[n], &ko, &kl, &vo, &cs) || vo != rd.rec_off[n]) {
+                n = 0;
+                break;
+            }
+            const uint64_t c = orc_crc64_iso(rd.out + rd.out_off[n], rd.out_off[n + 1] - rd.out_off[n]);
+            if (cs != 0 && c != cs && *first_bad == UINT64_MAX) *first_bad = n;
+        }
+    }
+    orc_file_result_free(&ri);
+    orc_file_result_free(&rd);
+    return n;
+}

@@ -59,6 +59,9 @@ uint64_t orc_crc64_iso(const uint8_t* p, uint64_t n);
  * b[key_off, key_off + key_len). 0 ok, -1 malformed. */
 int orc_index_entry(const uint8_t* b, uint64_t n, uint64_t* key_off, uint64_t* key_len, uint64_t* value_off,
                     uint64_t* checksum);
+/* sstables: index load + validateDataFile + Scan over in-memory images (CPU baseline of config 5);
+ * entries scanned, *first_bad = first checksum mismatch or UINT64_MAX */
+uint64_t orc_sst_scan(const uint8_t* index, uint64_t ilen, const uint8_t* data, uint64_t dlen, uint64_t* first_bad);
 
 #ifdef __cplusplus
 }

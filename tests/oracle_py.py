@@ -41,6 +41,8 @@ def lib():
         L.orc_file_header.argtypes = [c_void_p, c_uint64, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint64)]
         L.orc_parallel_read_at.restype = c_uint64
         L.orc_parallel_read_at.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, c_int]
+        L.orc_sst_scan.restype = c_uint64
+        L.orc_sst_scan.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]
         L.orc_crc64_iso.restype = c_uint64
         L.orc_crc64_iso.argtypes = [c_void_p, c_uint64]
         L.orc_index_entry.argtypes = [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
