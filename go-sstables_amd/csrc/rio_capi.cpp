@@ -152,6 +152,8 @@ struct rio_ctx {
     DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, sink, chunks, block_runs, chunk_excl, place, block_excl, state, info;
     // host-API arenas
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
+    // rio_sst_open: parsed index fields (4 x n), per-entry CRC-64, kernel results
+    DevBuf sst_fields, sst_crc, sst_res;
     uint8_t* pinned[2] = {nullptr, nullptr};
     hipEvent_t pin_ev[2] = {};
     // last host-API framing (rio_frame -> rio_decode)
@@ -228,7 +230,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->rec_desc, &c->sink, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
                       &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
-                      &c->readat_out, &c->readat_res, &c->seek_off})
+                      &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res})
         b->release();
     for (int i = 0; i < 2; i++) {
         if (c->pinned[i]) hipHostFree(c->pinned[i]);
@@ -762,3 +764,119 @@ extern "C" int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const u
                                 d_crc_out, d_result, s));
     return RIO_OK;
 }
+
+// ------------------------------------------------------------------------------------------
+// sstables: host-memory table handle (the cgo NewSSTableReader binding)
+// ------------------------------------------------------------------------------------------
+struct rio_sst {
+    std::vector<uint8_t> index, data, index_flags, data_flags;
+    std::vector<uint64_t> index_off, index_rec_off, data_off, data_rec_off;
+    std::vector<uint64_t> key_off, key_len, value_off, checksum, crc;
+    rio_sst_info info{};
+};
+
+// rio_frame + rio_decode into host vectors; the device arenas (ctx->out, out_off, rec_off) keep
+// the decoded file until the next decode on this ctx
+static int sst_decode_host(rio_ctx* ctx, const uint8_t* file, uint64_t len, std::vector<uint8_t>& out,
+                           std::vector<uint64_t>& off, std::vector<uint64_t>& rec_off, std::vector<uint8_t>& flags,
+                           rio_file_info& info) {
+    int rc = rio_frame(ctx, file, len, &info);
+    if (rc) return rc;
+    const uint64_t n = info.n_records;
+    out.assign(info.total_out_bytes + 1, 0);
+    off.assign(n + 1, 0);
+    rec_off.assign(n + 1, 0);
+    flags.assign(n + 1, 0);
+    rc = rio_decode(ctx, out.data(), info.total_out_bytes, off.data(), rec_off.data(), flags.data(), n, &info);
+    if (rc) return rc;
+    off.resize(info.n_records + 1);
+    return RIO_OK;
+}
+
+static bool sst_header_level(int s) {
+    return s == RIO_ERR_VERSION || s == RIO_ERR_COMPRESSION_TYPE || s == RIO_ERR_SHORT_FILE_HEADER;
+}
+
+extern "C" int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, const uint8_t* data_file,
+                            uint64_t data_len, rio_sst** out, rio_sst_info* info) {
+    if (!ctx || !out || !info || (!index_file && index_len) || (!data_file && data_len)) return RIO_ERR_ARG;
+    *out = nullptr;
+    memset(info, 0, sizeof *info);
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto* t = new rio_sst();
+    rio_sst_info& I = t->info;
+    I.first_bad_proto = I.first_bad_crc = I.first_unplaced = ~0ull;
+    int rc = sst_decode_host(ctx, index_file, index_len, t->index, t->index_off, t->index_rec_off, t->index_flags, I.index);
+    uint64_t n = 0;
+    if (!rc && !sst_header_level(I.index.status) && I.index.status != RIO_ERR_UNSUPPORTED) {
+        // the index arena is on the device (ctx->out / ctx->out_off): parse it there
+        n = I.index.n_records;
+        const uint64_t nn = std::max<uint64_t>(n, 1);
+        if (ctx->sst_fields.ensure(nn * 32) || ctx->sst_crc.ensure(nn * 8) || ctx->sst_res.ensure(32)) rc = RIO_ERR_HIP;
+        uint64_t* f = ctx->sst_fields.as<uint64_t>();
+        uint64_t* res = ctx->sst_res.as<uint64_t>();
+        if (!rc && launch_sst_index(ctx->out.as<uint8_t>(), ctx->out_off.as<uint64_t>(), n, f, f + nn, f + 2 * nn,
+                                    f + 3 * nn, res, ctx->stream) != hipSuccess)
+            rc = RIO_ERR_HIP;
+        t->key_off.assign(nn, 0);
+        t->key_len.assign(nn, 0);
+        t->value_off.assign(nn, 0);
+        t->checksum.assign(nn, 0);
+        t->crc.assign(nn, 0);
+        std::vector<uint64_t>* dst[4] = {&t->key_off, &t->key_len, &t->value_off, &t->checksum};
+        for (int k = 0; k < 4 && !rc; k++)
+            rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(dst[k]->data()), f + k * nn, nn * 8);
+        if (!rc) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(&I.first_bad_proto), res, 8);
+        if (!rc) {
+            // key offsets are absolute into the index arena, which t->index mirrors
+            rc = sst_decode_host(ctx, data_file, data_len, t->data, t->data_off, t->data_rec_off, t->data_flags, I.data);
+        }
+        if (!rc && !sst_header_level(I.data.status) && I.data.status != RIO_ERR_UNSUPPORTED) {
+            if (launch_sst_validate(ctx->out.as<uint8_t>(), ctx->out_off.as<uint64_t>(), ctx->rec_off.as<uint64_t>(),
+                                    I.data.n_records, f + 2 * nn, f + 3 * nn, n, ctx->sst_crc.as<uint64_t>(), res + 1,
+                                    ctx->stream) != hipSuccess)
+                rc = RIO_ERR_HIP;
+            if (!rc) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(t->crc.data()), ctx->sst_crc.p, nn * 8);
+            uint64_t vr[2] = {~0ull, ~0ull};
+            if (!rc) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(vr), res + 1, 16);
+            I.first_bad_crc = vr[0];
+            I.first_unplaced = vr[1];
+        }
+    }
+    I.n_entries = n;
+    *info = I;
+    if (rc) {
+        delete t;
+        return rc;
+    }
+    if (I.index.status == RIO_ERR_UNSUPPORTED || I.data.status == RIO_ERR_UNSUPPORTED) {
+        delete t;
+        return RIO_ERR_UNSUPPORTED;
+    }
+    *out = t;
+    return RIO_OK;
+}
+
+extern "C" int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, uint64_t* key_len,
+                             const uint8_t** value, uint64_t* value_len, int* is_nil, uint64_t* value_offset,
+                             uint64_t* checksum, uint64_t* crc) {
+    if (!t || i >= t->info.n_entries) return RIO_ERR_ARG;
+    if (key) *key = t->index.data() + t->key_off[i];
+    if (key_len) *key_len = t->key_len[i];
+    if (value_offset) *value_offset = t->value_off[i];
+    if (checksum) *checksum = t->checksum[i];
+    if (crc) *crc = t->crc[i];
+    if (i >= t->info.data.n_records) {
+        if (value) *value = nullptr;
+        if (value_len) *value_len = 0;
+        if (is_nil) *is_nil = 0;
+        return t->info.data.status == RIO_OK ? RIO_EOF : t->info.data.status;
+    }
+    const bool nil = (t->data_flags[i] & RIO_FLAG_NIL) != 0;
+    if (value) *value = nil ? nullptr : t->data.data() + t->data_off[i];
+    if (value_len) *value_len = t->data_off[i + 1] - t->data_off[i];
+    if (is_nil) *is_nil = nil ? 1 : 0;
+    return RIO_OK;
+}
+
+extern "C" void rio_sst_free(rio_sst* t) { delete t; }

@@ -63,6 +63,19 @@ class FileInfo(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved0"}
 
 
+class SstInfo(ctypes.Structure):
+    """rio_sst_info (include/rio.h)."""
+
+    _fields_ = [
+        ("index", FileInfo),
+        ("data", FileInfo),
+        ("n_entries", c_uint64),
+        ("first_bad_proto", c_uint64),
+        ("first_bad_crc", c_uint64),
+        ("first_unplaced", c_uint64),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "rio_strerror": (c_char_p, [c_int]),
@@ -115,6 +128,12 @@ _SIGS = {
     "rio_sst_validate": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "rio_sst_open": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_void_p), POINTER(SstInfo)]),
+    "rio_sst_entry": (
+        c_int,
+        [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_void_p), POINTER(c_uint64), POINTER(c_int),
+         POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
+    "rio_sst_free": (None, [c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

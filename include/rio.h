@@ -175,6 +175,36 @@ int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_
                      const uint64_t* d_checksum, uint64_t n_index, uint64_t* d_crc_out, uint64_t* d_result,
                      void* stream);
 
+/* ---- sstables, host-memory API (the cgo binding: one call per table) ------------------------
+ * rio_sst_open replaces NewSSTableReader's load (sstable_reader.go:250-345) for the tables the device
+ * path handles: H2D of index.rio and data.rio, device decode of both, IndexEntry parse and the CRC-64
+ * of every value on the device (the two calls above), D2H of what the iterator needs. The handle owns
+ * host copies; pointers from rio_sst_entry stay valid until rio_sst_free.
+ * Returns RIO_ERR_UNSUPPORTED (no handle, `info` filled) when either file is one the device path hands
+ * back (recordio v1/v2, lzw, multi-member gzip): the adapter keeps the reference reader. Otherwise the
+ * handle is returned and `info` says which of the reference's load errors applies: index/data status
+ * outside the EOF family (reading error), first_bad_proto (proto.Unmarshal error, slice_key_index.go:
+ * 107-110), first_unplaced (not the writer's layout: keep the reference reader), first_bad_crc
+ * (validateDataFile's ChecksumError, sstable_reader.go:205-238, unless SkipHashCheckOnLoad). */
+typedef struct rio_sst_info {
+    rio_file_info index;      /* ReadNext loop over index.rio */
+    rio_file_info data;       /* ReadNext loop over data.rio */
+    uint64_t n_entries;       /* index records = IndexEntries */
+    uint64_t first_bad_proto; /* ~0 = none */
+    uint64_t first_bad_crc;   /* ~0 = none */
+    uint64_t first_unplaced;  /* ~0 = none */
+} rio_sst_info;
+typedef struct rio_sst rio_sst;
+int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, const uint8_t* data_file,
+                 uint64_t data_len, rio_sst** out, rio_sst_info* info);
+/* Entry i in index order (SSTableFullScanIterator.Next, sstable_iterator.go:77-111): key, the value of
+ * data record i (is_nil for a nil record), the stored valueOffset and checksum and the value's CRC-64.
+ * Returns RIO_OK, RIO_ERR_ARG for i >= n_entries, or the data file's terminal status when data record i
+ * does not exist (the scan's dataReader.ReadNext error; key and checksum are still filled). */
+int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, uint64_t* key_len, const uint8_t** value,
+                  uint64_t* value_len, int* is_nil, uint64_t* value_offset, uint64_t* checksum, uint64_t* crc);
+void rio_sst_free(rio_sst* t);
+
 /* ---- single-record decode at an arbitrary offset (MMapReader.ReadNextAt semantics) on the
  * device; `d_file` device-resident. The decoded record is written to `d_out` (capacity out_cap);
  * *len_out / *nil_out / status go to host memory (this call synchronises). */

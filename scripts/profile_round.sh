@@ -15,7 +15,7 @@ step() {
     echo "== $name rc=$rc"; tail -3 "$OUT/$name.log"
     if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step tests 900 python -m pytest tests -m gpu -x -q
+step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --config "$CFG"
 grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
@@ -27,4 +27,10 @@ step pmc_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch"
 step pmc_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
     python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
 python scripts/traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$CFG" k_snappy_pipe "$OUT/traffic.json"
+# the SSTable line (SURVEY config 5) and its kernel trace
+step bench_c5 600 python bench.py --config c5
+grep '^{' "$OUT/bench_c5.log" > "$OUT/bench_c5.json" || true
+step rocprof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- \
+    python bench.py --config c5 --no-cpu-baseline
+find "$OUT/prof_c5" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_c5.csv" \;
 echo done

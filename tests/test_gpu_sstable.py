@@ -181,3 +181,70 @@ def test_large_table_sha1_keys(tmp_path):
     base = str(tmp_path / "t")
     S.write_sstable(base, [(k, val) for k in keys])
     check_against_oracle(base)
+
+
+# ---- the host-memory handle (rio_sst_open / rio_sst_entry): what the cgo NewSSTableReader binds ----
+def sst_open_host(base):
+    import ctypes
+
+    from recordio import _lib as L
+    from recordio.device import DeviceDecoder
+
+    lib = L.lib()
+    dec = DeviceDecoder(0)
+    imgs = [open(os.path.join(base, f), "rb").read() for f in ("index.rio", "data.rio")]
+    h = ctypes.c_void_p()
+    info = L.SstInfo()
+    rc = lib.rio_sst_open(dec.ctx, imgs[0], len(imgs[0]), imgs[1], len(imgs[1]), ctypes.byref(h), ctypes.byref(info))
+    if rc:
+        return rc, info, None
+    ents = []
+    try:
+        for i in range(info.n_entries):
+            k, v = ctypes.c_void_p(), ctypes.c_void_p()
+            kl, vl, vo, cs, crc = (ctypes.c_uint64() for _ in range(5))
+            nil = ctypes.c_int()
+            st = lib.rio_sst_entry(h, i, ctypes.byref(k), ctypes.byref(kl), ctypes.byref(v), ctypes.byref(vl),
+                                   ctypes.byref(nil), ctypes.byref(vo), ctypes.byref(cs), ctypes.byref(crc))
+            key = ctypes.string_at(k, kl.value) if kl.value else b""
+            val = None if (st or nil.value) else (ctypes.string_at(v, vl.value) if vl.value else b"")
+            ents.append((st, key, val, vo.value, cs.value, crc.value))
+        assert lib.rio_sst_entry(h, info.n_entries, None, None, None, None, None, None, None, None) == L.RIO_ERR_ARG
+    finally:
+        lib.rio_sst_free(h)
+    return rc, info, ents
+
+
+@pytest.mark.parametrize("comp", [0, 2])
+def test_host_handle_matches_oracle(tmp_path, comp):
+    rng = random.Random(10 + comp)
+    items = [(be(i), None if i % 97 == 0 else text(rng, rng.randint(0, 2000))) for i in range(1500)]
+    base = str(tmp_path / "t")
+    write_triples(base, triples_for(items), comp)
+    o = orc.sstable_oracle(base)
+    rc, info, ents = sst_open_host(base)
+    assert rc == 0 and info.n_entries == 1500
+    none = (1 << 64) - 1
+    assert (info.first_bad_proto, info.first_bad_crc, info.first_unplaced) == (none, none, none)
+    for i, (st, k, v, vo, cs, crc) in enumerate(ents):
+        e = o["entries"][i]
+        assert st == 0 and (k, vo, cs) == tuple(e) and crc == o["crcs"][i] and v == o["values"][i]
+
+
+def test_host_handle_mismatch_and_handback(tmp_path):
+    tri = [(be(i), be(i + 1), crc64_iso(be(i + 1))) for i in range(1, 8)]
+    tri[3] = (be(4), be(0x15), crc64_iso(be(5)))
+    base = str(tmp_path / "t")
+    write_triples(base, tri)
+    rc, info, ents = sst_open_host(base)
+    assert rc == 0 and info.first_bad_crc == 3 and ents[3][5] == crc64_iso(be(0x15))
+    from recordio import _lib as L
+
+    for name in ("SimpleWriteHappyPathSSTable", "SimpleWriteHappyPathSSTableRecordIOV2"):
+        rc, info, _ = sst_open_host(os.path.join(GOLDEN, "sstables", name))
+        assert rc == L.RIO_ERR_UNSUPPORTED, (name, rc)
+    base2 = str(tmp_path / "m")
+    write_triples(base2, triples_for([(be(i), be(i)) for i in range(20)]),
+                  tamper=lambda i, e, off: b"\x0a\x7fab" if i == 6 else e)
+    rc, info, _ = sst_open_host(base2)
+    assert rc == 0 and info.first_bad_proto == 6
