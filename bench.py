@@ -10,7 +10,10 @@ rio_device_decode call. value = input file bytes decoded by all ranks / max-over
 Multi-GPU: one process per GPU (torchrun); every rank decodes its own file (file sharding, no
 data-path collective; the only collectives are the timing barrier and the max-over-ranks).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2g|c1|c3|c4|c5|wal]
+
+c5 (SSTable load + validation + scan) and wal (ordered WAL replay from host files) print their own
+metric lines; the default (c2) line is the BASELINE.json metric.
 """
 from __future__ import annotations
 
@@ -27,6 +30,10 @@ sys.path.insert(0, os.path.join(HERE, "go-sstables_amd"))
 METRIC = "recordio decode GiB/s (device-resident), v4 1 KiB records, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
+# WAL replay: 8 rotated WAL files of ~128 MiB (DefaultMaxWalSize, write_ahead_log.go:9),
+# 1 KiB text-like snappy records, replayed from the page cache into host memory
+WAL_FILES, WAL_RECORDS_PER_FILE = 8, 230_000
+
 CONFIGS = {
     # name: (records, record_bytes, compression, kind, description)
     "c2": (1_000_000, 1024, 2, 1, "C2: recordio v4, 1M x 1 KiB snappy records (text-like), one file per GPU"),
@@ -35,10 +42,14 @@ CONFIGS = {
     "c3": (10_000_000, 64, 2, 1, "C3: recordio v4, 10M x 64 B snappy records (header-bound)"),
     "c4": (16_384, 65536, 2, 1, "C4: recordio v4, 16384 x 64 KiB snappy records (decompress-bound), one file per GPU"),
     "c2g": (1_000_000, 1024, 1, 1, "C2-gzip: recordio v4, 1M x 1 KiB gzip records (text-like), one file per GPU"),
+    "wal": (WAL_FILES * WAL_RECORDS_PER_FILE, 1024, 2, 1, "WAL replay: 8 x ~128 MiB snappy WAL files (1 KiB "
+                                                          "text-like records) per GPU, sorted, delivered in order"),
     "c5": (1_250_000, 1024, 2, 0, "C5: SSTable load + validateDataFile + full scan, 1.25M SHA1 keys x 1 KiB values "
                                   "(data.rio snappy v4 + index.rio v4), one table per GPU (10M keys over 8 GPUs)"),
 }
 SST_METRIC = "sstable full scan GiB/s (device-resident: index load + CRC-64 validation + data decode)"
+WAL_METRIC = "wal replay GiB/s (host WAL files -> ordered host records, PCIe-inclusive)"
+PCIE_PEAK_GBPS = 128.0  # PCIe Gen5 x16, both directions (64 GB/s each)
 DECODE_KERNEL = {0: "k_decode_copy", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
 
 
@@ -293,6 +304,109 @@ def run_sstable(args, world, rank, local, device):
         print(json.dumps(line), flush=True)
 
 
+def run_wal(args, world, rank, local, device):
+    """One step = Replayer.Replay's device work over one WAL directory (rio_replay_*): map each file,
+    staged H2D, device framing + decode, D2H of records / offsets / flags, files handed out in order.
+    The per-record `process` callback is the caller's and is not part of the step."""
+    import tempfile
+
+    import numpy as np
+    import torch
+
+    from recordio import _lib as L
+    from recordio import generate
+
+    lib = L.lib()
+    tmp = tempfile.mkdtemp(prefix=f"wal_bench_r{rank}_")
+    paths, total_in, total_out = [], 0, 0
+    try:
+        for f in range(WAL_FILES):
+            img = generate(WAL_RECORDS_PER_FILE, 1024, 2, 1, seed=rank_seed(rank) * 100 + f + 1,
+                           threads=min(16, os.cpu_count() or 1))
+            p = os.path.join(tmp, "%06d.wal" % f)
+            img.tofile(p)
+            paths.append(p)
+            total_in += img.shape[0]
+            total_out += WAL_RECORDS_PER_FILE * 1024
+        arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+
+        def replay(workers, depth):
+            h = ctypes.c_void_p()
+            rc = lib.rio_replay_open(local, arr, len(paths), depth, workers, ctypes.byref(h))
+            if rc:
+                raise RuntimeError(f"rio_replay_open: {L.strerror(rc)}")
+            idx, out, off, fl, info = ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), \
+                L.FileInfo()
+            got = 0
+            try:
+                while True:
+                    rc = lib.rio_replay_next(h, ctypes.byref(idx), ctypes.byref(out), ctypes.byref(off),
+                                             ctypes.byref(fl), ctypes.byref(info))
+                    if rc == L.RIO_EOF:
+                        break
+                    if rc or info.n_records != WAL_RECORDS_PER_FILE or idx.value != got:
+                        raise RuntimeError(f"replay of file {idx.value}: rc={rc} {info.as_dict()}")
+                    got += 1
+            finally:
+                lib.rio_replay_free(h)
+            return got
+
+        def timed(workers, depth, steps):
+            if world > 1:
+                torch.distributed.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                replay(workers, depth)
+            return time.perf_counter() - t0
+
+        W, D = 2, 4
+        for _ in range(args.warmup):
+            replay(W, D)
+        dt = timed(W, D, args.steps)
+        value, ms_per_step, _ = job_throughput(dt, total_in, args.steps, world, device)
+        variants = {}
+        if rank == 0 and world == 1:
+            for w, d in ((1, 1), (1, 4), (3, 4), (4, 6)):
+                variants[f"workers{w}_depth{d}"] = round(total_in * 2 / 2**30 / timed(w, d, 2), 3)
+        pcie = (total_in + total_out + 9 * WAL_FILES * WAL_RECORDS_PER_FILE) * args.steps / dt / 1e9
+        line = {
+            "metric": WAL_METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: seeded text-like Zipf-word records, 8 WAL files per rank in the page cache",
+            "config": {"workload": CONFIGS["wal"][4], "files": WAL_FILES, "records": WAL_FILES * WAL_RECORDS_PER_FILE,
+                       "file_bytes": total_in, "decoded_bytes": total_out, "workers": W, "depth": D,
+                       "parallelism": f"directory per rank x{world}, no data-path collectives"},
+            "roofline": {"bound": "pcie", "achieved": round(pcie, 1), "peak": PCIE_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(pcie / PCIE_PEAK_GBPS, 4), "traffic": None, "kernel": "H2D+D2H",
+                         "note": "file bytes in + records, offsets and flags out per second"},
+            "variants_GiBps": variants,
+        }
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            import oracle_py as orc
+
+            t_total, nf = 0.0, 0
+            for p in paths[:3]:
+                img = np.fromfile(p, dtype=np.uint8)
+                t1 = time.perf_counter()
+                o = orc.file_reader_decode_arrays(img)
+                t_total += time.perf_counter() - t1
+                nf += 1
+                if o["n_records"] != WAL_RECORDS_PER_FILE:
+                    raise RuntimeError("oracle WAL decode disagreed")
+            in3 = sum(os.path.getsize(p) for p in paths[:nf])
+            line["cpu_baseline"] = {"value": round(in3 / 2**30 / t_total, 4), "unit": "GiB/s", "cores": 1,
+                                    "kind": "port", "sample": f"{nf} of the {WAL_FILES} WAL files ({in3} B), "
+                                    f"sequential FileReader.ReadNext-loop restatement, {_cpu_model()}"}
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+    finally:
+        import shutil
+
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -315,8 +429,8 @@ def main():
 
         dist.init_process_group(backend="nccl", device_id=device)
 
-    if args.config == "c5":
-        run_sstable(args, world, rank, local, device)
+    if args.config in ("c5", "wal"):
+        (run_sstable if args.config == "c5" else run_wal)(args, world, rank, local, device)
         if world > 1:
             torch.distributed.destroy_process_group()
         return

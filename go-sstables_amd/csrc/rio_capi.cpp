@@ -313,9 +313,24 @@ static int ensure_pinned(rio_ctx* c) {
     return RIO_OK;
 }
 
+// true when [p, p + n) is page-locked host memory HIP knows (hipHostMalloc / hipHostRegister): the
+// copy then goes by DMA directly, without the staging pieces. The probe's error on pageable memory
+// is cleared so a later hipGetLastError (kernel launch check) does not see it.
+static bool host_pinned(const void* p, uint64_t n) {
+    if (!p || n < (1u << 20)) return false;  // small copies: staging costs nothing
+    hipPointerAttribute_t a{};
+    const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    return ok;
+}
+
 // pageable host -> device through two pinned staging pieces (copy of piece k+1 overlaps the DMA
-// of piece k)
+// of piece k); pinned sources go directly
 static int h2d_staged(rio_ctx* c, void* dst, const uint8_t* src, uint64_t n) {
+    if (host_pinned(src, n)) {
+        HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
+        return RIO_OK;
+    }
     int rc = ensure_pinned(c);
     if (rc) return rc;
     uint64_t o = 0;
@@ -332,8 +347,13 @@ static int h2d_staged(rio_ctx* c, void* dst, const uint8_t* src, uint64_t n) {
     return RIO_OK;
 }
 
-// device -> pageable host through pinned staging
+// device -> pageable host through pinned staging; pinned destinations directly
 static int d2h_staged(rio_ctx* c, uint8_t* dst, const void* src, uint64_t n) {
+    if (host_pinned(dst, n)) {
+        HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return RIO_OK;
+    }
     int rc = ensure_pinned(c);
     if (rc) return rc;
     uint64_t o = 0, prev_o = 0, prev_m = 0;

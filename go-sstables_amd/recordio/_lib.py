@@ -134,6 +134,10 @@ _SIGS = {
         [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_void_p), POINTER(c_uint64), POINTER(c_int),
          POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
     "rio_sst_free": (None, [c_void_p]),
+    "rio_replay_open": (c_int, [c_int, c_void_p, c_uint64, c_uint32, c_uint32, POINTER(c_void_p)]),
+    "rio_replay_next": (
+        c_int, [c_void_p, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(FileInfo)]),
+    "rio_replay_free": (None, [c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

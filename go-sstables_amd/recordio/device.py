@@ -29,10 +29,16 @@ def to_device_file(image, device: int = 0) -> tuple[torch.Tensor, int]:
     """Copy a file image (bytes / numpy uint8) into HBM with RIO_DEVICE_PAD readable pad bytes."""
     import numpy as np
 
-    arr = np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray)) else image
-    n = int(arr.shape[0])
+    n = len(image)
     t = torch.zeros(n + L.RIO_DEVICE_PAD, dtype=torch.uint8, device=f"cuda:{device}")
-    t[:n].copy_(torch.from_numpy(np.ascontiguousarray(arr)))
+    if n:
+        import warnings
+
+        arr = np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray)) else image
+        with warnings.catch_warnings():  # a read-only source (bytes) is only read by the H2D copy
+            warnings.simplefilter("ignore", UserWarning)
+            src = torch.from_numpy(np.ascontiguousarray(arr))
+        t[:n].copy_(src)
     return t, n
 
 

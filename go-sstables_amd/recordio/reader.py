@@ -43,18 +43,35 @@ def _base_error(status: int, d0: int = 0, d1: int = 0) -> GoError:
     return GoError(L.strerror(status))
 
 
-def _open_error(status: int, path: str, d0: int, what: str) -> GoError:
+def _open_error(status: int, path: str, d0: int, what: str, size: int = -1) -> GoError:
     if status == L.RIO_ERR_VERSION:
         inner = GoError(f"version mismatch, expected a value from 1 to 4 but was {d0}")
     elif status == L.RIO_ERR_COMPRESSION_TYPE:
         inner = GoError(f"unknown compression type [{d0}]")
     elif status == L.RIO_ERR_SHORT_FILE_HEADER:
-        return wrap(f"error while reading header bytes of '{path}'", ErrUnexpectedEOF)
+        # io.ReadFull of the 8 header bytes (file_reader.go:36-40): io.EOF when the file is empty
+        return wrap(f"error while reading header bytes of '{path}'", EOF if size == 0 else ErrUnexpectedEOF)
     else:
         return GoError(f"{what}: {L.strerror(status)}")
     if what == "mmap":
         return wrap(f"failed reading header from buffer in mmap reader for '{path}'", inner)
     return wrap(f"error while parsing header of '{path}'", inner)
+
+
+def read_next_error(rc: int, path: str, d0: int, d1: int) -> GoError:
+    """FileReader.ReadNext's error for a terminal status of the whole-file decode (file_reader.go:61-131)."""
+    if rc == L.RIO_EOF_ZERO_TAIL:
+        return EOF  # file_reader.go:89-90: bare io.EOF
+    if rc == L.RIO_ERR_MAGIC:
+        return wrap(f"error while parsing record header for zeros towards the file end of '{path}'",
+                    MagicNumberMismatchErr)
+    # payload stage (io.ReadFull of the payload, file_reader.go:104-107): detail0 == 1 marks an
+    # unexpected EOF raised there rather than inside a header varint
+    if rc == L.RIO_EOF_PAYLOAD or (rc == L.RIO_ERR_UNEXPECTED_EOF and d0 == 1):
+        return wrap(f"error while reading into record buffer of '{path}'", _base_error(rc))
+    if rc == L.RIO_ERR_DECOMPRESS:
+        return ErrCorrupt  # file_reader.go:119-122 returns the codec error unwrapped
+    return wrap(f"error while parsing record header of '{path}'", _base_error(rc, d0, d1))
 
 
 class _Reader:
@@ -90,7 +107,7 @@ class _Reader:
             return GoError(f"{kind} for '{self.path}' is already {'opened' if opened else 'closed'}")
         if rc != L.RIO_OK:
             d0, _, _ = self._detail()
-            return _open_error(rc, self.path, d0, "mmap" if self._mmap else "file")
+            return _open_error(rc, self.path, d0, "mmap" if self._mmap else "file", self.Size())
         v, c = c_uint32(), c_uint32()
         L.lib().rio_reader_header(self._h, byref(v), byref(c))
         self.header = _Header(v.value, c.value)
@@ -138,18 +155,7 @@ class FileReader(_Reader):
         if rc == L.RIO_ERR_STATE:
             return self._not_open()
         d0, d1, _ = self._detail()
-        if rc == L.RIO_EOF_ZERO_TAIL:
-            return EOF  # file_reader.go:89-90: bare io.EOF
-        if rc == L.RIO_ERR_MAGIC:
-            return wrap(f"error while parsing record header for zeros towards the file end of '{self.path}'",
-                        MagicNumberMismatchErr)
-        # payload stage (io.ReadFull of the payload, file_reader.go:104-107): detail0 == 1 marks an
-        # unexpected EOF raised there rather than inside a header varint
-        if rc == L.RIO_EOF_PAYLOAD or (rc == L.RIO_ERR_UNEXPECTED_EOF and d0 == 1):
-            return wrap(f"error while reading into record buffer of '{self.path}'", _base_error(rc))
-        if rc == L.RIO_ERR_DECOMPRESS:
-            return ErrCorrupt  # file_reader.go:119-122 returns the codec error unwrapped
-        return wrap(f"error while parsing record header of '{self.path}'", _base_error(rc, d0, d1))
+        return read_next_error(rc, self.path, d0, d1)
 
     def FileInfo(self):  # noqa: N802
         fi = L.FileInfo()

@@ -205,6 +205,24 @@ int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, uint64_t* k
                   uint64_t* value_len, int* is_nil, uint64_t* value_offset, uint64_t* checksum, uint64_t* crc);
 void rio_sst_free(rio_sst* t);
 
+/* ---- ordered replay of a file list (the WAL replay adapter) ----------------------------------
+ * Replaces the per-file loop of wal.Replayer.Replay (wal/replayer.go:18-77; the caller walks the
+ * directory and sorts the *.wal paths as :20-37 does). A worker thread with its own context maps and
+ * decodes file k+1.. on `device` while the caller consumes file k; at most `depth` (0 = 2) decoded
+ * files are held ahead. `workers` (0 = 2, at most depth) threads each own a context and stream, so
+ * one file's H2D overlaps another's decode and D2H. rio_replay_next hands out the files strictly in list order: it returns
+ * RIO_EOF after the last one; otherwise that file's rc (RIO_OK, RIO_ERR_IO when it cannot be opened or
+ * mapped, RIO_ERR_HIP) with `info` and the arrays of rio_decode (out / out_off[n+1] / flags[n]), valid
+ * until the next rio_replay_next or rio_replay_free. Deliver records < info.n_records, then map
+ * info.status like FileReader.ReadNext's terminal error. A file with info.status RIO_ERR_UNSUPPORTED
+ * must be re-read whole by the reference reader before any of its records is delivered. */
+typedef struct rio_replay rio_replay;
+int rio_replay_open(int device, const char* const* paths, uint64_t n_paths, uint32_t depth, uint32_t workers,
+                    rio_replay** out);
+int rio_replay_next(rio_replay* r, uint64_t* index, const uint8_t** out, const uint64_t** out_off,
+                    const uint8_t** flags, rio_file_info* info);
+void rio_replay_free(rio_replay* r);
+
 /* ---- single-record decode at an arbitrary offset (MMapReader.ReadNextAt semantics) on the
  * device; `d_file` device-resident. The decoded record is written to `d_out` (capacity out_cap);
  * *len_out / *nil_out / status go to host memory (this call synchronises). */
