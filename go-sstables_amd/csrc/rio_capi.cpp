@@ -34,6 +34,8 @@ hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t 
 hipError_t launch_sst_validate(const uint8_t* data, const uint64_t* data_off, const uint64_t* data_rec_off,
                                uint64_t n_data, const uint64_t* value_off, const uint64_t* checksum,
                                uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s);
+hipError_t launch_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len, const uint8_t* keys,
+                               const uint64_t* key_off, uint64_t nq, rio_index_hit* hits, hipStream_t s);
 hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t* out, uint64_t out_cap,
                           ReadAtResult* res, hipStream_t s);
 hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
@@ -68,6 +70,7 @@ extern "C" const char* rio_strerror(int s) {
     case RIO_ERR_HIP: return "HIP runtime error";
     case RIO_ERR_STATE: return "reader state error";
     case RIO_ERR_IO: return "I/O error";
+    case RIO_ERR_PROTO: return "proto: cannot parse invalid wire-format data";
     default: return "unknown status";
     }
 }
@@ -900,3 +903,72 @@ extern "C" int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, 
 }
 
 extern "C" void rio_sst_free(rio_sst* t) { delete t; }
+
+// ------------------------------------------------------------------------------------------
+// DiskKeyIndex lookups (k_index_search in rio_kernels.hip)
+// ------------------------------------------------------------------------------------------
+extern "C" int rio_device_index_search(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint64_t seek_len,
+                                       const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n,
+                                       rio_index_hit* d_hits, void* stream) {
+    if (!ctx || !d_file || (n && (!d_keys || !d_key_off || !d_hits))) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(launch_index_search(d_file, len, seek_len ? seek_len : 4096, d_keys, d_key_off, n, d_hits, s));
+    return RIO_OK;
+}
+
+struct rio_index {
+    rio_ctx* ctx = nullptr;
+    uint64_t len = 0;
+    DevBuf file, keys, key_off, hits;
+};
+
+extern "C" int rio_index_open(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_index** out) {
+    if (!ctx || !out || (!file && len)) return RIO_ERR_ARG;
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto* x = new rio_index();
+    x->ctx = ctx;
+    x->len = len;
+    int rc = x->file.ensure(len + RIO_DEVICE_PAD) ? RIO_ERR_HIP : RIO_OK;
+    if (!rc) rc = h2d_staged(ctx, x->file.p, file, len);
+    if (!rc && hipMemsetAsync(x->file.as<uint8_t>() + len, 0, RIO_DEVICE_PAD, ctx->stream) != hipSuccess) rc = RIO_ERR_HIP;
+    if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = RIO_ERR_HIP;
+    if (rc) {
+        x->file.release();
+        delete x;
+        return rc;
+    }
+    *out = x;
+    return RIO_OK;
+}
+
+extern "C" int rio_index_search(rio_index* x, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
+                                rio_index_hit* hits) {
+    if (!x || (n && (!key_off || !hits))) return RIO_ERR_ARG;
+    if (n == 0) return RIO_OK;
+    rio_ctx* ctx = x->ctx;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t kb = key_off[n];
+    if (kb && !keys) return RIO_ERR_ARG;
+    HIP_TRY(x->keys.ensure(kb + 16));
+    HIP_TRY(x->key_off.ensure((n + 1) * 8));
+    HIP_TRY(x->hits.ensure(n * sizeof(rio_index_hit)));
+    int rc = kb ? h2d_staged(ctx, x->keys.p, keys, kb) : RIO_OK;
+    if (!rc) rc = h2d_staged(ctx, x->key_off.p, reinterpret_cast<const uint8_t*>(key_off), (n + 1) * 8);
+    if (rc) return rc;
+    HIP_TRY(launch_index_search(x->file.as<uint8_t>(), x->len, 4096, x->keys.as<uint8_t>(), x->key_off.as<uint64_t>(),
+                                n, x->hits.as<rio_index_hit>(), ctx->stream));
+    return d2h_staged(ctx, reinterpret_cast<uint8_t*>(hits), x->hits.p, n * sizeof(rio_index_hit));
+}
+
+extern "C" void rio_index_free(rio_index* x) {
+    if (!x) return;
+    hipSetDevice(x->ctx->device);
+    hipStreamSynchronize(x->ctx->stream);
+    x->file.release();
+    x->keys.release();
+    x->key_off.release();
+    x->hits.release();
+    delete x;
+}

@@ -19,6 +19,7 @@
 
 #include "rio_device.h"
 #include "rio_dev_util.h"
+#include "rio_pb.h"
 
 namespace rio {
 
@@ -1042,42 +1043,20 @@ __global__ void k_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t*
 }
 
 // MMapReader.SeekNext (mmap_reader.go:58-128): windowed scan for 91 8d 4c with its skip rule,
-// trial ReadNextAt per hit; CRC / magic / io.EOF-class failures continue the scan.
-__global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
-                            uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    ReadAtResult r{};
-    *rec_off = 0;
-    uint32_t ver = 0, comp = 0;
-    int e = RIO_OK;
-    if (len < RIO_FILE_HEADER_BYTES) {
-        e = RIO_ERR_SHORT_FILE_HEADER;
-    } else {
-        ver = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
-        comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
-        if (ver > RIO_VERSION4 || ver < RIO_VERSION1) e = RIO_ERR_VERSION;
-        else if (comp > RIO_COMP_LZW) e = RIO_ERR_COMPRESSION_TYPE;
-        else if (ver < RIO_VERSION3 || comp == RIO_COMP_GZIP || comp == RIO_COMP_LZW) e = RIO_ERR_UNSUPPORTED;
-    }
-    if (e) {
-        r.status = e;
-        *res = r;
-        return;
-    }
+// trial ReadNextAt per hit; CRC / magic / io.EOF-class failures continue the scan. Returns the
+// status; on RIO_OK r describes the record at rec_off (payload_off / len when !write).
+__device__ int seek_next_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_t comp, uint64_t off,
+                             uint64_t seek_len, uint8_t* out, uint64_t out_cap, bool write, ReadAtResult& r,
+                             uint64_t& rec_off) {
     const uint8_t M[3] = {0x91, 0x8D, 0x4C};
+    rec_off = 0;
     uint64_t next = off;
     for (;;) {
-        if (next > len) {
-            r.status = RIO_ERR_INVALID_OFFSET;
-            break;
-        }
+        if (next > len) return RIO_ERR_INVALID_OFFSET;
         const uint64_t num = len - next < seek_len ? len - next : seek_len;
-        if (num == 0) {
-            r.status = RIO_EOF;
-            break;
-        }
+        if (num == 0) return RIO_EOF;
         uint64_t i = 0;
-        bool boundary = false, done = false;
+        bool boundary = false;
         while (i < num) {
             uint64_t ix = i;
             for (int j = 0; j < 3; j++) {
@@ -1094,27 +1073,118 @@ __global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64
                 continue;
             }
             const uint64_t trial = next + i;
-            ReadAtResult t{};
-            const int te = read_at_dev(f, len, ver, comp, trial, out, out_cap, t, true);
+            const int te = read_at_dev(f, len, ver, comp, trial, out, out_cap, r, write);
             if (te != RIO_OK && (te == RIO_ERR_HEADER_CRC || te == RIO_ERR_MAGIC || te == RIO_EOF ||
                                  te == RIO_EOF_HEADER || te == RIO_EOF_PAYLOAD)) {
                 i = ix;
                 continue;
             }
-            t.status = te;
-            r = t;
-            *rec_off = trial;
-            done = true;
-            break;
+            rec_off = trial;
+            return te;
         }
-        if (done) break;
-        if (i == 0) {
-            r.status = RIO_EOF;
-            break;
-        }
+        if (i == 0) return RIO_EOF;
         next += i;
     }
+}
+
+__device__ __forceinline__ int file_header_dev(const uint8_t* f, uint64_t len, uint32_t& ver, uint32_t& comp) {
+    ver = comp = 0;
+    if (len < RIO_FILE_HEADER_BYTES) return RIO_ERR_SHORT_FILE_HEADER;
+    ver = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+    comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+    if (ver > RIO_VERSION4 || ver < RIO_VERSION1) return RIO_ERR_VERSION;
+    if (comp > RIO_COMP_LZW) return RIO_ERR_COMPRESSION_TYPE;
+    if (ver < RIO_VERSION3 || comp == RIO_COMP_GZIP || comp == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;
+    return RIO_OK;
+}
+
+__global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
+                            uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    ReadAtResult r{};
+    uint64_t ro = 0;
+    uint32_t ver, comp;
+    int e = file_header_dev(f, len, ver, comp);
+    if (e == RIO_OK) e = seek_next_dev(f, len, ver, comp, off, seek_len, out, out_cap, true, r, ro);
+    r.status = e;
+    *rec_off = ro;
     *res = r;
+}
+
+// ------------------------------------------------------------------------------------------
+// DiskKeyIndex lookups (sstables/disk_key_index.go:87-140), one lane per query key: the reference's
+// binarySearch over byte offsets [0, size) of an uncompressed index.rio, each probe findAt(h) =
+// SeekNext(h) + proto.Unmarshal into an IndexEntry, compared with bytes.Compare. Every lane runs
+// the exact probe sequence of a freshly loaded index (SeekNext is not monotone in h because of the
+// scan's skip rule, so a table of record starts alone would not reproduce it).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int bytes_compare_dev(const uint8_t* a, uint64_t an, const uint8_t* b, uint64_t bn) {
+    const uint64_t m = an < bn ? an : bn;
+    for (uint64_t k = 0; k < m; k++) {
+        const uint32_t x = a[k], y = b[k];
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return an < bn ? -1 : (an > bn ? 1 : 0);
+}
+
+// findAt: 0 and the entry's fields (key_off absolute in f), or a status
+__device__ int index_find_at(const uint8_t* f, uint64_t len, uint32_t ver, uint64_t h, uint64_t seek_len,
+                             uint64_t& ko, uint64_t& kl, uint64_t& vo, uint64_t& cs) {
+    ReadAtResult r{};
+    uint64_t ro;
+    const int e = seek_next_dev(f, len, ver, RIO_COMP_NONE, h, seek_len, nullptr, 0, false, r, ro);
+    if (e) return e;
+    const uint64_t pl = r.nil ? 0 : r.len;
+    const uint64_t po = r.nil ? 0 : r.payload_off;
+    if (!pb_index_entry(f + po, pl, ko, kl, vo, cs)) return RIO_ERR_PROTO;
+    ko += po;
+    return RIO_OK;
+}
+
+__device__ __forceinline__ bool eof_class(int e) {
+    return e == RIO_EOF || e == RIO_EOF_ZERO_TAIL || e == RIO_EOF_HEADER || e == RIO_EOF_PAYLOAD;
+}
+
+__global__ void __launch_bounds__(256) k_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len,
+                                                      const uint8_t* keys, const uint64_t* key_off, uint64_t nq,
+                                                      rio_index_hit* hits) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t ver, comp;
+    const int he = file_header_dev(f, len, ver, comp);
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
+        rio_index_hit out{};
+        const uint8_t* key = keys + key_off[q];
+        const uint64_t klen = key_off[q + 1] - key_off[q];
+        int e = he;
+        if (e == RIO_OK && comp != RIO_COMP_NONE) e = RIO_ERR_UNSUPPORTED;
+        uint64_t ko = 0, kl = 0, vo = 0, cs = 0;
+        if (e == RIO_OK) {
+            uint64_t i = 0, j = len;
+            while (i < j) {
+                const uint64_t h = (i + j) >> 1;
+                e = index_find_at(f, len, ver, h, seek_len, ko, kl, vo, cs);
+                if (e) break;
+                if (bytes_compare_dev(f + ko, kl, key, klen) < 0) i = h + 1; else j = h;
+            }
+            if (e == RIO_OK) {
+                e = index_find_at(f, len, ver, i, seek_len, ko, kl, vo, cs);
+                if (e == RIO_OK) {
+                    out.offset = i;
+                    out.found = i < len && bytes_compare_dev(f + ko, kl, key, klen) == 0;
+                    if (out.found) {
+                        out.value_offset = vo;
+                        out.checksum = cs;
+                    }
+                }
+            }
+            if (eof_class(e)) {  // binarySearch: an io.EOF probe means "not found" at offset size
+                e = RIO_OK;
+                out.offset = len;
+            }
+        }
+        out.status = e;
+        hits[q] = out;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1166,6 +1236,15 @@ hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t*
 hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
                             uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off, hipStream_t s) {
     hipLaunchKernelGGL(k_seek_next, dim3(1), dim3(64), 0, s, f, len, off, seek_len, out, out_cap, res, rec_off);
+    return hipGetLastError();
+}
+
+hipError_t launch_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len, const uint8_t* keys,
+                               const uint64_t* key_off, uint64_t nq, rio_index_hit* hits, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    const uint64_t blocks = (nq + 255) / 256;
+    hipLaunchKernelGGL(k_index_search, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, f, len,
+                       seek_len, keys, key_off, nq, hits);
     return hipGetLastError();
 }
 

@@ -25,79 +25,10 @@
 
 #include "rio_device.h"
 #include "rio_dev_util.h"
+#include "rio_pb.h"
 
 namespace rio {
 
-namespace {
-// protowire.ConsumeVarint over b[0, n): <= 10 bytes, the 10th <= 1
-__device__ __forceinline__ bool pb_varint(const uint8_t* b, uint64_t n, uint64_t& pos, uint64_t& v) {
-    uint64_t x = 0;
-    for (int i = 0; i < 10; i++) {
-        if (pos >= n) return false;
-        const uint32_t c = b[pos++];
-        if (i == 9 && c > 1) return false;
-        x |= (uint64_t)(c & 0x7F) << (7 * i);
-        if (c < 0x80) {
-            v = x;
-            return true;
-        }
-    }
-    return false;
-}
-
-// skip one field value (protowire.ConsumeFieldValue); groups iteratively to their matching end tag
-__device__ bool pb_skip(const uint8_t* b, uint64_t n, uint64_t& pos, uint64_t num, uint32_t wt) {
-    uint64_t v;
-    if (wt == 0) return pb_varint(b, n, pos, v);
-    if (wt == 1) {
-        if (n - pos < 8) return false;
-        pos += 8;
-        return true;
-    }
-    if (wt == 5) {
-        if (n - pos < 4) return false;
-        pos += 4;
-        return true;
-    }
-    if (wt == 2) {
-        if (!pb_varint(b, n, pos, v) || v > n - pos) return false;
-        pos += v;
-        return true;
-    }
-    if (wt != 3) return false;  // 4 unmatched end group, 6, 7 invalid
-    // group: nested start / end tags must match; a stack of field numbers would be exact, the depth
-    // plus the outermost number suffices for wire-valid input and rejects the rest
-    uint32_t depth = 1;
-    uint64_t stack[16];
-    stack[0] = num;
-    while (depth) {
-        uint64_t tag;
-        if (!pb_varint(b, n, pos, tag)) return false;
-        const uint64_t fn = tag >> 3;
-        const uint32_t t = (uint32_t)(tag & 7);
-        if (fn < 1 || fn > 0x1FFFFFFFull) return false;
-        if (t == 4) {
-            if (stack[depth - 1] != fn) return false;
-            depth--;
-        } else if (t == 3) {
-            if (depth == 16) return false;
-            stack[depth++] = fn;
-        } else if (t == 0) {
-            if (!pb_varint(b, n, pos, v)) return false;
-        } else if (t == 1 || t == 5) {
-            const uint64_t w = t == 1 ? 8 : 4;
-            if (n - pos < w) return false;
-            pos += w;
-        } else if (t == 2) {
-            if (!pb_varint(b, n, pos, v) || v > n - pos) return false;
-            pos += v;
-        } else {
-            return false;
-        }
-    }
-    return true;
-}
-}  // namespace
 
 __global__ void __launch_bounds__(256) k_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n,
                                                    uint64_t* key_off, uint64_t* key_len, uint64_t* value_off,
@@ -106,26 +37,8 @@ __global__ void __launch_bounds__(256) k_sst_index(const uint8_t* arena, const u
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t base = off[i], len = off[i + 1] - base;
         const uint8_t* b = arena + base;
-        uint64_t pos = 0, ko = 0, kl = 0, vo = 0, cs = 0;
-        bool ok = true;
-        while (ok && pos < len) {
-            uint64_t tag, v;
-            if (!pb_varint(b, len, pos, tag)) { ok = false; break; }
-            const uint64_t fn = tag >> 3;
-            const uint32_t wt = (uint32_t)(tag & 7);
-            if (fn < 1 || fn > 0x1FFFFFFFull) { ok = false; break; }
-            if (fn == 1 && wt == 2) {
-                if (!pb_varint(b, len, pos, v) || v > len - pos) { ok = false; break; }
-                ko = pos;
-                kl = v;
-                pos += v;
-            } else if ((fn == 2 || fn == 3) && wt == 0) {
-                if (!pb_varint(b, len, pos, v)) { ok = false; break; }
-                if (fn == 2) vo = v; else cs = v;
-            } else {
-                ok = pb_skip(b, len, pos, fn, wt);
-            }
-        }
+        uint64_t ko, kl, vo, cs;
+        const bool ok = pb_index_entry(b, len, ko, kl, vo, cs);
         key_off[i] = base + ko;
         key_len[i] = kl;
         value_off[i] = vo;

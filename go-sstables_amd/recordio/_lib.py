@@ -36,6 +36,7 @@ RIO_ERR_ARG = 17
 RIO_ERR_HIP = 18
 RIO_ERR_STATE = 19
 RIO_ERR_IO = 20
+RIO_ERR_PROTO = 21
 
 EOF_CLASS = (RIO_EOF, RIO_EOF_ZERO_TAIL, RIO_EOF_HEADER, RIO_EOF_PAYLOAD)
 
@@ -73,6 +74,18 @@ class SstInfo(ctypes.Structure):
         ("first_bad_proto", c_uint64),
         ("first_bad_crc", c_uint64),
         ("first_unplaced", c_uint64),
+    ]
+
+
+class IndexHit(ctypes.Structure):
+    """rio_index_hit (include/rio.h)."""
+
+    _fields_ = [
+        ("offset", c_uint64),
+        ("value_offset", c_uint64),
+        ("checksum", c_uint64),
+        ("status", ctypes.c_int32),
+        ("found", ctypes.c_int32),
     ]
 
 
@@ -138,6 +151,11 @@ _SIGS = {
     "rio_replay_next": (
         c_int, [c_void_p, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(FileInfo)]),
     "rio_replay_free": (None, [c_void_p]),
+    "rio_device_index_search": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "rio_index_open": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_void_p)]),
+    "rio_index_search": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rio_index_free": (None, [c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -21,6 +21,7 @@ from recordio import _lib as L
 from recordio.errors import GoError
 
 from . import proto
+from .disk_index import DiskIndexLoader, DiskKeyIndex, IndexVal  # noqa: F401
 from .writer import NewSSTableStreamWriter, SSTableStreamWriter, write_sstable  # noqa: F401
 
 IndexFileName = "index.rio"

@@ -1,0 +1,163 @@
+"""DiskIndexLoader / DiskKeyIndex mirror (sstables/disk_key_index.go) over the device lookup kernel.
+
+Load keeps index.rio resident in HBM (rio_index_open). Get / Contains / IteratorStartingAt /
+IteratorBetween run the reference's binarySearch on the device (rio_index_search, one lane per
+key), with the probe sequence and error rules of a freshly loaded DiskKeyIndex. GetBatch looks up
+many keys in one launch, which is the path's reason to exist. The iterators walk on from the searched
+offset with SeekNext through the MMapReader mirror (disk_key_index.go:141-165).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from recordio import _lib as L
+from recordio.errors import EOF, GoError, errors_is, wrap
+from recordio.reader import NewMemoryMappedReaderWithPath
+
+
+NotFound = GoError("key not found")  # skiplist.NotFound (skiplist/skiplist.go)
+Done = GoError("no more items in iterator")  # skiplist.Done
+
+
+class IndexVal:
+    """sstables.IndexVal {Offset, Checksum} (sstable_index.go)"""
+
+    __slots__ = ("Offset", "Checksum")
+
+    def __init__(self, offset=0, checksum=0):
+        self.Offset, self.Checksum = offset, checksum
+
+    def __eq__(self, o):
+        return isinstance(o, IndexVal) and (self.Offset, self.Checksum) == (o.Offset, o.Checksum)
+
+    def __repr__(self):
+        return f"IndexVal(Offset={self.Offset}, Checksum={self.Checksum})"
+
+
+def _error(status: int) -> GoError:
+    if status == L.RIO_ERR_PROTO:
+        return GoError("proto: cannot parse invalid wire-format data")
+    from recordio.reader import _base_error
+
+    return _base_error(status)
+
+
+class DiskKeyIndex:
+    def __init__(self, path: str, device: int = 0):
+        self.path = path
+        self.device = device
+        self._h = None
+        self._reader = None
+
+    def Open(self):  # noqa: N802
+        with open(self.path, "rb") as fh:
+            img = fh.read()
+        h = ctypes.c_void_p()
+        rc = L.lib().rio_index_open(L.default_ctx(self.device), img, len(img), ctypes.byref(h))
+        if rc:
+            return GoError(f"error while loading index '{self.path}' to the device: {L.strerror(rc)}")
+        self._h, self.size = h, len(img)
+        self._reader, err = NewMemoryMappedReaderWithPath(self.path, self.device)
+        if err is not None:
+            return err
+        return self._reader.Open()
+
+    def Close(self):  # noqa: N802
+        if self._h is not None:
+            L.lib().rio_index_free(self._h)
+            self._h = None
+        return self._reader.Close() if self._reader is not None else None
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None:
+            L.lib().rio_index_free(self._h)
+            self._h = None
+
+    def search(self, keys) -> list:
+        """One rio_index_hit per key: (offset, found, value_offset, checksum, status)."""
+        keys = [bytes(k) for k in keys]
+        n = len(keys)
+        if n == 0:
+            return []
+        off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([len(k) for k in keys], out=off[1:])
+        blob = b"".join(keys) or b"\0"
+        hits = (L.IndexHit * n)()
+        rc = L.lib().rio_index_search(self._h, blob, off.ctypes.data, n, hits)
+        if rc:
+            raise GoError(f"rio_index_search: {L.strerror(rc)}")
+        return [(h.offset, bool(h.found), h.value_offset, h.checksum, h.status) for h in hits]
+
+    def GetBatch(self, keys):  # noqa: N802
+        """[(IndexVal, err)] per key, Get's semantics."""
+        out = []
+        for off, found, vo, cs, st in self.search(keys):
+            if st:
+                out.append((IndexVal(), _error(st)))
+            elif not found:
+                out.append((IndexVal(), NotFound))
+            else:
+                out.append((IndexVal(vo, cs), None))
+        return out
+
+    def Get(self, key):  # noqa: N802
+        return self.GetBatch([key])[0]
+
+    def Contains(self, key):  # noqa: N802
+        off, found, _, _, st = self.search([key])[0]
+        return (False, _error(st)) if st else (found, None)
+
+    def Iterator(self):  # noqa: N802
+        return _DiskKeyIndexIterator(self._reader, 8, self.size), None
+
+    def IteratorStartingAt(self, key):  # noqa: N802
+        off, _, _, _, st = self.search([key])[0]
+        if st:
+            return None, _error(st)
+        return _DiskKeyIndexIterator(self._reader, off, self.size), None
+
+    def IteratorBetween(self, lo, hi):  # noqa: N802
+        if bytes(lo) > bytes(hi):
+            return None, GoError("keyHigher is lower than keyLower")
+        (s, _, _, _, st1), (e, found, _, _, st2) = self.search([lo, hi])
+        if st1 or st2:
+            return None, _error(st1 or st2)
+        if not found:
+            e -= 1  # keyHigher is inclusive
+        return _DiskKeyIndexIterator(self._reader, s, e), None
+
+
+class _DiskKeyIndexIterator:
+    """disk_key_index.go:141-165: SeekNext from the current offset, then offset + 1."""
+
+    def __init__(self, reader, offset, end):
+        self.r, self.cur, self.end = reader, offset, end
+
+    def Next(self):  # noqa: N802
+        from .proto import decode_index_entry
+
+        if self.cur > self.end:
+            return None, IndexVal(), Done
+        off, rec, err = self.r.SeekNext(self.cur)
+        if err is not None:
+            if errors_is(err, EOF):
+                return None, IndexVal(), Done
+            return None, IndexVal(), err
+        try:
+            k, vo, cs = decode_index_entry(rec or b"")
+        except ValueError as e:
+            return None, IndexVal(), wrap("proto", GoError(str(e)))
+        self.cur = off + 1
+        return k, IndexVal(vo, cs), None
+
+
+class DiskIndexLoader:
+    """disk_key_index.go:167-181"""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+
+    def Load(self, indexPath: str, _meta=None):  # noqa: N802,N803
+        return DiskKeyIndex(indexPath, self.device), None

@@ -48,6 +48,75 @@ def encode_index_entry(key: bytes, value_offset: int, checksum: int) -> bytes:
     return bytes(out)
 
 
+def decode_index_entry(b: bytes):
+    """proto.Unmarshal into a reset IndexEntry for the iterators' one-record-at-a-time path
+    (DiskKeyIndexIterator.Next, disk_key_index.go:141-165): (key, valueOffset, checksum); ValueError
+    on malformed input. Bulk parsing runs on the device (rio_sst_index_parse, rio_index_search)."""
+    key, vo, cs = b"", 0, 0
+    pos = 0
+    while pos < len(b):
+        tag, pos = _varint(b, pos)
+        num, wt = tag >> 3, tag & 7
+        if num < 1 or num > 0x1FFFFFFF:
+            raise ValueError("invalid field number")
+        if wt == 0:
+            v, pos = _varint(b, pos)
+            if num == 2:
+                vo = v
+            elif num == 3:
+                cs = v
+        elif wt == 2:
+            ln, pos = _varint(b, pos)
+            if ln > len(b) - pos:
+                raise ValueError("truncated bytes")
+            if num == 1:
+                key = bytes(b[pos:pos + ln])
+            pos += ln
+        elif wt in (1, 5):
+            w = 8 if wt == 1 else 4
+            if w > len(b) - pos:
+                raise ValueError("truncated fixed")
+            pos += w
+        elif wt == 3:
+            pos = _skip_group(b, pos, num)
+        else:
+            raise ValueError(f"wire type {wt}")
+    return key, vo, cs
+
+
+def _skip_group(b: bytes, pos: int, num: int) -> int:
+    """protowire.ConsumeGroup: nested start/end tags must match, depth <= 16 (as the kernels)."""
+    stack = [num]
+    while stack:
+        tag, pos = _varint(b, pos)
+        fn, t = tag >> 3, tag & 7
+        if fn < 1 or fn > 0x1FFFFFFF:
+            raise ValueError("invalid field number")
+        if t == 4:
+            if stack[-1] != fn:
+                raise ValueError("mismatched end group")
+            stack.pop()
+        elif t == 3:
+            if len(stack) == 16:
+                raise ValueError("group nesting")
+            stack.append(fn)
+        elif t == 0:
+            _, pos = _varint(b, pos)
+        elif t in (1, 5):
+            w = 8 if t == 1 else 4
+            if w > len(b) - pos:
+                raise ValueError("truncated fixed")
+            pos += w
+        elif t == 2:
+            ln, pos = _varint(b, pos)
+            if ln > len(b) - pos:
+                raise ValueError("truncated bytes")
+            pos += ln
+        else:
+            raise ValueError(f"wire type {t}")
+    return pos
+
+
 @dataclass
 class MetaData:
     numRecords: int = 0

@@ -84,6 +84,7 @@ typedef enum rio_status {
     RIO_ERR_HIP = 18,             /* HIP runtime failure */
     RIO_ERR_STATE = 19,           /* reader not opened / already closed / already opened */
     RIO_ERR_IO = 20,              /* file open / mmap / read failure */
+    RIO_ERR_PROTO = 21,           /* proto.Unmarshal of an IndexEntry failed (invalid wire format) */
     RIO_STATUS_COUNT_ = 21
 } rio_status;
 
@@ -204,6 +205,36 @@ int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, co
 int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, uint64_t* key_len, const uint8_t** value,
                   uint64_t* value_len, int* is_nil, uint64_t* value_offset, uint64_t* checksum, uint64_t* crc);
 void rio_sst_free(rio_sst* t);
+
+/* ---- DiskKeyIndex lookups (sstables/disk_key_index.go:87-140) --------------------------------
+ * Batched DiskKeyIndex.Get / Contains / IteratorStartingAt: one result per query key, each the
+ * reference's binarySearch over the byte offsets of an uncompressed index.rio with every probe
+ * findAt(h) = SeekNext(h) + proto.Unmarshal(IndexEntry), exactly as a freshly loaded DiskKeyIndex
+ * runs it (the reference's offsetCache is per index and may keep an empty entry at an offset whose
+ * probe hit io.EOF; later lookups on the same Go object then see that entry: see DESIGN.md §8).
+ *   status  RIO_OK (no error; `found` tells Get / Contains), else findAt's error: SeekNext's
+ *           non-EOF error (e.g. RIO_ERR_UNEXPECTED_EOF) or RIO_ERR_PROTO. RIO_ERR_UNSUPPORTED for a
+ *           compressed or v1/v2 index (keep the reference index).
+ *   offset  binarySearch's offset (IteratorStartingAt starts there; size when an io.EOF probe ended it)
+ *   value_offset / checksum  IndexVal when found. */
+typedef struct rio_index_hit {
+    uint64_t offset;
+    uint64_t value_offset;
+    uint64_t checksum;
+    int32_t status;
+    int32_t found;
+} rio_index_hit;
+/* device-resident: d_file (RIO_DEVICE_PAD readable bytes past len), query i = d_keys[d_key_off[i] ..
+ * d_key_off[i+1]), results to d_hits[n]; seek_len 0 = 4096 (mmap_reader.go:370); no host sync */
+int rio_device_index_search(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint64_t seek_len,
+                            const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n, rio_index_hit* d_hits,
+                            void* stream);
+/* host-memory handle (the cgo DiskIndexLoader.Load / Get binding): the index file stays resident in
+ * HBM; each search copies the keys in and the hits out (synchronises). */
+typedef struct rio_index rio_index;
+int rio_index_open(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_index** out);
+int rio_index_search(rio_index* idx, const uint8_t* keys, const uint64_t* key_off, uint64_t n, rio_index_hit* hits);
+void rio_index_free(rio_index* idx);
 
 /* ---- ordered replay of a file list (the WAL replay adapter) ----------------------------------
  * Replaces the per-file loop of wal.Replayer.Replay (wal/replayer.go:18-77; the caller walks the

@@ -707,3 +707,64 @@ uint64_t orc_sst_scan(const uint8_t* index, uint64_t ilen, const uint8_t* data, 
     orc_file_result_free(&rd);
     return n;
 }
+
+/* ---------------------------------------------------------------------------------------- */
+/* DiskKeyIndex.binarySearch (sstables/disk_key_index.go:87-127) over a fresh index (empty     */
+/* offsetCache): sort.Search over byte offsets [0, size) where each probe is findAt(h) =        */
+/* MMapProtoReader.SeekNext(h) (recordio/proto/mmap_proto_reader.go:26-38) + proto.Unmarshal    */
+/* into an IndexEntry. An io.EOF probe ends the search as "not found" at offset size; any other */
+/* probe error is returned. Status: RIO_OK, the SeekNext error, or ORC_ERR_PROTO.              */
+/* ---------------------------------------------------------------------------------------- */
+#define ORC_ERR_PROTO 21
+
+static int bytes_compare(const uint8_t* a, uint64_t an, const uint8_t* b, uint64_t bn) {
+    uint64_t m = an < bn ? an : bn;
+    int c = m ? memcmp(a, b, m) : 0;
+    if (c) return c < 0 ? -1 : 1;
+    return an < bn ? -1 : (an > bn ? 1 : 0);
+}
+
+/* findAt: returns 0 with the entry, or a status; *eof = the error is io.EOF-class */
+static int find_at(const uint8_t* f, uint64_t len, uint64_t h, uint64_t seek_len, uint8_t** rec, uint64_t* key_off,
+                   uint64_t* key_len, uint64_t* vo, uint64_t* cs) {
+    uint64_t ro, rl;
+    int nil;
+    *rec = NULL;
+    int e = orc_seek_next(f, len, h, seek_len, &ro, rec, &rl, &nil);
+    if (e) return e;
+    if (orc_index_entry(*rec ? *rec : (const uint8_t*)"", nil ? 0 : rl, key_off, key_len, vo, cs)) return ORC_ERR_PROTO;
+    return 0;
+}
+
+int orc_disk_index_search(const uint8_t* f, uint64_t len, const uint8_t* key, uint64_t klen, uint64_t seek_len,
+                          uint64_t* offset, int* found, uint64_t* value_off, uint64_t* checksum) {
+    uint64_t n = len, i = 0, j = n, ko, kl, vo, cs;
+    uint8_t* rec = NULL;
+    *offset = 0;
+    *found = 0;
+    *value_off = *checksum = 0;
+    while (i < j) {
+        uint64_t h = (i + j) >> 1;
+        int e = find_at(f, len, h, seek_len, &rec, &ko, &kl, &vo, &cs);
+        if (e) {
+            free(rec);
+            if (rio_status_is_eof(e)) { *offset = n; return RIO_OK; }
+            return e;
+        }
+        int c = bytes_compare(rec + ko, kl, key, klen);
+        free(rec);
+        rec = NULL;
+        if (c < 0) i = h + 1; else j = h;
+    }
+    int e = find_at(f, len, i, seek_len, &rec, &ko, &kl, &vo, &cs);
+    if (e) {
+        free(rec);
+        if (rio_status_is_eof(e)) { *offset = n; return RIO_OK; }
+        return e;
+    }
+    *offset = i;
+    *found = i < n && bytes_compare(rec + ko, kl, key, klen) == 0;
+    if (*found) { *value_off = vo; *checksum = cs; }
+    free(rec);
+    return RIO_OK;
+}

@@ -61,6 +61,9 @@ int orc_index_entry(const uint8_t* b, uint64_t n, uint64_t* key_off, uint64_t* k
                     uint64_t* checksum);
 /* sstables: index load + validateDataFile + Scan over in-memory images (CPU baseline of config 5);
  * entries scanned, *first_bad = first checksum mismatch or UINT64_MAX */
+/* DiskKeyIndex.binarySearch over a fresh index (disk_key_index.go:87-127); ORC_ERR_PROTO = 21 */
+int orc_disk_index_search(const uint8_t* f, uint64_t len, const uint8_t* key, uint64_t klen, uint64_t seek_len,
+                          uint64_t* offset, int* found, uint64_t* value_off, uint64_t* checksum);
 uint64_t orc_sst_scan(const uint8_t* index, uint64_t ilen, const uint8_t* data, uint64_t dlen, uint64_t* first_bad);
 
 #ifdef __cplusplus

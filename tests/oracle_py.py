@@ -47,6 +47,8 @@ def lib():
         L.orc_crc64_iso.argtypes = [c_void_p, c_uint64]
         L.orc_index_entry.argtypes = [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
                                       POINTER(c_uint64)]
+        L.orc_disk_index_search.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, POINTER(c_uint64),
+                                            POINTER(c_int), POINTER(c_uint64), POINTER(c_uint64)]
         _lib = L
     return _lib
 
@@ -188,3 +190,25 @@ def sstable_oracle(base: str) -> dict:
     return {"index_status": idx["status"], "data_status": dat["status"], "entries": entries,
             "bad_proto": bad_proto, "values": dat["records"], "crcs": crcs, "first_bad": first_bad,
             "unplaced": unplaced}
+
+
+def disk_index_search(index: bytes, key: bytes, seek_len: int = 4096):
+    """DiskKeyIndex.binarySearch restatement on a fresh index: (status, offset, found, valueOffset, checksum)."""
+    b, n = _buf(index)
+    off, vo, cs = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    found = ctypes.c_int()
+    kb = bytes(key) or b"\0"
+    st = lib().orc_disk_index_search(b, n, kb, len(key), seek_len, byref(off), byref(found), byref(vo), byref(cs))
+    return st, off.value, bool(found.value), vo.value, cs.value
+
+
+def seek_next_entries(index: bytes, start: int, end: int):
+    """DiskKeyIndexIterator.Next loop (disk_key_index.go:141-165) with the oracle's SeekNext: keys."""
+    out, cur = [], start
+    while cur <= end:
+        st, ro, rec = seek_next(index, cur)
+        if st != 0:
+            break
+        out.append(index_entry(rec or b"")[0])
+        cur = ro + 1
+    return out
