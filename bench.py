@@ -10,9 +10,10 @@ rio_device_decode call. value = input file bytes decoded by all ranks / max-over
 Multi-GPU: one process per GPU (torchrun); every rank decodes its own file (file sharding, no
 data-path collective; the only collectives are the timing barrier and the max-over-ranks).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2g|c1|c3|c4|c5|wal]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2g|c1|c3|c4|c5|wal|idx]
 
-c5 (SSTable load + validation + scan) and wal (ordered WAL replay from host files) print their own
+c5 (SSTable load + validation + scan), wal (ordered WAL replay from host files) and idx (batched
+DiskKeyIndex.Get) print their own
 metric lines; the default (c2) line is the BASELINE.json metric.
 """
 from __future__ import annotations
@@ -44,11 +45,14 @@ CONFIGS = {
     "c2g": (1_000_000, 1024, 1, 1, "C2-gzip: recordio v4, 1M x 1 KiB gzip records (text-like), one file per GPU"),
     "wal": (WAL_FILES * WAL_RECORDS_PER_FILE, 1024, 2, 1, "WAL replay: 8 x ~128 MiB snappy WAL files (1 KiB "
                                                           "text-like records) per GPU, sorted, delivered in order"),
+    "idx": (1_000_000, 20, 0, 0, "DiskKeyIndex Get: 1M SHA1 keys (half present) against the C5 index.rio "
+                                 "(1.25M entries), one lane per key"),
     "c5": (1_250_000, 1024, 2, 0, "C5: SSTable load + validateDataFile + full scan, 1.25M SHA1 keys x 1 KiB values "
                                   "(data.rio snappy v4 + index.rio v4), one table per GPU (10M keys over 8 GPUs)"),
 }
 SST_METRIC = "sstable full scan GiB/s (device-resident: index load + CRC-64 validation + data decode)"
 WAL_METRIC = "wal replay GiB/s (host WAL files -> ordered host records, PCIe-inclusive)"
+IDX_METRIC = "DiskKeyIndex lookups/s (device-resident index.rio, batched Get)"
 PCIE_PEAK_GBPS = 128.0  # PCIe Gen5 x16, both directions (64 GB/s each)
 DECODE_KERNEL = {0: "k_decode_copy", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
 
@@ -407,6 +411,106 @@ def run_wal(args, world, rank, local, device):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def run_index(args, world, rank, local, device):
+    """One step = DiskKeyIndex.Get for a batch of keys (disk_key_index.go:36-49) on the device: every
+    lane runs the reference's binarySearch (SeekNext probes + IndexEntry parse + key compare) over
+    the C5 table's index.rio, resident in HBM."""
+    import hashlib
+    import struct
+
+    import numpy as np
+    import torch
+
+    from recordio import _lib as L
+    from recordio.device import to_device_file
+
+    n_entries = CONFIGS["c5"][0]
+    nq = CONFIGS["idx"][0]
+    index_img, _ = sstable_images(n_entries, rank)
+    d_index, li = to_device_file(index_img, local)
+    rng = np.random.default_rng(rank_seed(rank))
+    # present keys (the table's SHA1 keys) and absent ones (SHA1 of other integers), shuffled
+    ids = rng.integers(0, n_entries, nq // 2)
+    keys = [hashlib.sha1(struct.pack(">I", rank * n_entries + int(i))).digest() for i in ids]
+    keys += [hashlib.sha1(struct.pack(">I", 0x80000000 + rank * nq + i)).digest() for i in range(nq - nq // 2)]
+    order = rng.permutation(nq)
+    keys = [keys[i] for i in order]
+    blob = np.frombuffer(b"".join(keys), dtype=np.uint8)
+    off = np.arange(nq + 1, dtype=np.int64) * 20
+    d_keys = torch.from_numpy(blob.copy()).to(device)
+    d_off = torch.from_numpy(off).to(device)
+    hit_sz = ctypes.sizeof(L.IndexHit)
+    d_hits = torch.empty(nq * hit_sz, dtype=torch.uint8, device=device)
+    lib = L.lib()
+    ctx = L.default_ctx(local)
+    stream = torch.cuda.Stream(device=device)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        rc = lib.rio_device_index_search(ctx, d_index.data_ptr(), li, 0, d_keys.data_ptr(), d_off.data_ptr(), nq,
+                                         d_hits.data_ptr(), sp)
+        if rc:
+            raise RuntimeError(L.strerror(rc))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    hits = (L.IndexHit * nq).from_buffer_copy(d_hits.cpu().numpy().tobytes())
+    found = sum(h.found for h in hits)
+    if any(h.status for h in hits) or found < nq // 2 - nq // 100:
+        raise RuntimeError(f"index search: found {found} of {nq // 2} present keys")
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    value, ms_per_step, _ = job_throughput(dt, nq, args.steps, world, device)
+    value *= 2**30  # job_throughput reports units / 2^30 per second; here the unit is one lookup
+    alg = nq * (20 + 8 + hit_sz)  # key + its offset in, one hit out
+    line = {
+        "metric": IDX_METRIC, "value": round(value, 1), "unit": "lookups/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: C5 table's index (SHA1 keys), half the queries present",
+        "config": {"workload": CONFIGS["idx"][4], "queries": nq, "index_entries": n_entries, "index_bytes": li,
+                   "found": found, "parallelism": f"index per rank x{world}, no data-path collectives"},
+        "roofline": {"bound": "hbm", "achieved": round(alg / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "k_index_search", "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg,
+                     "note": "dependent probe chains (~21 SeekNext probes per key): latency-bound, not bandwidth"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        import oracle_py as orc
+
+        olib = orc.lib()
+        o_off, o_vo, o_cs, o_found = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        base = index_img.ctypes.data  # the index image in place: no per-query copy
+        kbuf = ctypes.create_string_buffer(blob.tobytes(), len(blob))
+        kaddr = ctypes.addressof(kbuf)
+        t1 = time.perf_counter()
+        m = 0
+        while m < nq and time.perf_counter() - t1 < 10.0:
+            st = olib.orc_disk_index_search(base, li, kaddr + 20 * m, 20, 4096, ctypes.byref(o_off),
+                                            ctypes.byref(o_found), ctypes.byref(o_vo), ctypes.byref(o_cs))
+            if st or bool(o_found.value) != bool(hits[m].found) or o_off.value != hits[m].offset:
+                raise RuntimeError(f"oracle index search disagrees with the device at query {m}")
+            m += 1
+        t_cpu = time.perf_counter() - t1
+        line["cpu_baseline"] = {"value": round(m / t_cpu, 1), "unit": "lookups/s", "cores": 1, "kind": "port",
+                                "sample": f"first {m} queries, oracle binarySearch restatement (one SeekNext "
+                                f"window + IndexEntry parse per probe), {_cpu_model()}"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -429,8 +533,8 @@ def main():
 
         dist.init_process_group(backend="nccl", device_id=device)
 
-    if args.config in ("c5", "wal"):
-        (run_sstable if args.config == "c5" else run_wal)(args, world, rank, local, device)
+    if args.config in ("c5", "wal", "idx"):
+        {"c5": run_sstable, "wal": run_wal, "idx": run_index}[args.config](args, world, rank, local, device)
         if world > 1:
             torch.distributed.destroy_process_group()
         return
