@@ -36,6 +36,10 @@ hipError_t launch_sst_validate(const uint8_t* data, const uint64_t* data_off, co
                                uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s);
 hipError_t launch_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len, const uint8_t* keys,
                                const uint64_t* key_off, uint64_t nq, rio_index_hit* hits, hipStream_t s);
+hipError_t launch_encode(const EncParams& P, void* cub_tmp, size_t cub_bytes, hipStream_t s);
+uint64_t enc_scratch_bytes(uint64_t n, uint64_t bytes, uint32_t compression);
+uint64_t enc_table_bytes();
+size_t enc_cub_bytes(uint64_t n);
 hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t* out, uint64_t out_cap,
                           ReadAtResult* res, hipStream_t s);
 hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
@@ -157,6 +161,10 @@ struct rio_ctx {
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
     // rio_sst_open: parsed index fields (4 x n), per-entry CRC-64, kernel results
     DevBuf sst_fields, sst_crc, sst_res;
+    // rio_device_encode: compressed payloads, their offsets and lengths, hash tables, headers,
+    // record sizes, scan temp; rio_encode_file: records, offsets, flags, file image, record offsets
+    DevBuf enc_scr, enc_scr_off, enc_clen, enc_tab, enc_hdr, enc_size, enc_tmp, enc_cub;
+    DevBuf enc_rec, enc_rec_off, enc_flags, enc_out, enc_out_off, enc_len;
     uint8_t* pinned[2] = {nullptr, nullptr};
     hipEvent_t pin_ev[2] = {};
     // last host-API framing (rio_frame -> rio_decode)
@@ -233,7 +241,9 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->rec_desc, &c->sink, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
                       &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
-                      &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res})
+                      &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res, &c->enc_scr, &c->enc_scr_off, &c->enc_clen, &c->enc_tab,
+                      &c->enc_hdr, &c->enc_size, &c->enc_tmp, &c->enc_cub, &c->enc_rec, &c->enc_rec_off, &c->enc_flags, &c->enc_out,
+                      &c->enc_out_off, &c->enc_len})
         b->release();
     for (int i = 0; i < 2; i++) {
         if (c->pinned[i]) hipHostFree(c->pinned[i]);
@@ -971,4 +981,87 @@ extern "C" void rio_index_free(rio_index* x) {
     x->key_off.release();
     x->hits.release();
     delete x;
+}
+
+// ------------------------------------------------------------------------------------------
+// recordio v4 encoding (rio_encode.hip)
+// ------------------------------------------------------------------------------------------
+extern "C" uint64_t rio_encode_bound(uint64_t n, uint64_t total_bytes, uint32_t compression) {
+    const uint64_t payload = compression == RIO_COMP_SNAPPY ? 32 * n + total_bytes + total_bytes / 6 : total_bytes;
+    return RIO_FILE_HEADER_BYTES + RIO_RECORD_HEADER_V4_MAX * n + payload + 64;
+}
+
+extern "C" int rio_device_encode(rio_ctx* ctx, const uint8_t* d_records, const uint64_t* d_rec_off,
+                                 const uint8_t* d_flags, uint64_t n, uint64_t total_bytes, uint32_t compression,
+                                 uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_rec_off, uint64_t* d_out_len,
+                                 void* stream) {
+    if (!ctx || !d_rec_off || !d_out || !d_out_len || (n && (!d_records || !d_out_rec_off))) return RIO_ERR_ARG;
+    if (compression != RIO_COMP_NONE && compression != RIO_COMP_SNAPPY) return RIO_ERR_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t cub = std::max<size_t>(enc_cub_bytes(n), 256);
+    HIP_TRY(ctx->enc_scr.ensure(enc_scratch_bytes(n, total_bytes, compression)));
+    HIP_TRY(ctx->enc_scr_off.ensure((n + 1) * 8));
+    HIP_TRY(ctx->enc_clen.ensure(n * 8 + 8));
+    // per-lane global hash tables only when some record can exceed the LDS kernel's 1 KiB
+    if (compression == RIO_COMP_SNAPPY && total_bytes > 1024) HIP_TRY(ctx->enc_tab.ensure(enc_table_bytes()));
+    HIP_TRY(ctx->enc_hdr.ensure(n * 64 + 64));
+    HIP_TRY(ctx->enc_size.ensure((n + 1) * 8));
+    HIP_TRY(ctx->enc_tmp.ensure((n + 1) * 8));
+    HIP_TRY(ctx->enc_cub.ensure(cub));
+    EncParams P{};
+    P.rec = d_records;
+    P.rec_off = d_rec_off;
+    P.flags = d_flags;
+    P.n = n;
+    P.compression = compression;
+    P.scratch = ctx->enc_scr.as<uint8_t>();
+    P.scr_off = ctx->enc_scr_off.as<uint64_t>();
+    P.clen = ctx->enc_clen.as<uint64_t>();
+    P.gtab = ctx->enc_tab.as<uint16_t>();
+    P.hdr = ctx->enc_hdr.as<uint8_t>();
+    P.size = ctx->enc_size.as<uint64_t>();
+    P.tmp = ctx->enc_tmp.as<uint64_t>();
+    P.out = d_out;
+    P.out_cap = out_cap;
+    P.out_rec_off = d_out_rec_off;
+    P.out_len = d_out_len;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(launch_encode(P, ctx->enc_cub.p, ctx->enc_cub.cap, s));
+    return RIO_OK;
+}
+
+extern "C" int rio_encode_file(rio_ctx* ctx, const uint8_t* records, const uint64_t* rec_off, const uint8_t* flags,
+                               uint64_t n, uint32_t compression, uint8_t* out, uint64_t out_cap, uint64_t* out_rec_off,
+                               uint64_t* out_len) {
+    if (!ctx || !rec_off || !out_len || (n && !out_rec_off)) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const uint64_t total = rec_off[n] - rec_off[0];
+    if (total && !records) return RIO_ERR_ARG;
+    const uint64_t bound = rio_encode_bound(n, total, compression);
+    HIP_TRY(ctx->enc_rec.ensure(total + RIO_DEVICE_PAD));
+    HIP_TRY(ctx->enc_rec_off.ensure((n + 1) * 8));
+    HIP_TRY(ctx->enc_flags.ensure(n + 8));
+    HIP_TRY(ctx->enc_out.ensure(bound));
+    HIP_TRY(ctx->enc_out_off.ensure(n * 8 + 8));
+    HIP_TRY(ctx->enc_len.ensure(8));
+    int rc = total ? h2d_staged(ctx, ctx->enc_rec.p, records + rec_off[0], total) : RIO_OK;
+    // offsets relative to the first record
+    std::vector<uint64_t> rel(n + 1);
+    for (uint64_t i = 0; i <= n; i++) rel[i] = rec_off[i] - rec_off[0];
+    if (!rc) rc = h2d_staged(ctx, ctx->enc_rec_off.p, reinterpret_cast<const uint8_t*>(rel.data()), (n + 1) * 8);
+    if (!rc && flags && n) rc = h2d_staged(ctx, ctx->enc_flags.p, flags, n);
+    if (rc) return rc;
+    rc = rio_device_encode(ctx, ctx->enc_rec.as<uint8_t>(), ctx->enc_rec_off.as<uint64_t>(),
+                           flags ? ctx->enc_flags.as<uint8_t>() : nullptr, n, total, compression,
+                           ctx->enc_out.as<uint8_t>(), bound, ctx->enc_out_off.as<uint64_t>(),
+                           ctx->enc_len.as<uint64_t>(), nullptr);
+    if (rc) return rc;
+    uint64_t len = 0;
+    rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(&len), ctx->enc_len.p, 8);
+    if (rc) return rc;
+    *out_len = len;
+    if (len > out_cap || !out) return RIO_ERR_CAPACITY;
+    rc = d2h_staged(ctx, out, ctx->enc_out.p, len);
+    if (!rc && n) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(out_rec_off), ctx->enc_out_off.p, n * 8);
+    return rc;
 }

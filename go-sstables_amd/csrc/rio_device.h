@@ -113,4 +113,24 @@ struct FrameParams {
     rio_file_info* info;  // device copy of the public result
 };
 
+// rio_encode.hip: recordio v4 encoding of a batch of records (rio_device_encode)
+struct EncParams {
+    const uint8_t* rec;        // records arena
+    const uint64_t* rec_off;   // [n + 1]
+    const uint8_t* flags;      // [n] RIO_FLAG_NIL, or null
+    uint64_t n;
+    uint32_t compression;
+    uint8_t* scratch;          // compressed payloads, record i at scr_off[i]
+    uint64_t* scr_off;         // [n + 1]
+    uint64_t* clen;            // [n] payload length in the file (c for snappy, u for none)
+    uint16_t* gtab;            // global tables: kMaxTable entries per lane of k_snappy_encode<false>
+    uint8_t* hdr;              // [n][kHdrSlot] header bytes; hdr[i * kHdrSlot + 63] = header length
+    uint64_t* size;            // [n + 1] exclusive scan of the record sizes = file offsets - 8
+    uint64_t* tmp;             // [n + 1] scan inputs (payload bounds, then record sizes)
+    uint8_t* out;
+    uint64_t out_cap;
+    uint64_t* out_rec_off;     // [n] file offset of each record (what Write returns)
+    uint64_t* out_len;         // [1] file length
+};
+
 }  // namespace rio

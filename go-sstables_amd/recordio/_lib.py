@@ -151,6 +151,13 @@ _SIGS = {
     "rio_replay_next": (
         c_int, [c_void_p, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(FileInfo)]),
     "rio_replay_free": (None, [c_void_p]),
+    "rio_encode_bound": (c_uint64, [c_uint64, c_uint64, c_uint32]),
+    "rio_device_encode": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p,
+                c_void_p, c_void_p]),
+    "rio_encode_file": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p,
+                POINTER(c_uint64)]),
     "rio_device_index_search": (
         c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
     "rio_index_open": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_void_p)]),

@@ -206,6 +206,24 @@ int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, uint64_t* k
                   uint64_t* value_len, int* is_nil, uint64_t* value_offset, uint64_t* checksum, uint64_t* crc);
 void rio_sst_free(rio_sst* t);
 
+/* ---- recordio v4 encoding on the device (the write side: FileWriter.Write for a batch) --------
+ * Replaces a loop of FileWriter.Write (recordio/file_writer.go:189-233; compaction output,
+ * sstable_merger.go:36-169): record i = d_records[d_rec_off[i] .. d_rec_off[i+1]) (RIO_DEVICE_PAD
+ * readable bytes past the arena end), d_flags[i] & RIO_FLAG_NIL marks a nil record (d_flags NULL =
+ * none), compression RIO_COMP_NONE or RIO_COMP_SNAPPY (golang/snappy v1.0.0 block encoding). The
+ * whole v4 file (8-byte header + records) goes to d_out, byte-identical to the reference writer; record
+ * i's file offset (what Write returns) to d_out_rec_off[i], the file length to *d_out_len. With
+ * out_cap >= rio_encode_bound(n, total_bytes) the file always fits; otherwise nothing is written
+ * when *d_out_len > out_cap. Stream-ordered, no host sync. total_bytes = d_rec_off[n]. */
+uint64_t rio_encode_bound(uint64_t n_records, uint64_t total_bytes, uint32_t compression);
+int rio_device_encode(rio_ctx* ctx, const uint8_t* d_records, const uint64_t* d_rec_off, const uint8_t* d_flags,
+                      uint64_t n, uint64_t total_bytes, uint32_t compression, uint8_t* d_out, uint64_t out_cap,
+                      uint64_t* d_out_rec_off, uint64_t* d_out_len, void* stream);
+/* host-memory form (the cgo binding): H2D of the records, device encode, D2H of the file image and
+ * offsets; *out_len = file length (RIO_ERR_CAPACITY when it exceeds out_cap). Synchronises. */
+int rio_encode_file(rio_ctx* ctx, const uint8_t* records, const uint64_t* rec_off, const uint8_t* flags, uint64_t n,
+                    uint32_t compression, uint8_t* out, uint64_t out_cap, uint64_t* out_rec_off, uint64_t* out_len);
+
 /* ---- DiskKeyIndex lookups (sstables/disk_key_index.go:87-140) --------------------------------
  * Batched DiskKeyIndex.Get / Contains / IteratorStartingAt: one result per query key, each the
  * reference's binarySearch over the byte offsets of an uncompressed index.rio with every probe
