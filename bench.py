@@ -10,10 +10,10 @@ rio_device_decode call. value = input file bytes decoded by all ranks / max-over
 Multi-GPU: one process per GPU (torchrun); every rank decodes its own file (file sharding, no
 data-path collective; the only collectives are the timing barrier and the max-over-ranks).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2g|c1|c3|c4|c5|wal|idx]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2g|c1|c3|c4|c5|wal|idx|enc]
 
-c5 (SSTable load + validation + scan), wal (ordered WAL replay from host files) and idx (batched
-DiskKeyIndex.Get) print their own
+c5 (SSTable load + validation + scan), wal (ordered WAL replay from host files) idx (batched
+DiskKeyIndex.Get) and enc (device v4 encode) print their own
 metric lines; the default (c2) line is the BASELINE.json metric.
 """
 from __future__ import annotations
@@ -47,12 +47,15 @@ CONFIGS = {
                                                           "text-like records) per GPU, sorted, delivered in order"),
     "idx": (1_000_000, 20, 0, 0, "DiskKeyIndex Get: 1M SHA1 keys (half present) against the C5 index.rio "
                                  "(1.25M entries), one lane per key"),
+    "enc": (1_000_000, 1024, 2, 1, "Encode: 1M x 1 KiB text-like records -> recordio v4 snappy file image "
+                                    "(FileWriter.Write batch), device-resident"),
     "c5": (1_250_000, 1024, 2, 0, "C5: SSTable load + validateDataFile + full scan, 1.25M SHA1 keys x 1 KiB values "
                                   "(data.rio snappy v4 + index.rio v4), one table per GPU (10M keys over 8 GPUs)"),
 }
 SST_METRIC = "sstable full scan GiB/s (device-resident: index load + CRC-64 validation + data decode)"
 WAL_METRIC = "wal replay GiB/s (host WAL files -> ordered host records, PCIe-inclusive)"
 IDX_METRIC = "DiskKeyIndex lookups/s (device-resident index.rio, batched Get)"
+ENC_METRIC = "recordio v4 encode GiB/s of records (device-resident, golang/snappy block format)"
 PCIE_PEAK_GBPS = 128.0  # PCIe Gen5 x16, both directions (64 GB/s each)
 DECODE_KERNEL = {0: "k_decode_copy", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
 
@@ -511,6 +514,101 @@ def run_index(args, world, rank, local, device):
         print(json.dumps(line), flush=True)
 
 
+def run_encode(args, world, rank, local, device):
+    """One step = FileWriter.Write for 1M records (file_writer.go:189-233) on the device: snappy
+    block encoding per record, v4 headers with CRC-32C, file offsets, the file image
+    (rio_device_encode). The records come from decoding the C2 file on the device, and the
+    re-encoded image must equal that file byte for byte."""
+    import numpy as np
+    import torch
+
+    from recordio import _lib as L
+    from recordio import generate
+    from recordio.device import DeviceDecoder, to_device_file
+
+    n, rec_len, comp, kind, desc = CONFIGS["enc"]
+    image = generate(n, rec_len, comp, kind, seed=rank_seed(rank), threads=min(16, os.cpu_count() or 1))
+    d_file, flen = to_device_file(image, local)
+    dec = DeviceDecoder(local)
+    b, info = dec.decode(d_file, flen)
+    if info["n_records"] != n:
+        raise RuntimeError(f"decode of the input failed: {info}")
+    total = int(info["total_out_bytes"])
+    lib = L.lib()
+    cap = int(lib.rio_encode_bound(n, total, comp))
+    d_out = torch.empty(cap, dtype=torch.uint8, device=device)
+    d_roff = torch.empty(n, dtype=torch.int64, device=device)
+    d_len = torch.zeros(1, dtype=torch.int64, device=device)
+    ctx = L.default_ctx(local)
+    stream = torch.cuda.Stream(device=device)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        rc = lib.rio_device_encode(ctx, b.out.data_ptr(), b.out_off.data_ptr(), b.flags.data_ptr(), n, total, comp,
+                                   d_out.data_ptr(), cap, d_roff.data_ptr(), d_len.data_ptr(), sp)
+        if rc:
+            raise RuntimeError(L.strerror(rc))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    ln = int(d_len.item())
+    if ln != flen or not torch.equal(d_out[:ln], d_file[:flen]):
+        raise RuntimeError("device encode of the decoded records is not the original file")
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    step_ms = ev0.elapsed_time(ev1) / args.steps
+    value, ms_per_step, _ = job_throughput(dt, total, args.steps, world, device)
+    alg = total + 9 * n + flen  # records + offsets/flags in, the file out
+    line = {
+        "metric": ENC_METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: seeded text-like Zipf-word records (the C2 file decoded on the device), one batch per rank",
+        "config": {"workload": desc, "records": n, "record_bytes": rec_len, "record_total": total, "file_bytes": flen,
+                   "parallelism": f"batch per rank x{world}, no data-path collectives"},
+        "roofline": {"bound": "hbm", "achieved": round(alg / (step_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(alg / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "rio_device_encode (all launches)", "kernel_ms": round(step_ms, 4),
+                     "alg_bytes_per_launch": alg,
+                     "note": "dominated by k_snappy_encode<true>: one lane per record, serial golang/snappy match loop"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        import oracle_py as orc
+
+        recs = b.out[:total].cpu().numpy()
+        offs = b.out_off[:n + 1].cpu().numpy().astype(np.uint64)
+        flags = b.flags[:n].cpu().numpy()
+        m = 100_000
+        sub = np.ascontiguousarray(offs[:m + 1])
+        out = np.empty(int(sub[-1]) * 2 + 64 * m, dtype=np.uint8)
+        olib = orc.lib()
+        runs, t_cpu = 0, 0.0
+        while runs < 5 and t_cpu < 10.0:
+            t1 = time.perf_counter()
+            got = olib.orc_encode_file(recs.ctypes.data, sub.ctypes.data, flags.ctypes.data, m, comp, out.ctypes.data,
+                                       out.shape[0], None)
+            t_cpu += time.perf_counter() - t1
+            runs += 1
+            if not got:
+                raise RuntimeError("oracle encode failed")
+        line["cpu_baseline"] = {"value": round(int(sub[-1]) * runs / 2**30 / t_cpu, 4), "unit": "GiB/s", "cores": 1,
+                                "kind": "port", "sample": f"first {m} records x{runs} runs, oracle FileWriter.Write "
+                                f"+ golang/snappy restatement, {_cpu_model()}"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -533,8 +631,9 @@ def main():
 
         dist.init_process_group(backend="nccl", device_id=device)
 
-    if args.config in ("c5", "wal", "idx"):
-        {"c5": run_sstable, "wal": run_wal, "idx": run_index}[args.config](args, world, rank, local, device)
+    if args.config in ("c5", "wal", "idx", "enc"):
+        {"c5": run_sstable, "wal": run_wal, "idx": run_index, "enc": run_encode}[args.config](
+            args, world, rank, local, device)
         if world > 1:
             torch.distributed.destroy_process_group()
         return

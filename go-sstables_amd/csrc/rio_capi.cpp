@@ -1003,7 +1003,7 @@ extern "C" int rio_device_encode(rio_ctx* ctx, const uint8_t* d_records, const u
     HIP_TRY(ctx->enc_scr_off.ensure((n + 1) * 8));
     HIP_TRY(ctx->enc_clen.ensure(n * 8 + 8));
     // per-lane global hash tables only when some record can exceed the LDS kernel's 1 KiB
-    if (compression == RIO_COMP_SNAPPY && total_bytes > 1024) HIP_TRY(ctx->enc_tab.ensure(enc_table_bytes()));
+    if (compression == RIO_COMP_SNAPPY) HIP_TRY(ctx->enc_tab.ensure(enc_table_bytes()));
     HIP_TRY(ctx->enc_hdr.ensure(n * 64 + 64));
     HIP_TRY(ctx->enc_size.ensure((n + 1) * 8));
     HIP_TRY(ctx->enc_tmp.ensure((n + 1) * 8));

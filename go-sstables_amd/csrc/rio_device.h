@@ -131,6 +131,7 @@ struct EncParams {
     uint64_t out_cap;
     uint64_t* out_rec_off;     // [n] file offset of each record (what Write returns)
     uint64_t* out_len;         // [1] file length
+    uint32_t lds_small;        // records <= 1 KiB on the LDS-table kernel
 };
 
 }  // namespace rio

@@ -768,3 +768,148 @@ int orc_disk_index_search(const uint8_t* f, uint64_t len, const uint8_t* key, ui
     free(rec);
     return RIO_OK;
 }
+
+/* ---------------------------------------------------------------------------------------- */
+/* Write side (checker and CPU baseline of rio_device_encode): FileWriter.Write over a batch    */
+/* (recordio/file_writer.go:160-233) with golang/snappy v1.0.0's Encode (encode.go:18-41,       */
+/* encode_other.go: emitLiteral, emitCopy, encodeBlock). Restated from the published Go source. */
+/* ---------------------------------------------------------------------------------------- */
+static uint32_t le32(const uint8_t* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static uint64_t le64(const uint8_t* p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static uint32_t snappy_hash(uint32_t u, uint32_t shift) { return (u * 0x1e35a7bdu) >> shift; }
+
+static uint64_t w_uvarint(uint8_t* b, uint64_t v) {
+    uint64_t i = 0;
+    for (; v >= 0x80; v >>= 7) b[i++] = (uint8_t)(v | 0x80);
+    b[i++] = (uint8_t)v;
+    return i;
+}
+
+static uint64_t w_literal(uint8_t* dst, const uint8_t* lit, uint64_t n) {
+    uint64_t i, m = n - 1;
+    if (m < 60) { dst[0] = (uint8_t)(m << 2); i = 1; }
+    else if (m < 256) { dst[0] = 60 << 2; dst[1] = (uint8_t)m; i = 2; }
+    else { dst[0] = 61 << 2; dst[1] = (uint8_t)m; dst[2] = (uint8_t)(m >> 8); i = 3; }
+    memcpy(dst + i, lit, n);
+    return i + n;
+}
+
+static uint64_t w_copy(uint8_t* dst, uint64_t offset, uint64_t length) {
+    uint64_t i = 0;
+    for (; length >= 68; length -= 64, i += 3) {
+        dst[i] = 63 << 2 | 2; dst[i + 1] = (uint8_t)offset; dst[i + 2] = (uint8_t)(offset >> 8);
+    }
+    if (length > 64) {
+        dst[i] = 59 << 2 | 2; dst[i + 1] = (uint8_t)offset; dst[i + 2] = (uint8_t)(offset >> 8);
+        i += 3;
+        length -= 60;
+    }
+    if (length >= 12 || offset >= 2048) {
+        dst[i] = (uint8_t)((length - 1) << 2 | 2); dst[i + 1] = (uint8_t)offset; dst[i + 2] = (uint8_t)(offset >> 8);
+        return i + 3;
+    }
+    dst[i] = (uint8_t)((offset >> 8) << 5 | (length - 4) << 2 | 1);
+    dst[i + 1] = (uint8_t)offset;
+    return i + 2;
+}
+
+static uint64_t w_block(uint8_t* dst, const uint8_t* src, int64_t n) {
+    static uint16_t table[1 << 14];
+    uint32_t shift = 24;
+    for (int64_t ts = 1 << 8; ts < (1 << 14) && ts < n; ts *= 2) shift--;
+    memset(table, 0, sizeof table);
+    uint64_t d = 0;
+    const int64_t s_limit = n - 15;
+    int64_t next_emit = 0, s = 1;
+    uint32_t next_hash = snappy_hash(le32(src + s), shift);
+    for (;;) {
+        int64_t skip = 32, next_s = s, candidate = 0;
+        for (;;) {
+            s = next_s;
+            int64_t between = skip >> 5;
+            next_s = s + between;
+            skip += between;
+            if (next_s > s_limit) goto remainder;
+            candidate = table[next_hash];
+            table[next_hash] = (uint16_t)s;
+            next_hash = snappy_hash(le32(src + next_s), shift);
+            if (le32(src + s) == le32(src + candidate)) break;
+        }
+        d += w_literal(dst + d, src + next_emit, (uint64_t)(s - next_emit));
+        for (;;) {
+            int64_t base = s;
+            s += 4;
+            for (int64_t i = candidate + 4; s < n && src[i] == src[s]; i++, s++) {}
+            d += w_copy(dst + d, (uint64_t)(base - candidate), (uint64_t)(s - base));
+            next_emit = s;
+            if (s >= s_limit) goto remainder;
+            uint64_t x = le64(src + s - 1);
+            table[snappy_hash((uint32_t)x, shift)] = (uint16_t)(s - 1);
+            uint32_t ch = snappy_hash((uint32_t)(x >> 8), shift);
+            candidate = table[ch];
+            table[ch] = (uint16_t)s;
+            if ((uint32_t)(x >> 8) != le32(src + candidate)) {
+                next_hash = snappy_hash((uint32_t)(x >> 16), shift);
+                s++;
+                break;
+            }
+        }
+    }
+remainder:
+    if (next_emit < n) d += w_literal(dst + d, src + next_emit, (uint64_t)(n - next_emit));
+    return d;
+}
+
+/* snappy.Encode into dst (capacity >= 32 + n + n / 6) */
+uint64_t orc_snappy_encode(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    uint64_t d = w_uvarint(dst, n);
+    while (n > 0) {
+        uint64_t blk = n < 65536 ? n : 65536;
+        d += blk < 17 ? w_literal(dst + d, src, blk) : w_block(dst + d, src, (int64_t)blk);
+        src += blk;
+        n -= blk;
+    }
+    return d;
+}
+
+/* The file FileWriter writes for these records (compression none or snappy): returns its length,
+ * or 0 when it would exceed cap. rec_off[i] = file offset of record i (Write's return value). */
+uint64_t orc_encode_file(const uint8_t* records, const uint64_t* off, const uint8_t* flags, uint64_t n, uint32_t comp,
+                         uint8_t* out, uint64_t cap, uint64_t* rec_off) {
+    if (cap < 8) return 0;
+    uint64_t o = 8;
+    out[0] = 4; out[1] = out[2] = out[3] = 0;
+    out[4] = (uint8_t)comp; out[5] = out[6] = out[7] = 0;
+    uint8_t* scratch = NULL;
+    uint64_t scap = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        int nil = flags && (flags[i] & 1);
+        uint64_t u = nil ? 0 : off[i + 1] - off[i], c = 0;
+        const uint8_t* pay = records + off[i];
+        uint64_t plen = u;
+        if (comp == RIO_COMP_SNAPPY) {
+            if (scap < 32 + u + u / 6) {
+                free(scratch);
+                scap = 32 + u + u / 6;
+                scratch = (uint8_t*)malloc(scap);
+            }
+            c = orc_snappy_encode(scratch, pay, u);
+            pay = scratch;
+            plen = c;
+        }
+        uint8_t h[40];
+        uint64_t k = w_uvarint(h, 0x130691);
+        h[k++] = nil ? 1 : 0;
+        k += w_uvarint(h + k, u);
+        k += w_uvarint(h + k, c);
+        k += w_uvarint(h + k, orc_crc32c(h, k));
+        uint64_t sz = k + (nil ? 0 : plen);
+        if (o + sz > cap) { free(scratch); return 0; }
+        memcpy(out + o, h, k);
+        if (!nil && plen) memcpy(out + o + k, pay, plen);
+        if (rec_off) rec_off[i] = o;
+        o += sz;
+    }
+    free(scratch);
+    return o;
+}

@@ -64,6 +64,10 @@ int orc_index_entry(const uint8_t* b, uint64_t n, uint64_t* key_off, uint64_t* k
 /* DiskKeyIndex.binarySearch over a fresh index (disk_key_index.go:87-127); ORC_ERR_PROTO = 21 */
 int orc_disk_index_search(const uint8_t* f, uint64_t len, const uint8_t* key, uint64_t klen, uint64_t seek_len,
                           uint64_t* offset, int* found, uint64_t* value_off, uint64_t* checksum);
+/* FileWriter.Write over a batch with golang/snappy v1.0.0 (write-side checker / CPU baseline) */
+uint64_t orc_snappy_encode(uint8_t* dst, const uint8_t* src, uint64_t n);
+uint64_t orc_encode_file(const uint8_t* records, const uint64_t* off, const uint8_t* flags, uint64_t n, uint32_t comp,
+                         uint8_t* out, uint64_t cap, uint64_t* rec_off);
 uint64_t orc_sst_scan(const uint8_t* index, uint64_t ilen, const uint8_t* data, uint64_t dlen, uint64_t* first_bad);
 
 #ifdef __cplusplus

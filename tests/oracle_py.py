@@ -49,6 +49,10 @@ def lib():
                                       POINTER(c_uint64)]
         L.orc_disk_index_search.argtypes = [c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, POINTER(c_uint64),
                                             POINTER(c_int), POINTER(c_uint64), POINTER(c_uint64)]
+        L.orc_snappy_encode.restype = c_uint64
+        L.orc_snappy_encode.argtypes = [c_void_p, c_void_p, c_uint64]
+        L.orc_encode_file.restype = c_uint64
+        L.orc_encode_file.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p]
         _lib = L
     return _lib
 
@@ -212,3 +216,20 @@ def seek_next_entries(index: bytes, start: int, end: int):
         out.append(index_entry(rec or b"")[0])
         cur = ro + 1
     return out
+
+
+def encode_file(records, comp):
+    """FileWriter.Write over a batch (oracle restatement): (file bytes, record offsets)."""
+    import numpy as np
+
+    n = len(records)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum([0 if r is None else len(r) for r in records], out=off[1:])
+    blob = b"".join(r or b"" for r in records) + b"\0"
+    flags = np.array([1 if r is None else 0 for r in records] + [0], dtype=np.uint8)
+    cap = 8 + n * 40 + int(off[-1]) * 7 // 6 + 32 * n + 64
+    out = ctypes.create_string_buffer(cap)
+    roff = np.zeros(max(n, 1), dtype=np.uint64)
+    ln = lib().orc_encode_file(blob, off.ctypes.data, flags.ctypes.data, n, comp, out, cap, roff.ctypes.data)
+    assert ln
+    return out.raw[:ln], [int(x) for x in roff[:n]]

@@ -1,13 +1,16 @@
 """recordio v4 encoding on the device (GPU): rio_encode_file / rio_device_encode vs the reference
 writer. The reference's own v4 fixtures pin the expected bytes directly where they exist
 (recordio/test_files/v4_compat, written by FileWriter with golang/snappy v1.0.0). Elsewhere the
-expected bytes come from the host writer restatement, which tests/test_writer.py pins to the same
-fixtures. Plus round trips through the device decoder."""
+expected bytes come from the oracle's restatement (oracle/rio_oracle.c orc_encode_file) and the host
+writer, both pinned to the same fixtures by tests/test_writer.py. Plus round trips through the
+device decoder."""
 import ctypes
 import random
 
 import numpy as np
 import pytest
+
+import oracle_py as orc
 
 from conftest import read_fixture
 from corpus import mixed_records, text_records
@@ -40,14 +43,6 @@ def device_encode(records, comp):
     return out.raw[:ln.value], [int(x) for x in roff[:n]]
 
 
-def writer_offsets(img_records, comp):
-    offs, o = [], 8
-    for r in img_records:
-        offs.append(o)
-        o += len(encode_file([r], comp)) - 8
-    return offs
-
-
 @pytest.mark.parametrize("name,records,comp", [
     ("recordio_UncompressedSingleRecord", [asc(13)], 0),
     ("recordio_UncompressedWriterMultiRecord_asc", [asc(i) for i in range(255)], 0),
@@ -77,10 +72,11 @@ def test_byte_identical_to_writer(comp, kind):
         base = b"".join(text_records(200, seed=13, lo=500, hi=1500))
         recs = [base[:1024], base[:1025], base[:65536], base[:65537], base[:200000], bytes(150000), None, b""]
     img, offs = device_encode(recs, comp)
-    want = encode_file(recs, comp)
+    want, want_offs = orc.encode_file(recs, comp)
     assert len(img) == len(want)
     assert img == want
-    assert offs == writer_offsets(recs, comp)
+    assert img == encode_file(recs, comp)
+    assert offs == want_offs
 
 
 @pytest.mark.parametrize("comp", [0, 2])

@@ -27,6 +27,16 @@ def asc(n):
 ])
 def test_generator_byte_identical_to_reference_writer(name, records, comp):
     assert encode_file(records, comp) == read_fixture("v4_compat", name)
+    # the oracle's restatement (checker of the device encoder) too
+    assert orc.encode_file(records, comp)[0] == read_fixture("v4_compat", name)
+
+
+@pytest.mark.parametrize("comp", [0, 2])
+def test_oracle_encoder_matches_generator(comp):
+    from corpus import mixed_records
+
+    recs = mixed_records(1500, seed=comp + 40, max_len=70000)
+    assert orc.encode_file(recs, comp)[0] == encode_file(recs, comp)
 
 
 def test_writer_size_kats(tmp_path, expectations):
