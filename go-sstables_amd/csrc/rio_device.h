@@ -65,6 +65,8 @@ struct ScanState {
     uint64_t decode_err_rec;  // min 2 * record + (1: cannot be placed -> unsupported) that failed (kNone = none)
     uint32_t capacity_fail;
     uint32_t huge_streams;  // a record stream exceeds 32-bit positions: k_snappy_global runs
+    uint32_t any_mixed;     // snappy: some record is not one literal covering its output (k_place);
+                            // 0 => every record is copied by k_snappy_literal instead of k_snappy_pipe
 };
 
 // Result of the single-record (ReadNextAt) kernel.

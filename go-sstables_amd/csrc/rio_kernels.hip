@@ -311,6 +311,7 @@ __global__ void k_header(FrameParams P) {
     st->decode_err_rec = kNone;
     st->capacity_fail = 0;
     st->huge_streams = 0;
+    st->any_mixed = 0;
     st->slow = 0;
     if (P.len < RIO_FILE_HEADER_BYTES) {
         st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;
@@ -815,6 +816,36 @@ __global__ void __launch_bounds__(1024) k_scan_top(FrameParams P) {
     if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
 }
 
+// Header length of a snappy stream that is one literal element producing exactly `len` bytes with
+// nothing after it, or 0 (an empty stream for an empty record counts as such, header length 0 is
+// then harmless). Tag 00: literal, length - 1 = tag >> 2, or 60..63 => 1..4 little-endian bytes.
+__device__ __forceinline__ uint32_t snappy_literal_hdr(const uint8_t* p, uint64_t slen, uint64_t len) {
+    if (slen == 0) return len == 0 ? 1u : 0u;
+    // one literal = 1..5 header bytes + exactly len data bytes: decided from the sizes alone for
+    // every compressible record, so only candidates cost a load
+    if (slen <= len || slen > len + 5) return 0;
+    const uint32_t tag = p[0];
+    if (tag & 3u) return 0;
+    const uint32_t x = tag >> 2;
+    uint64_t L;
+    uint32_t h;
+    if (x < 60) {
+        L = (uint64_t)x + 1;
+        h = 1;
+    } else {
+        const uint32_t nb = x - 59;
+        if (slen < 1 + nb) return 0;
+        uint64_t v = 0;
+        for (uint32_t b = 0; b < nb; b++) v |= (uint64_t)p[1 + b] << (8 * b);
+        L = v + 1;
+        h = 1 + nb;
+    }
+    return (L == len && h + L == slen) ? h : 0u;
+}
+__device__ __forceinline__ bool snappy_single_literal(const uint8_t* p, uint64_t slen, uint64_t len) {
+    return snappy_literal_hdr(p, slen, len) != 0;
+}
+
 // Placement: one wave per chunk copies its owned scratch records to their global index (64
 // records per step, out_off by a wave prefix sum: coalesced stores instead of one thread's serial
 // record loop).
@@ -850,6 +881,8 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint64_t* so = P.scratch_off + c * P.slots;
     const uint64_t* sl = P.scratch_len + c * P.slots;
     const uint64_t* sp = P.scratch_pay + c * P.slots;
+    const bool snappy = st->compression == RIO_COMP_SNAPPY;
+    bool mixed = false;
     uint64_t carry = pl.base_bytes;
     for (uint64_t k0 = 0; k0 < pl.owned; k0 += 64) {
         const uint64_t k = k0 + lane;
@@ -865,9 +898,15 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
             P.flags[i] = (l & kNilBit) ? RIO_FLAG_NIL : 0;
             P.rec_desc[i] = make_uint4((uint32_t)start, (uint32_t)(start >> 32), (uint32_t)slen, (uint32_t)len);
             if ((slen | len) > 0xFFFFFFFFull) atomicOr(&P.state->huge_streams, 1u);
+            // a snappy stream that is exactly one literal element of the record's whole length
+            // (what golang/snappy emits for incompressible input) decodes as a copy
+            if (snappy && !(l & kNilBit)) mixed |= !snappy_single_literal(P.file + start, slen, len);
         }
         carry += __shfl(excl + len, 63);
     }
+    // every writer stores the same 1: a plain store, not an atomic (17 k same-address atomics from
+    // the chunk waves of a 1 M-record file serialized at L2 and cost 0.35 ms)
+    if (snappy && __any(mixed) && lane == 0) P.state->any_mixed = 1u;
 }
 
 // Capacity check + sentinel out_off[n] + zero-tail range.
@@ -924,6 +963,33 @@ __global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
         const uint8_t* src = P.file + P.rec_off[i] + (P.rec_pay[i] & 0xFF);
         uint8_t* dst = P.out + o0;
         const uint64_t len = o1 - o0;
+        for (uint64_t k = 16 * lane; k < len; k += 256) {
+            const uint4 v = ldu16(src + k);
+            if (k + 16 <= len)
+                stu16(dst + k, v);
+            else
+                st_partial(dst + k, v, (uint32_t)(len - k));
+        }
+    }
+}
+
+// Snappy files whose every record is one literal (incompressible values: the reference benchmark's
+// random records) skip the lane-per-record decoder: 16-lane groups copy each literal's bytes like
+// k_decode_copy. k_snappy_pipe exits at once for such files (rio_snappy.hip).
+__global__ void __launch_bounds__(256) k_snappy_literal(FrameParams P) {
+    const ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || st->any_mixed) return;
+    const uint64_t n = st->n_records;
+    const uint32_t lane = threadIdx.x & 15;
+    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
+    for (uint64_t i = grp; i < n; i += ngrp) {
+        const uint64_t o0 = P.out_off[i], len = P.out_off[i + 1] - o0;
+        if (len == 0) continue;
+        const uint64_t pay = P.rec_pay[i];  // 64-bit stream position and length (any file size)
+        const uint8_t* s0 = P.file + P.rec_off[i] + (pay & 0xFF);
+        const uint8_t* src = s0 + snappy_literal_hdr(s0, pay >> 8, len);
+        uint8_t* dst = P.out + o0;
         for (uint64_t k = 16 * lane; k < len; k += 256) {
             const uint4 v = ldu16(src + k);
             if (k + 16 <= len)
@@ -1220,6 +1286,7 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     hipLaunchKernelGGL(k_post_scan, dim3(1), dim3(64), 0, s, P);
     if (ev) (void)hipEventRecord(ev[3], s);
     hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_snappy_literal, dim3(2048), dim3(256), 0, s, P);
     launch_snappy_decode(P, s);
     launch_gzip_decode(P, s);
     if (ev) (void)hipEventRecord(ev[4], s);

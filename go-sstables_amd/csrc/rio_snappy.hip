@@ -25,6 +25,8 @@
 //     wave touches each bank once, whatever positions the lanes are at.
 // k_snappy_global: records whose compressed stream exceeds 32-bit positions (never produced by a
 // real encoder) decode with byte loops straight to HBM.
+// Files whose every record is a single literal (k_place sets ScanState::any_mixed otherwise) are
+// copied by k_snappy_literal (rio_kernels.hip) and both kernels here exit at once.
 #include <hip/hip_runtime.h>
 
 #include "rio_device.h"
@@ -332,6 +334,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     ScanState* st = P.state;
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || snappy_wide(P, st))
         return;
+    if (!st->any_mixed) return;  // every record is one literal: k_snappy_literal copies them
     const uint64_t n = st->n_records;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     // lane number: waves are numbered across workgroups first, so that a file with few records
@@ -353,7 +356,8 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
 // stream over 4 GiB): every record decoded by one thread with byte loops straight to HBM.
 __global__ void __launch_bounds__(256) k_snappy_global(FrameParams P) {
     ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !snappy_wide(P, st))
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !snappy_wide(P, st) ||
+        !st->any_mixed)
         return;
     const uint64_t n = st->n_records;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
