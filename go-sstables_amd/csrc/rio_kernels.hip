@@ -33,25 +33,30 @@ __device__ __forceinline__ uint32_t crc32c_byte(uint32_t c, uint32_t b) {
     return c;
 }
 
+// Byte sources for the header / scan code: RawBytes reads the file directly; WinBytes (rio_pb.h)
+// serves a lane's bytes from a 16-byte window and reloads it only when a position leaves it.
 // io.ByteReader over file bytes [base, base+avail); `cap` = checksumByteReader cache (36 for v4
 // FileReader, checksum_byte_reader.go:25-27), ~0 when no cache applies.
-struct Src {
-    const uint8_t* f;
+template <class B>
+struct SrcT {
+    B& get;
     uint64_t base, avail, pos, cap;
 };
 
-__device__ __forceinline__ int src_byte(Src& s, uint32_t& b) {
+template <class B>
+__device__ __forceinline__ int src_byte(SrcT<B>& s, uint32_t& b) {
     if (s.pos >= s.avail) return RIO_EOF;
     if (s.pos >= s.cap) {
         s.pos++;
         return RIO_ERR_HEADER_TOO_LONG;
     }
-    b = s.f[s.base + s.pos++];
+    b = s.get(s.base + s.pos++);
     return RIO_OK;
 }
 
 // encoding/binary.ReadUvarint semantics
-__device__ int read_uvarint(Src& s, uint64_t& x) {
+template <class B>
+__device__ __forceinline__ int read_uvarint(SrcT<B>& s, uint64_t& x) {
     uint64_t v = 0;
     uint32_t sh = 0;
     for (int i = 0; i < 10; i++) {
@@ -78,9 +83,10 @@ struct Hdr {
 __device__ __forceinline__ int later_field(int e) { return e == RIO_EOF ? RIO_EOF_HEADER : e; }
 
 // readRecordHeaderV4 (common_reader.go:110-151) / readRecordHeaderV3 (:83-108)
-__device__ int parse_header(const uint8_t* f, uint64_t p, uint64_t avail, uint64_t cap, uint32_t ver,
-                            Hdr& h) {
-    Src s{f, p, avail, 0, cap};
+template <class B>
+__device__ __forceinline__ int parse_header_t(B& get, uint64_t p, uint64_t avail, uint64_t cap, uint32_t ver, Hdr& h,
+                                              const uint32_t* crc_tab = nullptr) {
+    SrcT<B> s{get, p, avail, 0, cap};
     uint64_t m = 0;
     h.nil = 0;
     h.hdr_len = 0;
@@ -97,7 +103,11 @@ __device__ int parse_header(const uint8_t* f, uint64_t p, uint64_t avail, uint64
     if (e) return later_field(e);
     if (ver == RIO_VERSION4) {
         uint32_t crc = 0xFFFFFFFFu;
-        for (uint64_t i = 0; i < s.pos; i++) crc = crc32c_byte(crc, f[p + i]);
+        // byte table in LDS when the kernel has one (T[0..255] of crc32c_tab_init), else bitwise
+        if (crc_tab)
+            for (uint64_t i = 0; i < s.pos; i++) crc = crc_tab[(crc ^ get(p + i)) & 0xFFu] ^ (crc >> 8);
+        else
+            for (uint64_t i = 0; i < s.pos; i++) crc = crc32c_byte(crc, get(p + i));
         h.act_crc = crc ^ 0xFFFFFFFFu;
         e = read_uvarint(s, h.exp_crc);
         if (e) return later_field(e);
@@ -106,6 +116,12 @@ __device__ int parse_header(const uint8_t* f, uint64_t p, uint64_t avail, uint64
     h.nil = (nb == 1);
     h.hdr_len = (uint32_t)s.pos;
     return RIO_OK;
+}
+
+__device__ __forceinline__ int parse_header(const uint8_t* f, uint64_t p, uint64_t avail, uint64_t cap, uint32_t ver,
+                                            Hdr& h) {
+    RawBytes raw{f};
+    return parse_header_t(raw, p, avail, cap, ver, h);
 }
 
 // ---- register-window header parse (fast path) --------------------------------------------
@@ -1046,8 +1062,11 @@ __global__ void k_finalize(FrameParams P) {
 // ------------------------------------------------------------------------------------------
 // Single record at an arbitrary offset: MMapReader.ReadNextAt (mmap_reader.go:130-203, 298-356)
 // ------------------------------------------------------------------------------------------
-__device__ int read_at_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_t comp, uint64_t off,
-                           uint8_t* out, uint64_t out_cap, ReadAtResult& r, bool write) {
+// ReadNextAt up to the payload: bounds, header, nil, payload extent. RIO_OK with r.nil, or with
+// r.payload_off / r.len (= the payload length in the file) set.
+template <class B>
+__device__ __forceinline__ int read_at_locate(B& get, uint64_t len, uint32_t ver, uint32_t comp, uint64_t off,
+                                              ReadAtResult& r, Hdr& h, const uint32_t* crc_tab = nullptr) {
     r.nil = 0;
     r.len = 0;
     r.det0 = r.det1 = 0;
@@ -1055,8 +1074,7 @@ __device__ int read_at_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_
     const uint64_t wmax = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : RIO_RECORD_HEADER_V3_MAX;
     const uint64_t w = len - off < wmax ? len - off : wmax;
     if (w == 0) return RIO_EOF;  // bare io.EOF
-    Hdr h;
-    int e = parse_header(f, off, w, ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : ~0ull, ver, h);
+    int e = parse_header_t(get, off, w, ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : ~0ull, ver, h, crc_tab);
     if (e == RIO_EOF) e = RIO_EOF_HEADER;
     if (e == RIO_ERR_HEADER_CRC) {
         r.det0 = h.exp_crc;
@@ -1070,10 +1088,20 @@ __device__ int read_at_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_
     }
     const uint64_t plen = comp != RIO_COMP_NONE ? h.c : h.u;
     if (plen > len - off - h.hdr_len) return RIO_EOF_PAYLOAD;
-    const uint8_t* pay = f + off + h.hdr_len;
     r.payload_off = off + h.hdr_len;
+    r.len = plen;
+    return RIO_OK;
+}
+
+__device__ int read_at_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_t comp, uint64_t off,
+                           uint8_t* out, uint64_t out_cap, ReadAtResult& r, bool write) {
+    Hdr h;
+    RawBytes raw{f};
+    const int e0 = read_at_locate(raw, len, ver, comp, off, r, h);
+    if (e0 || r.nil) return e0;
+    const uint64_t plen = r.len;
+    const uint8_t* pay = f + off + h.hdr_len;
     if (comp == RIO_COMP_NONE) {
-        r.len = plen;
         if (!write) return RIO_OK;
         if (plen > out_cap) return RIO_ERR_CAPACITY;
         for (uint64_t k = 0; k < plen; k++) out[k] = pay[k];
@@ -1111,9 +1139,8 @@ __global__ void k_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t*
 // MMapReader.SeekNext (mmap_reader.go:58-128): windowed scan for 91 8d 4c with its skip rule,
 // trial ReadNextAt per hit; CRC / magic / io.EOF-class failures continue the scan. Returns the
 // status; on RIO_OK r describes the record at rec_off (payload_off / len when !write).
-__device__ int seek_next_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_t comp, uint64_t off,
-                             uint64_t seek_len, uint8_t* out, uint64_t out_cap, bool write, ReadAtResult& r,
-                             uint64_t& rec_off) {
+template <class B, class Trial>
+__device__ __forceinline__ int seek_next_t(B& get, uint64_t len, uint64_t off, uint64_t seek_len, Trial&& trial, uint64_t& rec_off) {
     const uint8_t M[3] = {0x91, 0x8D, 0x4C};
     rec_off = 0;
     uint64_t next = off;
@@ -1126,7 +1153,7 @@ __device__ int seek_next_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint3
         while (i < num) {
             uint64_t ix = i;
             for (int j = 0; j < 3; j++) {
-                if (f[next + ix] != M[j]) break;
+                if (get(next + ix) != M[j]) break;
                 ix++;
                 if (ix >= num) {
                     boundary = true;
@@ -1138,19 +1165,27 @@ __device__ int seek_next_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint3
                 i = ix + 1;
                 continue;
             }
-            const uint64_t trial = next + i;
-            const int te = read_at_dev(f, len, ver, comp, trial, out, out_cap, r, write);
+            const uint64_t at = next + i;
+            const int te = trial(at);
             if (te != RIO_OK && (te == RIO_ERR_HEADER_CRC || te == RIO_ERR_MAGIC || te == RIO_EOF ||
                                  te == RIO_EOF_HEADER || te == RIO_EOF_PAYLOAD)) {
                 i = ix;
                 continue;
             }
-            rec_off = trial;
+            rec_off = at;
             return te;
         }
         if (i == 0) return RIO_EOF;
         next += i;
     }
+}
+
+__device__ int seek_next_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_t comp, uint64_t off,
+                             uint64_t seek_len, uint8_t* out, uint64_t out_cap, bool write, ReadAtResult& r,
+                             uint64_t& rec_off) {
+    RawBytes raw{f};
+    return seek_next_t(raw, len, off, seek_len,
+                       [&](uint64_t at) { return read_at_dev(f, len, ver, comp, at, out, out_cap, r, write); }, rec_off);
 }
 
 __device__ __forceinline__ int file_header_dev(const uint8_t* f, uint64_t len, uint32_t& ver, uint32_t& comp) {
@@ -1184,25 +1219,34 @@ __global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64
 // the exact probe sequence of a freshly loaded index (SeekNext is not monotone in h because of the
 // scan's skip rule, so a table of record starts alone would not reproduce it).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int bytes_compare_dev(const uint8_t* a, uint64_t an, const uint8_t* b, uint64_t bn) {
+// bytes.Compare(file[a, a + an), key[0, bn)): the file side through the lane's window
+__device__ __forceinline__ int bytes_compare_dev(WinBytes& wb, uint64_t a, uint64_t an, const uint8_t* b, uint64_t bn) {
     const uint64_t m = an < bn ? an : bn;
     for (uint64_t k = 0; k < m; k++) {
-        const uint32_t x = a[k], y = b[k];
+        const uint32_t x = wb(a + k), y = b[k];
         if (x != y) return x < y ? -1 : 1;
     }
     return an < bn ? -1 : (an > bn ? 1 : 0);
 }
 
-// findAt: 0 and the entry's fields (key_off absolute in f), or a status
-__device__ int index_find_at(const uint8_t* f, uint64_t len, uint32_t ver, uint64_t h, uint64_t seek_len,
-                             uint64_t& ko, uint64_t& kl, uint64_t& vo, uint64_t& cs) {
+// findAt: 0 and the entry's fields (key_off absolute in f), or a status. All bytes come through the
+// lane's 16-byte window: one load per 16 bytes scanned or parsed instead of one per byte (the
+// kernel is bound by L2 requests, not by latency).
+__device__ __forceinline__ int index_find_at(WinBytes& wb, uint64_t len, uint32_t ver, uint64_t h, uint64_t seek_len,
+                                             const uint32_t* T, uint64_t& ko, uint64_t& kl, uint64_t& vo, uint64_t& cs) {
     ReadAtResult r{};
+    Hdr hd;
     uint64_t ro;
-    const int e = seek_next_dev(f, len, ver, RIO_COMP_NONE, h, seek_len, nullptr, 0, false, r, ro);
+    const int e = seek_next_t(
+        wb, len, h, seek_len,
+        [&](uint64_t at) __attribute__((always_inline)) {
+            return read_at_locate(wb, len, ver, RIO_COMP_NONE, at, r, hd, T);
+        },
+        ro);
     if (e) return e;
     const uint64_t pl = r.nil ? 0 : r.len;
     const uint64_t po = r.nil ? 0 : r.payload_off;
-    if (!pb_index_entry(f + po, pl, ko, kl, vo, cs)) return RIO_ERR_PROTO;
+    if (!pb_index_entry_t(wb, po, pl, ko, kl, vo, cs)) return RIO_ERR_PROTO;
     ko += po;
     return RIO_OK;
 }
@@ -1214,6 +1258,8 @@ __device__ __forceinline__ bool eof_class(int e) {
 __global__ void __launch_bounds__(256) k_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len,
                                                       const uint8_t* keys, const uint64_t* key_off, uint64_t nq,
                                                       rio_index_hit* hits) {
+    __shared__ uint32_t T[1024];  // CRC-32C tables (T[0..255] = the byte table)
+    crc32c_tab_init(T);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t ver, comp;
     const int he = file_header_dev(f, len, ver, comp);
@@ -1224,19 +1270,20 @@ __global__ void __launch_bounds__(256) k_index_search(const uint8_t* f, uint64_t
         int e = he;
         if (e == RIO_OK && comp != RIO_COMP_NONE) e = RIO_ERR_UNSUPPORTED;
         uint64_t ko = 0, kl = 0, vo = 0, cs = 0;
+        WinBytes wb{f};
         if (e == RIO_OK) {
             uint64_t i = 0, j = len;
             while (i < j) {
                 const uint64_t h = (i + j) >> 1;
-                e = index_find_at(f, len, ver, h, seek_len, ko, kl, vo, cs);
+                e = index_find_at(wb, len, ver, h, seek_len, T, ko, kl, vo, cs);
                 if (e) break;
-                if (bytes_compare_dev(f + ko, kl, key, klen) < 0) i = h + 1; else j = h;
+                if (bytes_compare_dev(wb, ko, kl, key, klen) < 0) i = h + 1; else j = h;
             }
             if (e == RIO_OK) {
-                e = index_find_at(f, len, ver, i, seek_len, ko, kl, vo, cs);
+                e = index_find_at(wb, len, ver, i, seek_len, T, ko, kl, vo, cs);
                 if (e == RIO_OK) {
                     out.offset = i;
-                    out.found = i < len && bytes_compare_dev(f + ko, kl, key, klen) == 0;
+                    out.found = i < len && bytes_compare_dev(wb, ko, kl, key, klen) == 0;
                     if (out.found) {
                         out.value_offset = vo;
                         out.checksum = cs;
