@@ -33,4 +33,9 @@ grep '^{' "$OUT/bench_c5.log" > "$OUT/bench_c5.json" || true
 step rocprof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- \
     python bench.py --config c5 --no-cpu-baseline
 find "$OUT/prof_c5" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_c5.csv" \;
+# the other bench lines (their own metrics): WAL replay, batched DiskKeyIndex.Get, device encode, random records
+for c in wal idx enc c2r; do
+    step bench_$c 600 python bench.py --config $c
+    grep '^{' "$OUT/bench_$c.log" > "$OUT/bench_$c.json" || true
+done
 echo done
