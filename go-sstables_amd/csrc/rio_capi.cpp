@@ -37,7 +37,11 @@ hipError_t launch_sst_validate(const uint8_t* data, const uint64_t* data_off, co
                                uint64_t n_data, const uint64_t* value_off, const uint64_t* checksum,
                                uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s);
 hipError_t launch_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len, const uint8_t* keys,
-                               const uint64_t* key_off, uint64_t nq, rio_index_hit* hits, hipStream_t s);
+                               const uint64_t* key_off, uint64_t nq, const uint32_t* perm, rio_index_hit* hits,
+                               hipStream_t s);
+size_t key_sort_tmp_bytes(uint64_t n);
+hipError_t launch_key_sort(const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint64_t* pfx_in, uint64_t* pfx_out,
+                           uint32_t* idx_in, uint32_t* perm, void* tmp, size_t tmp_bytes, hipStream_t s);
 hipError_t launch_encode(const EncParams& P, void* cub_tmp, size_t cub_bytes, hipStream_t s);
 uint64_t enc_scratch_bytes(uint64_t n, uint64_t bytes, uint32_t compression);
 uint64_t enc_table_bytes();
@@ -167,6 +171,8 @@ struct rio_ctx {
     // record sizes, scan temp; rio_encode_file: records, offsets, flags, file image, record offsets
     DevBuf enc_scr, enc_scr_off, enc_clen, enc_tab, enc_hdr, enc_size, enc_tmp, enc_cub;
     DevBuf enc_rec, enc_rec_off, enc_flags, enc_out, enc_out_off, enc_len;
+    // index search: key prefixes, indices, permutation, radix sort temp
+    DevBuf q_pfx, q_pfx_out, q_idx, q_perm, q_tmp;
     uint8_t* pinned[2] = {nullptr, nullptr};
     hipEvent_t pin_ev[2] = {};
     // last host-API framing (rio_frame -> rio_decode)
@@ -245,7 +251,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
                       &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
                       &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res, &c->enc_scr, &c->enc_scr_off, &c->enc_clen, &c->enc_tab,
                       &c->enc_hdr, &c->enc_size, &c->enc_tmp, &c->enc_cub, &c->enc_rec, &c->enc_rec_off, &c->enc_flags, &c->enc_out,
-                      &c->enc_out_off, &c->enc_len})
+                      &c->enc_out_off, &c->enc_len, &c->q_pfx, &c->q_pfx_out, &c->q_idx, &c->q_perm, &c->q_tmp})
         b->release();
     for (int i = 0; i < 2; i++) {
         if (c->pinned[i]) hipHostFree(c->pinned[i]);
@@ -989,7 +995,19 @@ extern "C" int rio_device_index_search(rio_ctx* ctx, const uint8_t* d_file, uint
     if (!ctx || !d_file || (n && (!d_keys || !d_key_off || !d_hits))) return RIO_ERR_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    HIP_TRY(launch_index_search(d_file, len, seek_len ? seek_len : 4096, d_keys, d_key_off, n, d_hits, s));
+    const uint32_t* perm = nullptr;
+    if (n >= 4096 && n < 0x7FFFFFFFull) {  // big batches: visit the queries in key order (rio_sort.hip)
+        const size_t tb = std::max<size_t>(key_sort_tmp_bytes(n), 256);
+        HIP_TRY(ctx->q_pfx.ensure(n * 8));
+        HIP_TRY(ctx->q_pfx_out.ensure(n * 8));
+        HIP_TRY(ctx->q_idx.ensure(n * 4));
+        HIP_TRY(ctx->q_perm.ensure(n * 4));
+        HIP_TRY(ctx->q_tmp.ensure(tb));
+        HIP_TRY(launch_key_sort(d_keys, d_key_off, n, ctx->q_pfx.as<uint64_t>(), ctx->q_pfx_out.as<uint64_t>(),
+                                ctx->q_idx.as<uint32_t>(), ctx->q_perm.as<uint32_t>(), ctx->q_tmp.p, ctx->q_tmp.cap, s));
+        perm = ctx->q_perm.as<uint32_t>();
+    }
+    HIP_TRY(launch_index_search(d_file, len, seek_len ? seek_len : 4096, d_keys, d_key_off, n, perm, d_hits, s));
     return RIO_OK;
 }
 
@@ -1033,8 +1051,9 @@ extern "C" int rio_index_search(rio_index* x, const uint8_t* keys, const uint64_
     int rc = kb ? h2d_staged(ctx, x->keys.p, keys, kb) : RIO_OK;
     if (!rc) rc = h2d_staged(ctx, x->key_off.p, reinterpret_cast<const uint8_t*>(key_off), (n + 1) * 8);
     if (rc) return rc;
-    HIP_TRY(launch_index_search(x->file.as<uint8_t>(), x->len, 4096, x->keys.as<uint8_t>(), x->key_off.as<uint64_t>(),
-                                n, x->hits.as<rio_index_hit>(), ctx->stream));
+    rc = rio_device_index_search(ctx, x->file.as<uint8_t>(), x->len, 4096, x->keys.as<uint8_t>(),
+                                 x->key_off.as<uint64_t>(), n, x->hits.as<rio_index_hit>(), nullptr);
+    if (rc) return rc;
     return d2h_staged(ctx, reinterpret_cast<uint8_t*>(hits), x->hits.p, n * sizeof(rio_index_hit));
 }
 

@@ -1257,13 +1257,14 @@ __device__ __forceinline__ bool eof_class(int e) {
 
 __global__ void __launch_bounds__(256) k_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len,
                                                       const uint8_t* keys, const uint64_t* key_off, uint64_t nq,
-                                                      rio_index_hit* hits) {
+                                                      const uint32_t* perm, rio_index_hit* hits) {
     __shared__ uint32_t T[1024];  // CRC-32C tables (T[0..255] = the byte table)
     crc32c_tab_init(T);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t ver, comp;
     const int he = file_header_dev(f, len, ver, comp);
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += stride) {
+    for (uint64_t qq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; qq < nq; qq += stride) {
+        const uint64_t q = perm ? perm[qq] : qq;  // queries in key order (rio_sort.hip), results in place
         rio_index_hit out{};
         const uint8_t* key = keys + key_off[q];
         const uint64_t klen = key_off[q + 1] - key_off[q];
@@ -1354,11 +1355,12 @@ hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64
 }
 
 hipError_t launch_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len, const uint8_t* keys,
-                               const uint64_t* key_off, uint64_t nq, rio_index_hit* hits, hipStream_t s) {
+                               const uint64_t* key_off, uint64_t nq, const uint32_t* perm, rio_index_hit* hits,
+                               hipStream_t s) {
     if (nq == 0) return hipSuccess;
     const uint64_t blocks = (nq + 255) / 256;
     hipLaunchKernelGGL(k_index_search, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, f, len,
-                       seek_len, keys, key_off, nq, hits);
+                       seek_len, keys, key_off, nq, perm, hits);
     return hipGetLastError();
 }
 

@@ -175,3 +175,17 @@ def test_reference_index_api(tmp_path):
         assert [e is None for _, e in batch] == [False] + [True] * 7 + [False]
     finally:
         idx.Close()
+
+
+def test_large_batch_sorted_path_matches_oracle():
+    # >= 4096 keys: the device visits the queries in key-prefix order (rio_sort.hip); every hit must
+    # still land at its own query index, including keys with equal 8-byte prefixes
+    rng = random.Random(11)
+    keys = sorted({bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 24))) for _ in range(3000)})
+    idx = index_image(entries_for(keys, nil_every=17))
+    qs = []
+    for _ in range(6000):
+        k = rng.choice(keys)
+        r = rng.random()
+        qs.append(k if r < 0.5 else (k[:8] + bytes([rng.getrandbits(8)]) if r < 0.8 else k[:rng.randint(0, len(k))]))
+    check(idx, qs)
