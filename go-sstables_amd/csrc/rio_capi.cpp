@@ -26,6 +26,7 @@
 
 #include "rio.h"
 #include "rio_device.h"
+#include "rio_host.h"
 
 namespace rio {
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
@@ -334,70 +335,6 @@ static int ensure_pinned(rio_ctx* c) {
     return RIO_OK;
 }
 
-// Host copies into / out of the pinned staging pieces, split over a small persistent pool: one
-// core's memcpy (~10 GB/s) otherwise bounds the staged PCIe path well below the link. One job at a
-// time (callers on other contexts wait their turn); workers live for the process.
-class CopyPool {
-  public:
-    static CopyPool& get() {
-        static CopyPool* p = new CopyPool();
-        return *p;
-    }
-    void copy(void* dst, const void* src, size_t n) {
-        const size_t W = workers_.size();
-        if (W == 0 || n < (4u << 20)) {
-            memcpy(dst, src, n);
-            return;
-        }
-        std::lock_guard<std::mutex> one(submit_);
-        const size_t parts = W + 1, step = ((n + parts - 1) / parts + 63) & ~size_t(63);
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            d_ = static_cast<uint8_t*>(dst);
-            s_ = static_cast<const uint8_t*>(src);
-            n_ = n;
-            step_ = step;
-            remaining_ = W;
-            gen_++;
-        }
-        cv_.notify_all();
-        memcpy(dst, src, std::min(step, n));  // part 0 on the caller
-        std::unique_lock<std::mutex> g(mu_);
-        done_.wait(g, [&] { return remaining_ == 0; });
-    }
-
-  private:
-    CopyPool() {
-        const char* v = getenv("RIO_COPY_THREADS");
-        const long t = v ? strtol(v, nullptr, 0) : 4;  // measured: 0 -> 8.0, 4 -> 14.7, 6 -> 14.3, 12 -> 14.1 GiB/s e2e on C2
-        for (long i = 0; i < std::min(t, 32L); i++) workers_.emplace_back([this, i] { run((size_t)i + 1); });
-        for (auto& w : workers_) w.detach();
-    }
-    void run(size_t part) {
-        uint64_t seen = 0;
-        for (;;) {
-            std::unique_lock<std::mutex> g(mu_);
-            cv_.wait(g, [&] { return gen_ != seen; });
-            seen = gen_;
-            uint8_t* d = d_;
-            const uint8_t* s = s_;
-            const size_t n = n_, step = step_;
-            g.unlock();
-            const size_t o = part * step;
-            if (o < n) memcpy(d + o, s + o, std::min(step, n - o));
-            g.lock();
-            if (--remaining_ == 0) done_.notify_one();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex submit_, mu_;
-    std::condition_variable cv_, done_;
-    uint8_t* d_ = nullptr;
-    const uint8_t* s_ = nullptr;
-    size_t n_ = 0, step_ = 0, remaining_ = 0;
-    uint64_t gen_ = 0;
-};
-
 // true when [p, p + n) is page-locked host memory HIP knows (hipHostMalloc / hipHostRegister): the
 // copy then goes by DMA directly, without the staging pieces. The probe's error on pageable memory
 // is cleared so a later hipGetLastError (kernel launch check) does not see it.
@@ -423,7 +360,7 @@ static int h2d_staged(rio_ctx* c, void* dst, const uint8_t* src, uint64_t n) {
     while (o < n) {
         const uint64_t m = std::min<uint64_t>(kStage, n - o);
         HIP_TRY(hipEventSynchronize(c->pin_ev[k]));
-        CopyPool::get().copy(c->pinned[k], src + o, m);
+        HostPool::get().copy(c->pinned[k], src + o, m);
         HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, c->pinned[k], m, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipEventRecord(c->pin_ev[k], c->stream));
         o += m;
@@ -451,7 +388,7 @@ static int d2h_staged(rio_ctx* c, uint8_t* dst, const void* src, uint64_t n) {
         HIP_TRY(hipEventRecord(c->pin_ev[k], c->stream));
         if (have_prev) {
             HIP_TRY(hipEventSynchronize(c->pin_ev[k ^ 1]));
-            CopyPool::get().copy(dst + prev_o, c->pinned[k ^ 1], prev_m);
+            HostPool::get().copy(dst + prev_o, c->pinned[k ^ 1], prev_m);
         }
         have_prev = true;
         prev_o = o;
@@ -461,7 +398,7 @@ static int d2h_staged(rio_ctx* c, uint8_t* dst, const void* src, uint64_t n) {
     }
     if (have_prev) {
         HIP_TRY(hipEventSynchronize(c->pin_ev[k ^ 1]));
-        CopyPool::get().copy(dst + prev_o, c->pinned[k ^ 1], prev_m);
+        HostPool::get().copy(dst + prev_o, c->pinned[k ^ 1], prev_m);
     }
     return RIO_OK;
 }

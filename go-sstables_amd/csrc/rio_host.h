@@ -1,0 +1,85 @@
+// rio_host.h — host-side helpers shared by the runtime files (rio_capi.cpp, rio_replay.cpp).
+#pragma once
+#include <algorithm>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace rio {
+
+// A small persistent pool for host-side byte moving: copies into / out of the pinned staging pieces,
+// and the WAL replay's file reads. One core's memcpy (~10 GB/s) or pread otherwise bounds the PCIe
+// paths well below the link. One job at a time (callers on other contexts or workers wait their
+// turn); workers live for the process. RIO_COPY_THREADS sets the worker count (default 4; measured
+// on C2 end-to-end: 0 -> 8.0, 4 -> 14.7, 6 -> 14.3, 12 -> 14.1 GiB/s).
+class HostPool {
+  public:
+    static HostPool& get() {
+        static HostPool* p = new HostPool();
+        return *p;
+    }
+    size_t parts() const { return workers_.size() + 1; }
+    // fn(part, parts) for part in [0, parts): part 0 on the caller, the rest on the workers
+    void run(const std::function<void(size_t, size_t)>& fn) {
+        const size_t W = workers_.size();
+        if (W == 0) {
+            fn(0, 1);
+            return;
+        }
+        std::lock_guard<std::mutex> one(submit_);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            remaining_ = W;
+            gen_++;
+        }
+        cv_.notify_all();
+        fn(0, W + 1);
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [&] { return remaining_ == 0; });
+    }
+    void copy(void* dst, const void* src, size_t n) {
+        if (workers_.empty() || n < (4u << 20)) {
+            memcpy(dst, src, n);
+            return;
+        }
+        run([&](size_t part, size_t parts) {
+            const size_t step = ((n + parts - 1) / parts + 63) & ~size_t(63), o = part * step;
+            if (o < n) memcpy(static_cast<uint8_t*>(dst) + o, static_cast<const uint8_t*>(src) + o, std::min(step, n - o));
+        });
+    }
+
+  private:
+    HostPool() {
+        const char* v = getenv("RIO_COPY_THREADS");
+        const long t = v ? strtol(v, nullptr, 0) : 4;
+        for (long i = 0; i < std::min(t, 32L); i++) workers_.emplace_back([this, i] { loop((size_t)i + 1); });
+        for (auto& w : workers_) w.detach();
+    }
+    void loop(size_t part) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> g(mu_);
+            cv_.wait(g, [&] { return gen_ != seen; });
+            seen = gen_;
+            const std::function<void(size_t, size_t)>* fn = fn_;
+            g.unlock();
+            (*fn)(part, workers_.size() + 1);
+            g.lock();
+            if (--remaining_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex submit_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t, size_t)>* fn_ = nullptr;
+    size_t remaining_ = 0;
+    uint64_t gen_ = 0;
+};
+
+}  // namespace rio

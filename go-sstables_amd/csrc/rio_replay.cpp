@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cerrno>
 #include <cstdio>
@@ -29,6 +30,9 @@
 #include <vector>
 
 #include "rio.h"
+#include "rio_host.h"
+
+using rio::HostPool;
 
 namespace {
 
@@ -127,12 +131,27 @@ int read_file(const std::string& path, PinnedBuf& in, uint64_t& len) {
     if (!rc && len) {
         if (!in.alloc(len)) rc = RIO_ERR_HIP;
         posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
-        uint64_t o = 0;
-        while (!rc && o < len) {
-            const ssize_t k = pread(fd, in.bytes() + o, std::min<uint64_t>(len - o, 64ull << 20), (off_t)o);
-            if (k < 0 && errno == EINTR) continue;
-            if (k <= 0) rc = RIO_ERR_IO;  // error, or the file shrank under us
-            else o += (uint64_t)k;
+        // the file's byte ranges read in parallel on the host pool (one thread's pread, a kernel
+        // copy out of the page cache, ran at 11-20 GB/s)
+        std::atomic<int> err{RIO_OK};
+        auto read_range = [&](uint64_t o, uint64_t end) {
+            while (o < end && err.load(std::memory_order_relaxed) == RIO_OK) {
+                const ssize_t k = pread(fd, in.bytes() + o, std::min<uint64_t>(end - o, 64ull << 20), (off_t)o);
+                if (k < 0 && errno == EINTR) continue;
+                if (k <= 0) err = RIO_ERR_IO;  // error, or the file shrank under us
+                else o += (uint64_t)k;
+            }
+        };
+        if (!rc) {
+            if (len < (8u << 20)) {
+                read_range(0, len);
+            } else {
+                HostPool::get().run([&](size_t part, size_t parts) {
+                    const uint64_t step = ((len + parts - 1) / parts + 4095) & ~4095ull, o = part * step;
+                    if (o < len) read_range(o, std::min<uint64_t>(len, o + step));
+                });
+            }
+            rc = err.load();
         }
     }
     ::close(fd);
