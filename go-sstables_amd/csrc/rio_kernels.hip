@@ -897,7 +897,8 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint64_t* so = P.scratch_off + c * P.slots;
     const uint64_t* sl = P.scratch_len + c * P.slots;
     const uint64_t* sp = P.scratch_pay + c * P.slots;
-    const bool snappy = st->compression == RIO_COMP_SNAPPY;
+    // once any wave has found a mixed record the file takes k_snappy_pipe: later waves skip the probe
+    const bool snappy = st->compression == RIO_COMP_SNAPPY && !*(volatile const uint32_t*)&st->any_mixed;
     bool mixed = false;
     uint64_t carry = pl.base_bytes;
     for (uint64_t k0 = 0; k0 < pl.owned; k0 += 64) {
