@@ -66,6 +66,10 @@ __device__ __forceinline__ uint4 shift_small(uint4 w, uint32_t sh) {
                       __builtin_amdgcn_alignbyte(e3, e2, b), __builtin_amdgcn_alignbyte(0u, e3, b));
 }
 
+// materialize x in a VGPR here: the selects that use it can no longer be turned into branches that
+// compute x on one side only (an empty asm with a register constraint; no instruction is emitted)
+__device__ __forceinline__ void pin_v(uint32_t& x) { asm volatile("" : "+v"(x)); }
+
 __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
     return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
@@ -241,10 +245,22 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             // literal: x < 60 -> length x + 1; x in [60, 63] -> x - 59 little-endian length bytes follow
             const bool lng = x >= 60;
             const uint32_t lmask = 0xFFFFFFFFu >> (((63u - x) << 3) & 31u);
-            const uint32_t lit_len = (lng ? (W1 & lmask) : x) + 1u;
-            const uint32_t len = is0 ? lit_len : (is1 ? (x & 7u) + 4u : x + 1u);
-            const uint32_t hl = is0 ? (lng ? x - 58u : 1u) : (is1 ? 2u : (is2 ? 3u : 5u));
-            const uint32_t off = is1 ? (((tag & 0xE0u) << 3) | (W1 & 0xFFu)) : (is2 ? (W1 & 0xFFFFu) : W1);
+            // every alternative computed unconditionally, then selected: the compiler otherwise
+            // turned these nested ternaries into exec-mask branches (3 per step)
+            uint32_t lit_long = (W1 & lmask) + 1u, lit_short = x + 1u;
+            uint32_t c1_len = (x & 7u) + 4u, c1_off = ((tag & 0xE0u) << 3) | (W1 & 0xFFu);
+            uint32_t c2_off = W1 & 0xFFFFu;
+            pin_v(lit_long);
+            pin_v(lit_short);
+            pin_v(c1_len);
+            pin_v(c1_off);
+            pin_v(c2_off);
+            const uint32_t lit_len = lng ? lit_long : lit_short;
+            const uint32_t len = is0 ? lit_len : (is1 ? c1_len : lit_short);
+            const uint32_t lit_hl = lng ? x - 58u : 1u;
+            const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
+            const uint32_t hl = is0 ? lit_hl : cp_hl;
+            const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
             // golang/snappy bounds, per record: header bytes present; literal source room or copy
             // offset in [1, bytes produced] (length / offset 0 wrap to the maximum key); output room
             const uint32_t sleft = s_end - s;
