@@ -8,8 +8,8 @@
 //
 // k_snappy_encode_lds    one lane per record of at most 1 KiB: the hash table (<= 1024 uint16
 //                        entries) sits in LDS laid out [hash][64 virtual lanes], which spreads the
-//                        lanes over the 64 banks whatever hashes they hold; 64 KiB per group of 32
-//                        records, run as 8 waves of 4 active lanes (more instruction streams).
+//                        lanes over the 64 banks whatever hashes they hold; 32 KiB per group of 16
+//                        records, run as 4 waves of 4 active lanes (more instruction streams).
 // k_snappy_encode_global one lane per larger record: table in a per-lane slot of global scratch
 //                        (16384 entries, reset per 64 KiB block).
 // k_enc_sizes             per record: header bytes (into a 64-B slot) and the record's file size.
@@ -347,12 +347,15 @@ hipError_t launch_encode(const EncParams& P0, void* cub_tmp, size_t cub_bytes, h
         if (n) {
             if (P.lds_small) {
                 auto grid = [&](uint64_t recs) { return dim3((unsigned)std::min<uint64_t>((n + recs - 1) / recs, 16384)); };
-                // 32 records per group (64 KiB of tables, two groups per CU) as 8 waves of 4 lanes:
-                // measured 35 GiB/s on C2-shaped input against 21 for one 64-lane wave per 64 records
-                if (enc_lanes() == 64)
-                    hipLaunchKernelGGL((k_snappy_encode_lds<64, 4>), grid(64), dim3(1024), 0, s, P);
-                else
-                    hipLaunchKernelGGL((k_snappy_encode_lds<32, 4>), grid(32), dim3(512), 0, s, P);
+                // 16 records per group (32 KiB of tables, five groups = 80 records per CU) as 4 waves
+                // of 4 lanes. Measured on C2-shaped input: one 64-lane wave per 64 records 20.7 GiB/s,
+                // 32 records as 8 waves x 4 lanes 35.5, 16 records as 4 x 4 36.4, 16 as 8 x 2 34.1
+                switch (enc_lanes()) {
+                case 64: hipLaunchKernelGGL((k_snappy_encode_lds<64, 4>), grid(64), dim3(1024), 0, s, P); break;
+                case 32: hipLaunchKernelGGL((k_snappy_encode_lds<32, 4>), grid(32), dim3(512), 0, s, P); break;
+                case 8: hipLaunchKernelGGL((k_snappy_encode_lds<16, 2>), grid(16), dim3(512), 0, s, P); break;
+                default: hipLaunchKernelGGL((k_snappy_encode_lds<16, 4>), grid(16), dim3(256), 0, s, P); break;
+                }
             }
             hipLaunchKernelGGL(k_snappy_encode_global, dim3(enc_groups()), dim3(64), 0, s, P);
         }
