@@ -43,6 +43,9 @@ constexpr uint32_t kGzLargeWin = 32768;   // DEFLATE window (maximum distance)
 constexpr uint32_t kFastBits = 9;         // decode-table bits
 constexpr uint32_t kFastSize = 1u << kFastBits;
 constexpr uint64_t kPayFail = 1ull << 63;  // rec_pay marker: inflate failed, no CRC check
+// RFC 1951 3.2.7 code-length code order; in constant memory so the uniform index is a scalar load
+// (a local array indexed at run time lived in scratch)
+__constant__ uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // per-wave decode tables
 struct GzTables {
@@ -332,11 +335,10 @@ __device__ int gz_record(GzLds<kWin>& S, const uint8_t* src, uint32_t slen, uint
             // code-length code lengths, in the RFC's order, into lens[0..19)
             if (lane < 19) T.lens[lane] = 0;
             __builtin_amdgcn_wave_barrier();
-            const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
             for (uint32_t k = 0; k < nclen; k++) {
                 B.refill(lane);
                 const uint32_t v = B.bits(3);
-                if (lane == 0) T.lens[order[k]] = (uint8_t)v;
+                if (lane == 0) T.lens[kClenOrder[k]] = (uint8_t)v;
             }
             if (B.overrun()) return kGzCorrupt;
             __builtin_amdgcn_wave_barrier();
