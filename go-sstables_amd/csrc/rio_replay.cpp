@@ -39,7 +39,8 @@ namespace {
 // Process-wide cache of page-locked host buffers. A replay streams gigabytes through host memory;
 // fresh pageable buffers cost a zero-fill plus a page fault per 4 KiB (measured: more than the H2D,
 // decode and D2H of the same file together), and pageable copies go through the staging pieces.
-// Pinned buffers are reused across files and replays and DMA'd directly. Best fit within 2x,
+// Pinned buffers are reused across files and replays and DMA'd directly. Best fit within 1.25x
+// (looser, a file's input block took a decoded-output block and forced a 15 ms hipHostMalloc),
 // at most kMaxCached bytes kept; intentionally never destroyed (process lifetime, no
 // static-destruction order against the HIP runtime).
 class PinnedPool {
@@ -53,7 +54,7 @@ class PinnedPool {
         {
             std::lock_guard<std::mutex> g(mu_);
             auto it = free_.lower_bound(n);
-            if (it != free_.end() && it->first <= 2 * n) {
+            if (it != free_.end() && it->first <= n + n / 4) {
                 void* p = it->second;
                 cap = it->first;
                 cached_ -= cap;
@@ -86,6 +87,48 @@ class PinnedPool {
     std::mutex mu_;
     std::multimap<size_t, void*> free_;
     size_t cached_ = 0;
+};
+
+// Process-wide cache of idle decode contexts, per device. A rio_ctx's stream and device arenas
+// grow to the largest file it has decoded; a replay that built fresh contexts paid that growth
+// (hipMalloc of every arena, first-touch) on each of its first files again (measured: 12-16 ms
+// decode+D2H of a 128 MiB file against 4.7 ms steady state; WAL bench 11.1 -> 16.7 GiB/s). rio_replay_free hands its contexts back here;
+// at most kMaxIdle are kept per device, the rest are destroyed. Never destroyed itself (same
+// reason as PinnedPool).
+class CtxPool {
+  public:
+    static CtxPool& get() {
+        static CtxPool* p = new CtxPool();
+        return *p;
+    }
+    int take(int device, rio_ctx** out) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto& v = idle_[device];
+            if (!v.empty()) {
+                *out = v.back();
+                v.pop_back();
+                return RIO_OK;
+            }
+        }
+        return rio_ctx_create(device, out);
+    }
+    void give(int device, rio_ctx* c) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto& v = idle_[device];
+            if (v.size() < kMaxIdle) {
+                v.push_back(c);
+                return;
+            }
+        }
+        rio_ctx_destroy(c);
+    }
+
+  private:
+    static constexpr size_t kMaxIdle = 4;
+    std::mutex mu_;
+    std::map<int, std::vector<rio_ctx*>> idle_;
 };
 
 struct PinnedBuf {
@@ -193,7 +236,8 @@ int decode_file(rio_ctx* ctx, const std::string& path, Decoded& d) {
 struct rio_replay {
     std::vector<std::string> paths;
     uint32_t depth = 2;
-    std::vector<rio_ctx*> ctxs;  // one per worker: own stream, arenas and pinned staging
+    int device = 0;
+    std::vector<rio_ctx*> ctxs;  // one per worker (from CtxPool): own stream, arenas and pinned staging
     std::vector<std::thread> workers;
     std::mutex mu;
     std::condition_variable cv;
@@ -228,6 +272,7 @@ extern "C" int rio_replay_open(int device, const char* const* paths, uint64_t n_
     for (uint64_t i = 0; i < n_paths; i++)
         if (!paths[i]) return RIO_ERR_ARG;
     auto* r = new rio_replay();
+    r->device = device;
     r->paths.assign(paths, paths + n_paths);
     r->depth = depth ? depth : 2;
     uint32_t W = workers ? workers : 2;
@@ -235,9 +280,9 @@ extern "C" int rio_replay_open(int device, const char* const* paths, uint64_t n_
     W = (uint32_t)std::min<uint64_t>(W, std::max<uint64_t>(n_paths, 1));
     for (uint32_t w = 0; w < W; w++) {
         rio_ctx* c = nullptr;
-        int rc = rio_ctx_create(device, &c);
+        int rc = CtxPool::get().take(device, &c);
         if (rc) {
-            for (rio_ctx* x : r->ctxs) rio_ctx_destroy(x);
+            for (rio_ctx* x : r->ctxs) CtxPool::get().give(device, x);
             delete r;
             return rc;
         }
@@ -279,6 +324,6 @@ extern "C" void rio_replay_free(rio_replay* r) {
     }
     for (auto& t : r->workers)
         if (t.joinable()) t.join();
-    for (rio_ctx* c : r->ctxs) rio_ctx_destroy(c);
+    for (rio_ctx* c : r->ctxs) CtxPool::get().give(r->device, c);
     delete r;
 }
