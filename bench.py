@@ -681,6 +681,26 @@ def main():
 
     value, ms_per_step, dt_max = job_throughput(dt, length, args.steps, world, device)
 
+    # when input + output fit the 256 MB MALL (C1), back-to-back steps re-read a warm
+    # cache. A second pass writes 1 GiB between decodes (outside the per-stage HIP events) and
+    # reports the cold-cache stage times beside the headline.
+    mall_flushed = None
+    if length + nb < (512 << 20):
+        evict = torch.empty(1 << 30, dtype=torch.uint8, device=device)
+        L.lib().rio_ctx_set_timing(dec.ctx, args.steps)
+        for _ in range(args.steps):
+            evict.fill_(1)
+            dec.launch(d_file, length, bufs, stream)
+        torch.cuda.synchronize(device)
+        cold = dec.stage_ms()
+        L.lib().rio_ctx_set_timing(dec.ctx, 1)
+        del evict
+        if len(cold) == 4:
+            cold_ms = sum(cold)
+            mall_flushed = {"ms_per_step": round(cold_ms, 4), "value": round(length / (cold_ms * 1e-3) / 2**30, 3),
+                            "unit": "GiB/s", "stages_ms": [round(x, 4) for x in cold],
+                            "note": "1 GiB device write between steps; per-stage HIP events, flush excluded"}
+
     # roofline of the dominant kernel (Snappy / copy decode): algorithmic bytes per launch =
     # input file bytes (headers + payloads read once) + decoded bytes written once
     # + 8(N+1) out_off + 8N rec_off + N flags read
@@ -721,6 +741,8 @@ def main():
                       "decode": round(stage[3], 4)} if len(stage) == 4 else None,
         "pipeline_roofline_frac": round(alg_bytes / (pipe_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
     }
+    if mall_flushed:
+        line["mall_flushed"] = mall_flushed
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(image, n_rec)
     if rank == 0 and world == 1 and not args.no_e2e:
