@@ -530,6 +530,15 @@ struct rio_reader {
     std::vector<uint8_t> flags;
     uint64_t cursor = 0;
     bool past_end = false;
+    // windowed decode (rio_stream) for files larger than `window`: ReadNext walks the current
+    // window's view, then fetches the next; the whole-file decode is the one-window case
+    uint64_t window = 0;  // 0: automatic (kAutoWindow above kAutoWindowFrom), ~0: never
+    rio_stream* stream = nullptr;
+    const uint8_t* w_out = nullptr;
+    const uint64_t* w_off = nullptr;
+    const uint8_t* w_flags = nullptr;
+    uint64_t w_n = 0;
+    bool w_last = true;
     // MMAP mode
     bool on_device = false;
     DevBuf dfile;
@@ -599,6 +608,9 @@ extern "C" int rio_reader_close(rio_reader* r) {
     r->open = false;
     if (r->map) munmap(const_cast<uint8_t*>(r->map), r->size);
     r->map = nullptr;
+    if (r->stream) rio_stream_free(r->stream);
+    r->stream = nullptr;
+    r->w_n = 0;
     r->dfile.release();
     r->on_device = false;
     return RIO_OK;
@@ -627,9 +639,44 @@ extern "C" void rio_reader_last_detail(rio_reader* r, uint64_t* d0, uint64_t* d1
     if (off) *off = r->err_off;
 }
 
+constexpr uint64_t kAutoWindowFrom = 1ull << 30, kAutoWindow = 256ull << 20;
+
+static uint64_t reader_window(const rio_reader* r) {
+    if (r->window == ~0ull) return 0;
+    const uint64_t w = r->window ? r->window : kAutoWindow;
+    const uint64_t from = r->window ? w : kAutoWindowFrom;
+    return r->size > RIO_FILE_HEADER_BYTES + from ? w : 0;
+}
+
+// the next window of a streamed file becomes the reader's view
+static int stream_fetch(rio_reader* r) {
+    uint64_t first = 0;
+    const uint8_t *o = nullptr, *fl = nullptr;
+    const uint64_t *off = nullptr, *ro = nullptr;
+    rio_file_info fi{};
+    int rc = rio_stream_next(r->stream, &first, &o, &off, &ro, &fl, &fi);
+    if (rc == RIO_EOF) rc = RIO_ERR_STATE;  // the last window was taken already (not reached: w_last)
+    if (rc) return rc;
+    r->w_out = o;
+    r->w_off = off;
+    r->w_flags = fl;
+    r->w_n = fi.n_records;
+    r->w_last = fi.status != RIO_OK;
+    r->cursor = 0;
+    r->info = fi;
+    return RIO_OK;
+}
+
 static int file_decode(rio_reader* r) {
     if (r->decoded) return r->decode_rc;
     r->decoded = true;
+    if (const uint64_t w = reader_window(r)) {
+        int rc = rio_stream_open(r->ctx->device, r->path.c_str(), w, 4, &r->stream);
+        if (!rc) rc = stream_fetch(r);
+        // a file the device path does not decode is refused at its first window, as below
+        if (!rc && r->info.status == RIO_ERR_UNSUPPORTED && r->w_n == 0) rc = RIO_ERR_UNSUPPORTED;
+        return r->decode_rc = rc;
+    }
     rio_file_info fi{};
     int rc = rio_frame(r->ctx, r->map, r->size, &fi);
     if (rc) return r->decode_rc = rc;
@@ -642,7 +689,30 @@ static int file_decode(rio_reader* r) {
                     fi.n_records, &fi);
     if (rc) return r->decode_rc = rc;
     r->info = fi;
+    r->w_out = r->out.data();
+    r->w_off = r->out_off.data();
+    r->w_flags = r->flags.data();
+    r->w_n = fi.n_records;
+    r->w_last = true;
     return r->decode_rc = RIO_OK;
+}
+
+// position the view on the next record: true if there is one, else the view holds the terminal info
+static int view_advance(rio_reader* r, bool& have) {
+    while (r->cursor >= r->w_n && !r->w_last) {
+        const int rc = stream_fetch(r);
+        if (rc) return rc;
+    }
+    have = r->cursor < r->w_n;
+    return RIO_OK;
+}
+
+extern "C" int rio_reader_set_window(rio_reader* r, uint64_t window_bytes) {
+    if (!r) return RIO_ERR_ARG;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (r->decoded) return RIO_ERR_STATE;
+    r->window = window_bytes;
+    return RIO_OK;
 }
 
 extern "C" int rio_reader_file_info(rio_reader* r, rio_file_info* info) {
@@ -651,6 +721,7 @@ extern "C" int rio_reader_file_info(rio_reader* r, rio_file_info* info) {
     if (!r->open || r->closed || r->mmap_mode) return RIO_ERR_STATE;
     int rc = file_decode(r);
     if (rc) return rc;
+    if (r->stream) return RIO_ERR_STATE;  // windowed: the whole-file totals are not known up front
     *info = r->info;
     return RIO_OK;
 }
@@ -673,11 +744,13 @@ extern "C" int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_
     int rc = file_decode(r);
     if (rc) return rc;
     if (r->past_end) return RIO_EOF;
-    if (r->cursor >= r->info.n_records) return terminal(r);
+    bool have = false;
+    if ((rc = view_advance(r, have))) return rc;
+    if (!have) return terminal(r);
     const uint64_t i = r->cursor++;
-    if (data) *data = r->out.data() + r->out_off[i];
-    if (len) *len = r->out_off[i + 1] - r->out_off[i];
-    if (is_nil) *is_nil = (r->flags[i] & RIO_FLAG_NIL) ? 1 : 0;
+    if (data) *data = r->w_out + r->w_off[i];
+    if (len) *len = r->w_off[i + 1] - r->w_off[i];
+    if (is_nil) *is_nil = (r->w_flags[i] & RIO_FLAG_NIL) ? 1 : 0;
     return RIO_OK;
 }
 
@@ -691,7 +764,9 @@ extern "C" int rio_reader_skip_next(rio_reader* r) {
     int rc = file_decode(r);
     if (rc) return rc;
     if (r->past_end) return RIO_EOF;
-    if (r->cursor < r->info.n_records) {
+    bool have = false;
+    if ((rc = view_advance(r, have))) return rc;
+    if (have) {
         r->cursor++;
         return RIO_OK;
     }

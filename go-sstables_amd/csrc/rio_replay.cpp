@@ -162,8 +162,39 @@ double now_ms() {
 
 const bool kTrace = getenv("RIO_REPLAY_TRACE") != nullptr;
 
-// whole file into a pinned buffer (pread: no mapping, so no page faults and no mm-lock contention
-// between the workers)
+// Bytes [off, off + n) of a file descriptor or of host memory into `dst`, split over the host
+// pool for large ranges (one thread's pread, a kernel copy out of the page cache, ran at 11-20 GB/s).
+// pread: no mapping, so no page faults and no mm-lock contention between the workers.
+struct Source {
+    int fd = -1;
+    const uint8_t* mem = nullptr;
+    int read(uint8_t* dst, uint64_t off, uint64_t n) const {
+        std::atomic<int> err{RIO_OK};
+        auto part_copy = [&](uint64_t o, uint64_t end) {
+            if (mem) {
+                memcpy(dst + (o - off), mem + o, end - o);
+                return;
+            }
+            while (o < end && err.load(std::memory_order_relaxed) == RIO_OK) {
+                const ssize_t k = pread(fd, dst + (o - off), std::min<uint64_t>(end - o, 64ull << 20), (off_t)o);
+                if (k < 0 && errno == EINTR) continue;
+                if (k <= 0) err = RIO_ERR_IO;  // error, or the file shrank under us
+                else o += (uint64_t)k;
+            }
+        };
+        if (n < (8u << 20)) {
+            part_copy(off, off + n);
+        } else {
+            HostPool::get().run([&](size_t part, size_t parts) {
+                const uint64_t step = ((n + parts - 1) / parts + 4095) & ~4095ull, o = part * step;
+                if (o < n) part_copy(off + o, off + std::min<uint64_t>(n, o + step));
+            });
+        }
+        return err.load();
+    }
+};
+
+// whole file into a pinned buffer
 int read_file(const std::string& path, PinnedBuf& in, uint64_t& len) {
     const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
     if (fd < 0) return RIO_ERR_IO;
@@ -174,31 +205,23 @@ int read_file(const std::string& path, PinnedBuf& in, uint64_t& len) {
     if (!rc && len) {
         if (!in.alloc(len)) rc = RIO_ERR_HIP;
         posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
-        // the file's byte ranges read in parallel on the host pool (one thread's pread, a kernel
-        // copy out of the page cache, ran at 11-20 GB/s)
-        std::atomic<int> err{RIO_OK};
-        auto read_range = [&](uint64_t o, uint64_t end) {
-            while (o < end && err.load(std::memory_order_relaxed) == RIO_OK) {
-                const ssize_t k = pread(fd, in.bytes() + o, std::min<uint64_t>(end - o, 64ull << 20), (off_t)o);
-                if (k < 0 && errno == EINTR) continue;
-                if (k <= 0) err = RIO_ERR_IO;  // error, or the file shrank under us
-                else o += (uint64_t)k;
-            }
-        };
-        if (!rc) {
-            if (len < (8u << 20)) {
-                read_range(0, len);
-            } else {
-                HostPool::get().run([&](size_t part, size_t parts) {
-                    const uint64_t step = ((len + parts - 1) / parts + 4095) & ~4095ull, o = part * step;
-                    if (o < len) read_range(o, std::min<uint64_t>(len, o + step));
-                });
-            }
-            rc = err.load();
-        }
+        if (!rc) rc = Source{fd, nullptr}.read(in.bytes(), 0, len);
     }
     ::close(fd);
     return rc;
+}
+
+// phase B of a framed ctx into one pinned block: out | out_off[n+1] | rec_off[n+1] | flags[n+1]
+int decode_into(rio_ctx* ctx, Decoded& d) {
+    const uint64_t n = d.info.n_records, nb = d.info.total_out_bytes;
+    const uint64_t o_off = align64(nb + 1), o_rec = o_off + align64((n + 1) * 8), o_fl = o_rec + align64((n + 1) * 8);
+    if (!d.buf.alloc(o_fl + n + 1)) return RIO_ERR_HIP;
+    d.out = d.buf.bytes();
+    d.out_off = reinterpret_cast<uint64_t*>(d.buf.bytes() + o_off);
+    d.rec_off = reinterpret_cast<uint64_t*>(d.buf.bytes() + o_rec);
+    d.flags = d.buf.bytes() + o_fl;
+    d.out_off[0] = 0;
+    return rio_decode(ctx, d.out, nb, d.out_off, d.rec_off, d.flags, n, &d.info);
 }
 
 int decode_file(rio_ctx* ctx, const std::string& path, Decoded& d) {
@@ -214,20 +237,11 @@ int decode_file(rio_ctx* ctx, const std::string& path, Decoded& d) {
         if (rc) return rc;
         t2 = now_ms();
     }
-    const uint64_t n = d.info.n_records, nb = d.info.total_out_bytes;
-    const uint64_t o_off = align64(nb + 1), o_rec = o_off + align64((n + 1) * 8), o_fl = o_rec + align64((n + 1) * 8);
-    if (!d.buf.alloc(o_fl + n + 1)) return RIO_ERR_HIP;
-    d.out = d.buf.bytes();
-    d.out_off = reinterpret_cast<uint64_t*>(d.buf.bytes() + o_off);
-    d.rec_off = reinterpret_cast<uint64_t*>(d.buf.bytes() + o_rec);
-    d.flags = d.buf.bytes() + o_fl;
-    d.out_off[0] = 0;
-    const double t3 = now_ms();
-    const int rc = rio_decode(ctx, d.out, nb, d.out_off, d.rec_off, d.flags, n, &d.info);
+    const int rc = decode_into(ctx, d);
     if (rc) return rc;
     if (kTrace)
-        fprintf(stderr, "replay %s: read %.1f frame(H2D+A) %.1f alloc %.1f decode(B+D2H) %.1f ms\n", path.c_str(),
-                t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
+        fprintf(stderr, "replay %s: read %.1f frame(H2D+A) %.1f decode(B+D2H) %.1f ms\n", path.c_str(), t1 - t0,
+                t2 - t1, now_ms() - t2);
     return RIO_OK;
 }
 
@@ -325,5 +339,242 @@ extern "C" void rio_replay_free(rio_replay* r) {
     for (auto& t : r->workers)
         if (t.joinable()) t.join();
     for (rio_ctx* c : r->ctxs) CtxPool::get().give(r->device, c);
+    delete r;
+}
+
+// ---- windowed sequential decode of one file (rio_stream_*) ------------------------------------
+//
+// FileReader.ReadNext over a file larger than the staging it should take (SURVEY §8b "per window
+// for files larger than staging"; the Go adapter's cgo call per window). Window k is the file's
+// 8-byte header followed by the bytes [s_k, e_k): a recordio file of its own, framed and decoded by
+// the whole-file path. Its terminal status decides the next window:
+//   * e_k = file end: the window's status is the file's;
+//   * raised at p > s_k: records before p are complete; the next window starts at p (a status at p
+//     may be an artifact of the cut, so p is framed again as the first record of the next window);
+//   * raised at p = s_k (no record completed): a truncation-type status (the EOF family,
+//     io.ErrUnexpectedEOF; the zero-tail test reads to the end of the file) doubles the window;
+//     any other status depends only on bytes inside the window and is the file's.
+// A record that fails to decompress ends the file at that window whatever the cut. The driver
+// thread reads and frames window k+1 on one context while a worker runs window k's decode and D2H
+// on the other, so the file's H2D overlaps its D2H. Records, offsets and statuses are those of the
+// whole-file decode: rec_off and status_offset are file offsets, out_off is window-relative.
+namespace {
+
+bool cut_type(int st) {
+    return st == RIO_EOF || st == RIO_EOF_ZERO_TAIL || st == RIO_EOF_HEADER || st == RIO_EOF_PAYLOAD ||
+           st == RIO_ERR_UNEXPECTED_EOF;
+}
+
+struct Window {
+    Decoded d;
+    uint64_t k = 0;
+    uint64_t first_record = 0;
+    bool terminal = false;
+};
+
+}  // namespace
+
+struct rio_stream {
+    Source src;
+    int fd = -1;
+    uint64_t len = 0;
+    uint64_t window = 0;
+    uint32_t depth = 4;
+    int device = 0;
+    static constexpr int kCtx = 2;
+    rio_ctx* ctx[kCtx] = {nullptr, nullptr};
+    std::thread driver, worker[kCtx];
+    std::mutex mu;
+    std::condition_variable cv;
+    struct Job {
+        bool has = false, terminal = false;
+        uint64_t k = 0, s = 0, first_record = 0;
+        rio_file_info fi{};
+    } job[kCtx];
+    bool busy[kCtx] = {false, false};
+    std::map<uint64_t, std::unique_ptr<Window>> ready;
+    std::unique_ptr<Window> current;
+    uint64_t next_out = 0;
+    uint64_t end_k = ~0ull;  // index of the terminal window once known
+    bool stop = false;
+
+    void post_fatal(uint64_t k, int rc) {
+        auto w = std::make_unique<Window>();
+        w->k = k;
+        w->d.rc = rc;
+        w->terminal = true;
+        std::lock_guard<std::mutex> g(mu);
+        end_k = std::min(end_k, k);
+        ready.emplace(k, std::move(w));
+        cv.notify_all();
+    }
+
+    void run_driver() {
+        uint8_t hdr[RIO_FILE_HEADER_BYTES] = {0};
+        const bool whole = len <= RIO_FILE_HEADER_BYTES + window;
+        if (!whole && src.read(hdr, 0, RIO_FILE_HEADER_BYTES)) return post_fatal(0, RIO_ERR_IO);
+        uint64_t s = whole ? 0 : RIO_FILE_HEADER_BYTES, first = 0;
+        for (uint64_t k = 0;; k++) {
+            const int c = (int)(k % kCtx);
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return stop || k > end_k || (!busy[c] && k < next_out + depth); });
+                if (stop || k > end_k) return;
+            }
+            uint64_t w = window, next_s = 0;
+            rio_file_info fi{};
+            bool terminal = false;
+            for (;;) {
+                const uint64_t e = whole ? len : std::min(len, s + w);
+                const uint64_t hl = whole ? 0 : RIO_FILE_HEADER_BYTES, n = hl + (e - s);
+                PinnedBuf in;
+                if (!in.alloc(n)) return post_fatal(k, RIO_ERR_HIP);
+                memcpy(in.bytes(), hdr, hl);
+                if (src.read(in.bytes() + hl, s, e - s)) return post_fatal(k, RIO_ERR_IO);
+                if (int rc = rio_frame(ctx[c], in.bytes(), n, &fi)) return post_fatal(k, rc);
+                const uint64_t p = fi.status_offset + s - hl;  // file offset of the status
+                if (e == len) {
+                    terminal = true;
+                } else if (p > s) {
+                    next_s = p;
+                } else if (cut_type(fi.status)) {
+                    w *= 2;
+                    continue;
+                } else {
+                    terminal = true;
+                }
+                break;
+            }
+            {
+                std::lock_guard<std::mutex> g(mu);
+                job[c] = Job{true, terminal, k, whole ? RIO_FILE_HEADER_BYTES : s, first, fi};
+                busy[c] = true;
+                if (terminal) end_k = std::min(end_k, k);
+                cv.notify_all();
+            }
+            if (terminal) return;
+            first += fi.n_records;
+            s = next_s;
+        }
+    }
+
+    void run_worker(int c) {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return stop || job[c].has; });
+                if (stop) return;
+                j = job[c];
+            }
+            auto w = std::make_unique<Window>();
+            w->k = j.k;
+            w->first_record = j.first_record;
+            w->d.info = j.fi;
+            w->d.rc = decode_into(ctx[c], w->d);
+            rio_file_info& fi = w->d.info;
+            const uint64_t shift = j.s - RIO_FILE_HEADER_BYTES;  // window offset -> file offset
+            for (uint64_t i = 0; !w->d.rc && shift && i < fi.n_records; i++) w->d.rec_off[i] += shift;
+            // a record the decode rejects (does not decompress, cannot be placed) ends the file
+            // here, whatever the cut
+            w->terminal = j.terminal || w->d.rc || fi.n_records < j.fi.n_records || fi.status != j.fi.status;
+            if (w->terminal) {
+                fi.status_offset += shift;
+            } else {
+                fi.status = RIO_OK;
+                fi.status_offset = 0;
+                fi.detail0 = fi.detail1 = 0;
+            }
+            std::lock_guard<std::mutex> g(mu);
+            if (w->terminal) end_k = std::min(end_k, j.k);
+            ready.emplace(j.k, std::move(w));
+            job[c].has = false;
+            busy[c] = false;
+            cv.notify_all();
+        }
+    }
+};
+
+static int stream_start(rio_stream* r, int device, uint64_t window, uint32_t depth, rio_stream** out) {
+    r->device = device;
+    r->window = window ? window : (64ull << 20);
+    r->depth = depth ? depth : 4;
+    for (int c = 0; c < rio_stream::kCtx; c++) {
+        if (int rc = CtxPool::get().take(device, &r->ctx[c])) {
+            for (int x = 0; x < c; x++) CtxPool::get().give(device, r->ctx[x]);
+            if (r->fd >= 0) ::close(r->fd);
+            delete r;
+            return rc;
+        }
+    }
+    for (int c = 0; c < rio_stream::kCtx; c++) r->worker[c] = std::thread([r, c] { r->run_worker(c); });
+    r->driver = std::thread([r] { r->run_driver(); });
+    *out = r;
+    return RIO_OK;
+}
+
+extern "C" int rio_stream_open(int device, const char* path, uint64_t window_bytes, uint32_t depth, rio_stream** out) {
+    if (!out || !path) return RIO_ERR_ARG;
+    *out = nullptr;
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return RIO_ERR_IO;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+        ::close(fd);
+        return RIO_ERR_IO;
+    }
+    posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+    auto* r = new rio_stream();
+    r->fd = fd;
+    r->src = Source{fd, nullptr};
+    r->len = (uint64_t)st.st_size;
+    return stream_start(r, device, window_bytes, depth, out);
+}
+
+extern "C" int rio_stream_open_host(int device, const uint8_t* data, uint64_t len, uint64_t window_bytes, uint32_t depth,
+                                    rio_stream** out) {
+    if (!out || (len && !data)) return RIO_ERR_ARG;
+    *out = nullptr;
+    auto* r = new rio_stream();
+    r->src = Source{-1, data};
+    r->len = len;
+    return stream_start(r, device, window_bytes, depth, out);
+}
+
+extern "C" int rio_stream_next(rio_stream* r, uint64_t* first_record, const uint8_t** out, const uint64_t** out_off,
+                               const uint64_t** rec_off, const uint8_t** flags, rio_file_info* info) {
+    if (!r) return RIO_ERR_ARG;
+    std::unique_lock<std::mutex> g(r->mu);
+    r->current.reset();  // the previous window's arrays are released here
+    const uint64_t want = r->next_out;
+    r->cv.wait(g, [&] { return want > r->end_k || r->ready.count(want) != 0; });
+    if (want > r->end_k) return RIO_EOF;
+    auto it = r->ready.find(want);
+    r->current = std::move(it->second);
+    r->ready.erase(it);
+    r->next_out++;
+    r->cv.notify_all();
+    const Window& w = *r->current;
+    if (first_record) *first_record = w.first_record;
+    if (info) *info = w.d.info;
+    if (out) *out = w.d.out;
+    if (out_off) *out_off = w.d.out_off;
+    if (rec_off) *rec_off = w.d.rec_off;
+    if (flags) *flags = w.d.flags;
+    return w.d.rc;
+}
+
+extern "C" void rio_stream_free(rio_stream* r) {
+    if (!r) return;
+    {
+        std::lock_guard<std::mutex> g(r->mu);
+        r->stop = true;
+        r->cv.notify_all();
+    }
+    if (r->driver.joinable()) r->driver.join();
+    for (auto& t : r->worker)
+        if (t.joinable()) t.join();
+    for (rio_ctx* c : r->ctx) CtxPool::get().give(r->device, c);
+    if (r->fd >= 0) ::close(r->fd);
     delete r;
 }

@@ -151,6 +151,12 @@ _SIGS = {
     "rio_replay_next": (
         c_int, [c_void_p, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(FileInfo)]),
     "rio_replay_free": (None, [c_void_p]),
+    "rio_stream_open": (c_int, [c_int, c_char_p, c_uint64, c_uint32, POINTER(c_void_p)]),
+    "rio_stream_open_host": (c_int, [c_int, c_void_p, c_uint64, c_uint64, c_uint32, POINTER(c_void_p)]),
+    "rio_stream_next": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
+                                POINTER(c_void_p), POINTER(FileInfo)]),
+    "rio_stream_free": (None, [c_void_p]),
+    "rio_reader_set_window": (c_int, [c_void_p, c_uint64]),
     "rio_encode_bound": (c_uint64, [c_uint64, c_uint64, c_uint32]),
     "rio_device_encode": (
         c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p,

@@ -128,7 +128,14 @@ class _Header:
 
 
 class FileReader(_Reader):
-    """recordio.FileReader (ReaderI) backed by a whole-file device decode."""
+    """recordio.FileReader (ReaderI) backed by the device decode: the whole file at once, or, for
+    files larger than `window_bytes` (default: files over 1 GiB in 256 MiB windows; ~0 = never),
+    window by window (rio_stream_*), with the same records and errors."""
+
+    def __init__(self, path: str, device: int = 0, window_bytes: int | None = None):
+        super().__init__(path, device)
+        if window_bytes is not None:
+            L.lib().rio_reader_set_window(self._h, window_bytes)
 
     def _not_open(self):
         return GoError(f"file reader for '{self.path}' was either not opened yet or is closed already")
@@ -220,9 +227,9 @@ class MMapReader(_Reader):
         L.lib().rio_reader_set_seek_len(self._h, v)
 
 
-def NewFileReaderWithPath(path: str, device: int = 0):  # noqa: N802
+def NewFileReaderWithPath(path: str, device: int = 0, window_bytes: int | None = None):  # noqa: N802
     try:
-        return FileReader(path, device), None
+        return FileReader(path, device, window_bytes), None
     except FileNotFoundError:
         return None, GoError(f"open {path}: no such file or directory")
 

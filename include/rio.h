@@ -272,6 +272,29 @@ int rio_replay_next(rio_replay* r, uint64_t* index, const uint8_t** out, const u
                     const uint8_t** flags, rio_file_info* info);
 void rio_replay_free(rio_replay* r);
 
+/* ---- windowed sequential decode of one file (FileReader.ReadNext, file_reader.go:61-131, over a
+ * file larger than the staging it should take: SURVEY §8b "one cgo call per window") -----------
+ * The file is framed and decoded in windows of about `window_bytes` (0 = 64 MiB; a record larger
+ * than a window doubles it) cut at record boundaries: one window's H2D overlaps the previous one's
+ * decode and D2H on a second context. At most `depth` (0 = 4) decoded windows are held ahead.
+ * rio_stream_next hands out the windows in file order: rc RIO_OK (or RIO_ERR_IO / RIO_ERR_HIP)
+ * with the window's records — out / out_off[n+1] (window-relative) / rec_off[n] (file offsets of
+ * the record headers) / flags[n], valid until the next rio_stream_next or rio_stream_free — and
+ * `first_record`, the file-wide index of its first record. info.status is RIO_OK while more windows
+ * follow; the last window carries the file's terminal status as the whole-file rio_frame /
+ * rio_decode pair reports it (status_offset a file offset; the failing record's index is
+ * first_record + info.n_records). RIO_EOF after the last window. RIO_ERR_UNSUPPORTED: the adapter
+ * continues with the reference reader after SkipNext over the records already delivered.
+ * rio_stream_open_host reads from host memory instead of a path (the caller keeps it alive until
+ * rio_stream_free). */
+typedef struct rio_stream rio_stream;
+int rio_stream_open(int device, const char* path, uint64_t window_bytes, uint32_t depth, rio_stream** out);
+int rio_stream_open_host(int device, const uint8_t* data, uint64_t len, uint64_t window_bytes, uint32_t depth,
+                         rio_stream** out);
+int rio_stream_next(rio_stream* s, uint64_t* first_record, const uint8_t** out, const uint64_t** out_off,
+                    const uint64_t** rec_off, const uint8_t** flags, rio_file_info* info);
+void rio_stream_free(rio_stream* s);
+
 /* ---- single-record decode at an arbitrary offset (MMapReader.ReadNextAt semantics) on the
  * device; `d_file` device-resident. The decoded record is written to `d_out` (capacity out_cap);
  * *len_out / *nil_out / status go to host memory (this call synchronises). */
@@ -282,7 +305,8 @@ int rio_device_read_at(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint64
 /* ------------------------------------------------------------------------------------------ */
 /* Reader handles mirroring recordio.ReaderI / recordio.ReadAtI on top of the device path.     */
 /* Returned data pointers stay valid until the next call on the same reader (ReadNextAt,       */
-/* SeekNext) or until Close (ReadNext); the Go adapter slices/copies them into Go memory.       */
+/* SeekNext) or until Close (ReadNext; windowed file readers: until the next ReadNext); the Go   */
+/* adapter slices/copies them into Go memory.                                                   */
 /* ------------------------------------------------------------------------------------------ */
 typedef struct rio_reader rio_reader;
 
@@ -305,8 +329,12 @@ int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, c
                          uint64_t* len, int* is_nil);
 /* MMapReader.seekLen (mmap_reader.go:370, default 4096; tests shrink it to 10) */
 int rio_reader_set_seek_len(rio_reader* r, uint64_t seek_len);
-/* whole-file result of a file reader after its (lazy) device decode */
+/* whole-file result of a file reader after its (lazy) device decode (RIO_ERR_STATE when windowed) */
 int rio_reader_file_info(rio_reader* r, rio_file_info* info);
+/* File readers decode files larger than 1 GiB in 256 MiB windows (rio_stream_*); before the first
+ * ReadNext / SkipNext this sets the window (files larger than it are windowed), or ~0 for whole-file
+ * decode always, or 0 for the automatic policy. Records and errors are the same either way. */
+int rio_reader_set_window(rio_reader* r, uint64_t window_bytes);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Input generator (host): byte-identical to FileWriter for v4 files (file_writer.go:160-233);   */
