@@ -639,7 +639,7 @@ extern "C" void rio_reader_last_detail(rio_reader* r, uint64_t* d0, uint64_t* d1
     if (off) *off = r->err_off;
 }
 
-constexpr uint64_t kAutoWindowFrom = 1ull << 30, kAutoWindow = 256ull << 20;
+constexpr uint64_t kAutoWindowFrom = 256ull << 20, kAutoWindow = 64ull << 20;
 
 static uint64_t reader_window(const rio_reader* r) {
     if (r->window == ~0ull) return 0;

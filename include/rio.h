@@ -331,7 +331,7 @@ int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, c
 int rio_reader_set_seek_len(rio_reader* r, uint64_t seek_len);
 /* whole-file result of a file reader after its (lazy) device decode (RIO_ERR_STATE when windowed) */
 int rio_reader_file_info(rio_reader* r, rio_file_info* info);
-/* File readers decode files larger than 1 GiB in 256 MiB windows (rio_stream_*); before the first
+/* File readers decode files larger than 256 MiB in 64 MiB windows (rio_stream_*); before the first
  * ReadNext / SkipNext this sets the window (files larger than it are windowed), or ~0 for whole-file
  * decode always, or 0 for the automatic policy. Records and errors are the same either way. */
 int rio_reader_set_window(rio_reader* r, uint64_t window_bytes);

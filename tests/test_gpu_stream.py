@@ -194,3 +194,28 @@ def test_random_damage_random_windows(tmp_path, seed):
     p = tmp_path / "d.rio"
     p.write_bytes(data)
     assert reader_loop(str(p), window) == reader_loop(str(p), NEVER)
+
+
+def test_file_reader_windows_large_files_by_default(tmp_path):
+    """Files over 256 MiB are windowed by default (FileInfo then has no whole-file totals); every
+    record equals the oracle's."""
+    import hashlib
+
+    img = generate(300_000, 1024, 0, kind=1, seed=21)
+    assert img.shape[0] > (256 << 20)
+    p = tmp_path / "big.rio"
+    img.tofile(str(p))
+    exp = orc.file_reader_decode_arrays(img)
+    r = FileReader(str(p))
+    assert r.Open() is None
+    h, n = hashlib.sha1(), 0
+    while True:
+        rec, err = r.ReadNext()
+        if err is not None:
+            break
+        h.update(rec)
+        n += 1
+    assert r.FileInfo() is None  # windowed
+    assert n == exp["n_records"] == 300_000
+    assert h.digest() == hashlib.sha1(exp["out"].tobytes()).digest()
+    assert "EOF" in str(err)
