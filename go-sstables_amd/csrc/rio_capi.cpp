@@ -403,12 +403,34 @@ static int d2h_staged(rio_ctx* c, uint8_t* dst, const void* src, uint64_t n) {
     return RIO_OK;
 }
 
-extern "C" int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_file_info* info) {
-    if (!ctx || (!file && len) || !info) return RIO_ERR_ARG;
+// host producer -> device through the two pinned staging pieces: producing piece k+1 overlaps
+// the DMA of piece k (the pieces are filled in order)
+static int h2d_fill(rio_ctx* c, void* dst, uint64_t n, rio::FillFn fill, void* user) {
+    int rc = ensure_pinned(c);
+    if (rc) return rc;
+    uint64_t o = 0;
+    int k = 0;
+    while (o < n) {
+        const uint64_t m = std::min<uint64_t>(kStage, n - o);
+        HIP_TRY(hipEventSynchronize(c->pin_ev[k]));
+        if ((rc = fill(user, c->pinned[k], o, m))) {
+            (void)hipStreamSynchronize(c->stream);  // the other piece's DMA may still read staging
+            return rc;
+        }
+        HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, c->pinned[k], m, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(c->pin_ev[k], c->stream));
+        o += m;
+        k ^= 1;
+    }
+    return RIO_OK;
+}
+
+static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const uint8_t* file, rio::FillFn fill,
+                        void* user) {
     HIP_TRY(hipSetDevice(ctx->device));
     ctx->framed = false;
     HIP_TRY(ctx->file.ensure(len + RIO_DEVICE_PAD));
-    int rc = h2d_staged(ctx, ctx->file.p, file, len);
+    int rc = fill ? h2d_fill(ctx, ctx->file.p, len, fill, user) : h2d_staged(ctx, ctx->file.p, file, len);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(ctx->file.as<uint8_t>() + len, 0, RIO_DEVICE_PAD, ctx->stream));
     FrameParams P;
@@ -423,6 +445,18 @@ extern "C" int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_fi
     ctx->file_len = len;
     return RIO_OK;
 }
+
+extern "C" int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_file_info* info) {
+    if (!ctx || (!file && len) || !info) return RIO_ERR_ARG;
+    return frame_common(ctx, len, info, file, nullptr, nullptr);
+}
+
+namespace rio {
+int frame_fill(rio_ctx* ctx, uint64_t len, FillFn fill, void* user, rio_file_info* info) {
+    if (!ctx || !fill || !info) return RIO_ERR_ARG;
+    return frame_common(ctx, len, info, nullptr, fill, user);
+}
+}  // namespace rio
 
 extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, uint64_t* rec_off,
                           uint8_t* flags, uint64_t rec_cap, rio_file_info* info) {
@@ -639,7 +673,7 @@ extern "C" void rio_reader_last_detail(rio_reader* r, uint64_t* d0, uint64_t* d1
     if (off) *off = r->err_off;
 }
 
-constexpr uint64_t kAutoWindowFrom = 256ull << 20, kAutoWindow = 64ull << 20;
+constexpr uint64_t kAutoWindowFrom = 256ull << 20, kAutoWindow = 128ull << 20;
 
 static uint64_t reader_window(const rio_reader* r) {
     if (r->window == ~0ull) return 0;

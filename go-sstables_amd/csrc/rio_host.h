@@ -10,6 +10,8 @@
 #include <thread>
 #include <vector>
 
+#include "rio.h"
+
 namespace rio {
 
 // A small persistent pool for host-side byte moving: copies into / out of the pinned staging pieces,
@@ -81,5 +83,13 @@ class HostPool {
     size_t remaining_ = 0;
     uint64_t gen_ = 0;
 };
+
+// Framing of a file whose bytes a host producer writes piece by piece into the context's pinned
+// staging (rio_capi.cpp): fill(user, dst, off, n) writes file bytes [off, off + n) to dst and
+// returns RIO_OK or an error, which aborts the frame. Producing piece k+1 overlaps the DMA of
+// piece k; then rio_frame's device work. Used by rio_replay.cpp (pread straight into staging, and
+// the windows of rio_stream: a synthetic file header followed by a byte range of the file).
+typedef int (*FillFn)(void* user, uint8_t* dst, uint64_t off, uint64_t n);
+int frame_fill(rio_ctx* ctx, uint64_t len, FillFn fill, void* user, rio_file_info* info);
 
 }  // namespace rio

@@ -194,23 +194,6 @@ struct Source {
     }
 };
 
-// whole file into a pinned buffer
-int read_file(const std::string& path, PinnedBuf& in, uint64_t& len) {
-    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
-    if (fd < 0) return RIO_ERR_IO;
-    struct stat st;
-    int rc = RIO_OK;
-    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) rc = RIO_ERR_IO;
-    len = rc ? 0 : (uint64_t)st.st_size;
-    if (!rc && len) {
-        if (!in.alloc(len)) rc = RIO_ERR_HIP;
-        posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
-        if (!rc) rc = Source{fd, nullptr}.read(in.bytes(), 0, len);
-    }
-    ::close(fd);
-    return rc;
-}
-
 // phase B of a framed ctx into one pinned block: out | out_off[n+1] | rec_off[n+1] | flags[n+1]
 int decode_into(rio_ctx* ctx, Decoded& d) {
     const uint64_t n = d.info.n_records, nb = d.info.total_out_bytes;
@@ -224,24 +207,47 @@ int decode_into(rio_ctx* ctx, Decoded& d) {
     return rio_decode(ctx, d.out, nb, d.out_off, d.rec_off, d.flags, n, &d.info);
 }
 
+// Source bytes [base + off, base + off + n) behind an optional synthetic prefix (a window's file
+// header): the rio::frame_fill producer
+struct Fill {
+    const Source* src;
+    uint64_t base = 0;
+    const uint8_t* prefix = nullptr;
+    uint64_t prefix_len = 0;
+    static int fn(void* user, uint8_t* dst, uint64_t off, uint64_t n) {
+        const Fill& f = *static_cast<const Fill*>(user);
+        if (off < f.prefix_len) {
+            const uint64_t k = std::min(n, f.prefix_len - off);
+            memcpy(dst, f.prefix + off, k);
+            dst += k;
+            off += k;
+            n -= k;
+        }
+        return n ? f.src->read(dst, f.base + (off - f.prefix_len), n) : RIO_OK;
+    }
+};
+
 int decode_file(rio_ctx* ctx, const std::string& path, Decoded& d) {
     const double t0 = now_ms();
-    uint64_t len = 0;
-    double t1, t2;
-    {
-        PinnedBuf in;
-        int rc = read_file(path, in, len);
-        if (rc) return rc;
-        t1 = now_ms();
-        rc = rio_frame(ctx, in.bytes(), len, &d.info);  // synchronises: `in` can go back to the pool
-        if (rc) return rc;
-        t2 = now_ms();
+    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return RIO_ERR_IO;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+        ::close(fd);
+        return RIO_ERR_IO;
     }
-    const int rc = decode_into(ctx, d);
+    posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+    // pread straight into the context's staging pieces, overlapping the H2D of the previous piece
+    const Source src{fd, nullptr};
+    Fill f{&src};
+    int rc = rio::frame_fill(ctx, (uint64_t)st.st_size, &Fill::fn, &f, &d.info);
+    ::close(fd);
+    if (rc) return rc;
+    const double t1 = now_ms();
+    rc = decode_into(ctx, d);
     if (rc) return rc;
     if (kTrace)
-        fprintf(stderr, "replay %s: read %.1f frame(H2D+A) %.1f decode(B+D2H) %.1f ms\n", path.c_str(), t1 - t0,
-                t2 - t1, now_ms() - t2);
+        fprintf(stderr, "replay %s: read+H2D+frame %.1f decode(B+D2H) %.1f ms\n", path.c_str(), t1 - t0, now_ms() - t1);
     return RIO_OK;
 }
 
@@ -427,11 +433,8 @@ struct rio_stream {
             for (;;) {
                 const uint64_t e = whole ? len : std::min(len, s + w);
                 const uint64_t hl = whole ? 0 : RIO_FILE_HEADER_BYTES, n = hl + (e - s);
-                PinnedBuf in;
-                if (!in.alloc(n)) return post_fatal(k, RIO_ERR_HIP);
-                memcpy(in.bytes(), hdr, hl);
-                if (src.read(in.bytes() + hl, s, e - s)) return post_fatal(k, RIO_ERR_IO);
-                if (int rc = rio_frame(ctx[c], in.bytes(), n, &fi)) return post_fatal(k, rc);
+                Fill f{&src, s, hdr, hl};
+                if (int rc = rio::frame_fill(ctx[c], n, &Fill::fn, &f, &fi)) return post_fatal(k, rc);
                 const uint64_t p = fi.status_offset + s - hl;  // file offset of the status
                 if (e == len) {
                     terminal = true;
@@ -497,7 +500,7 @@ struct rio_stream {
 
 static int stream_start(rio_stream* r, int device, uint64_t window, uint32_t depth, rio_stream** out) {
     r->device = device;
-    r->window = window ? window : (64ull << 20);
+    r->window = window ? window : (128ull << 20);
     r->depth = depth ? depth : 4;
     for (int c = 0; c < rio_stream::kCtx; c++) {
         if (int rc = CtxPool::get().take(device, &r->ctx[c])) {

@@ -274,7 +274,7 @@ void rio_replay_free(rio_replay* r);
 
 /* ---- windowed sequential decode of one file (FileReader.ReadNext, file_reader.go:61-131, over a
  * file larger than the staging it should take: SURVEY §8b "one cgo call per window") -----------
- * The file is framed and decoded in windows of about `window_bytes` (0 = 64 MiB; a record larger
+ * The file is framed and decoded in windows of about `window_bytes` (0 = 128 MiB; a record larger
  * than a window doubles it) cut at record boundaries: one window's H2D overlaps the previous one's
  * decode and D2H on a second context. At most `depth` (0 = 4) decoded windows are held ahead.
  * rio_stream_next hands out the windows in file order: rc RIO_OK (or RIO_ERR_IO / RIO_ERR_HIP)
@@ -331,7 +331,7 @@ int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, c
 int rio_reader_set_seek_len(rio_reader* r, uint64_t seek_len);
 /* whole-file result of a file reader after its (lazy) device decode (RIO_ERR_STATE when windowed) */
 int rio_reader_file_info(rio_reader* r, rio_file_info* info);
-/* File readers decode files larger than 256 MiB in 64 MiB windows (rio_stream_*); before the first
+/* File readers decode files larger than 256 MiB in 128 MiB windows (rio_stream_*); before the first
  * ReadNext / SkipNext this sets the window (files larger than it are windowed), or ~0 for whole-file
  * decode always, or 0 for the automatic policy. Records and errors are the same either way. */
 int rio_reader_set_window(rio_reader* r, uint64_t window_bytes);
