@@ -88,7 +88,7 @@ __device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& h
 #define RIO_NT 0
 #endif
 // timing-only experiment knobs (wrong output): 1 = no out16 funnel, 2 = no place16, 4 = no in16 funnel,
-// 8 = no flush bpermutes of the owner base
+// 8 = no flush bpermutes of the owner base, 16 = far-history loads to the sink (traffic attribution)
 #ifndef RIO_EXP
 #define RIO_EXP 0
 #endif
@@ -308,7 +308,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const bool want_desc = S.kind != 2 && nds == 0;
             S.desc = want_desc ? 1u : 0u;
             nds = want_desc ? 1u : nds;
-            const uint8_t* ap = S.kind == 2 ? gout + S.q
+            const uint8_t* ap = S.kind == 2 ? ((RIO_EXP & 16) ? sink : gout + S.q)
                                             : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
             S.aux = ld_far(ap);
         }
