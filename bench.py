@@ -766,6 +766,9 @@ def main():
         "stages_ms": {"walk": round(stage[0], 4), "scan": round(stage[1], 4), "place": round(stage[2], 4),
                       "decode": round(stage[3], 4)} if len(stage) == 4 else None,
         "pipeline_roofline_frac": round(alg_bytes / (pipe_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        # also output GiB/s and records/s (whole job, same timed region as `value`)
+        "output_GiBps": round(value * nb / length, 3),
+        "Mrecords_per_s": round(value * 2**30 / length * n / 1e6, 2),
     }
     if mall_flushed:
         line["mall_flushed"] = mall_flushed
