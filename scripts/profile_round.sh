@@ -6,6 +6,15 @@
 set -u
 TAG=$1; CFG=${2:-c2}
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
+if [ -n "${LINES_ONLY:-}" ]; then  # only the extra bench lines (second call of a round)
+    for c in $LINES_ONLY; do
+        echo "== bench_$c ($(date +%T))"
+        timeout -k 10 600 python bench.py --config $c > "$OUT/bench_$c.log" 2>&1 || { echo "bench_$c failed"; tail -5 "$OUT/bench_$c.log"; exit 1; }
+        grep '^{' "$OUT/bench_$c.log" > "$OUT/bench_$c.json" || true
+        tail -c 300 "$OUT/bench_$c.json"; echo
+    done
+    exit 0
+fi
 fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
 step() {
     local name=$1 to=$2; shift 2
@@ -33,8 +42,9 @@ grep '^{' "$OUT/bench_c5.log" > "$OUT/bench_c5.json" || true
 step rocprof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- \
     python bench.py --config c5 --no-cpu-baseline
 find "$OUT/prof_c5" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_c5.csv" \;
-# the other bench lines (their own metrics): WAL replay, batched DiskKeyIndex.Get, device encode, random records
-for c in wal idx enc c2r; do
+# the other bench lines (their own metrics): WAL replay, batched DiskKeyIndex.Get, device encode, random records;
+# PROFILE_LINES overrides the list (e.g. "c1 c3 c4 c2g" in a second call, keeping each call within gpurun's limit)
+for c in ${PROFILE_LINES:-wal idx enc c2r}; do
     step bench_$c 600 python bench.py --config $c
     grep '^{' "$OUT/bench_$c.log" > "$OUT/bench_$c.json" || true
 done
