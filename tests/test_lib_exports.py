@@ -39,3 +39,19 @@ def test_status_vocabulary():
 def test_code_object_targets_gfx950():
     data = open(L.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_stream_and_replay_argument_errors():
+    """Host-side argument and I/O errors of the windowed / replay handles come back before any
+    device call (no GPU needed): null handles, a missing path, a directory."""
+    lib = L.lib()
+    h = ctypes.c_void_p()
+    assert lib.rio_stream_open(0, None, 0, 0, ctypes.byref(h)) == L.RIO_ERR_ARG
+    assert lib.rio_stream_open(0, b"/nonexistent/file.rio", 0, 0, ctypes.byref(h)) == L.RIO_ERR_IO
+    assert lib.rio_stream_open(0, REPO.encode(), 0, 0, ctypes.byref(h)) == L.RIO_ERR_IO  # not a regular file
+    assert not h.value
+    assert lib.rio_stream_open_host(0, None, 5, 0, 0, ctypes.byref(h)) == L.RIO_ERR_ARG
+    assert lib.rio_stream_next(None, None, None, None, None, None, None) == L.RIO_ERR_ARG
+    lib.rio_stream_free(None)
+    assert lib.rio_replay_next(None, None, None, None, None, None) == L.RIO_ERR_ARG
+    lib.rio_replay_free(None)
