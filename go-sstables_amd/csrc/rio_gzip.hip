@@ -120,34 +120,37 @@ struct BitIn {
 // Canonical Huffman tables from code lengths lens[0..n) (Go huffmanDecoder.init acceptance).
 // Returns false for an invalid (over-subscribed or incomplete) code; an all-zero code is accepted
 // and fails when used.
+// Lane l in [1, 16) owns code length l (its count, first canonical code and first sorted index);
+// uses with a constant l read it back with readlane into a scalar register, so no per-lane arrays
+// of wave-uniform values occupy VGPRs.
 __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_t* sym, uint16_t* fast,
                          uint32_t lane) {
-    uint32_t c[16];
-#pragma unroll
-    for (int l = 0; l < 16; l++) c[l] = 0;
+    uint32_t my_c = 0;  // codes of length `lane`
     for (uint32_t g = 0; g < n; g += 64) {
         const uint32_t s = g + lane;
         const uint32_t L = s < n ? lens[s] : 0u;
 #pragma unroll
-        for (int l = 1; l < 16; l++) c[l] += (uint32_t)__builtin_popcountll(__ballot(L == (uint32_t)l));
+        for (int l = 1; l < 16; l++) {
+            const uint32_t k = (uint32_t)__builtin_popcountll(__ballot(L == (uint32_t)l));
+            my_c += lane == (uint32_t)l ? k : 0u;
+        }
     }
     uint32_t maxl = 0;
 #pragma unroll
-    for (int l = 1; l < 16; l++) maxl = c[l] ? (uint32_t)l : maxl;
-    uint32_t code = 0, next[16], idx[16], acc = 0;
+    for (int l = 1; l < 16; l++) maxl = __builtin_amdgcn_readlane(my_c, l) ? (uint32_t)l : maxl;
+    // canonical codes (RFC 1951 3.2.2): first code and first sorted index of every length
+    uint32_t code = 0, acc = 0, my_next = 0, my_idx = 0;
 #pragma unroll
     for (int l = 1; l < 16; l++) {
+        const uint32_t c = __builtin_amdgcn_readlane(my_c, l);
         code <<= 1;
-        next[l] = code;
-        idx[l] = acc;
-        if ((uint32_t)l <= maxl) code += c[l];
-        acc += c[l];
+        my_next = lane == (uint32_t)l ? code : my_next;
+        my_idx = lane == (uint32_t)l ? acc : my_idx;
+        if ((uint32_t)l <= maxl) code += c;
+        acc += c;
     }
-    if (lane < 16) cnt[lane] = 0;
+    if (lane < 16) cnt[lane] = (uint16_t)(lane ? my_c : 0u);
     __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int l = 1; l < 16; l++)
-        if (lane == (uint32_t)l) cnt[l] = (uint16_t)c[l];
     if (maxl == 0) {
         for (uint32_t e = lane; e < kFastSize; e += 64) fast[e] = 0;
         __builtin_amdgcn_wave_barrier();
@@ -157,17 +160,16 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
     const uint32_t full = code >> (15 - maxl);  // codes counted at length maxl
     if (full != (1u << maxl) && !(full == 1 && maxl == 1)) return false;
     // symbols sorted by (length, symbol): rank of each symbol among equal lengths via ballots
-    uint32_t off[16];
-#pragma unroll
-    for (int l = 1; l < 16; l++) off[l] = idx[l];
+    uint32_t my_off = my_idx;  // next free sorted slot of length `lane`
     for (uint32_t g = 0; g < n; g += 64) {
         const uint32_t s = g + lane;
         const uint32_t L = s < n ? lens[s] : 0u;
 #pragma unroll
         for (int l = 1; l < 16; l++) {
             const uint64_t m = __ballot(L == (uint32_t)l);
-            if (L == (uint32_t)l) sym[off[l] + lane_mbcnt(m)] = (uint16_t)s;
-            off[l] += (uint32_t)__builtin_popcountll(m);
+            const uint32_t base = __builtin_amdgcn_readlane(my_off, l);
+            if (L == (uint32_t)l) sym[base + lane_mbcnt(m)] = (uint16_t)s;
+            my_off += lane == (uint32_t)l ? (uint32_t)__builtin_popcountll(m) : 0u;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -177,7 +179,9 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
 #pragma unroll
         for (int l = 1; l <= (int)kFastBits; l++) {
             v = (v << 1) | ((e >> (l - 1)) & 1u);
-            if (ent == 0 && v - next[l] < c[l]) ent = (uint32_t)sym[idx[l] + v - next[l]] | ((uint32_t)l << 9);
+            const uint32_t nx = __builtin_amdgcn_readlane(my_next, l), c = __builtin_amdgcn_readlane(my_c, l);
+            if (ent == 0 && v - nx < c)
+                ent = (uint32_t)sym[__builtin_amdgcn_readlane(my_idx, l) + v - nx] | ((uint32_t)l << 9);
         }
         fast[e] = (uint16_t)ent;
     }
