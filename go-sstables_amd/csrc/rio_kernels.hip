@@ -1266,9 +1266,20 @@ __device__ __forceinline__ bool eof_class(int e) {
     return e == RIO_EOF || e == RIO_EOF_ZERO_TAIL || e == RIO_EOF_HEADER || e == RIO_EOF_PAYLOAD;
 }
 
-__global__ void __launch_bounds__(256) k_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len,
-                                                      const uint8_t* keys, const uint64_t* key_off, uint64_t nq,
-                                                      const uint32_t* perm, rio_index_hit* hits) {
+// minimum waves per SIMD for k_index_search (0 = the compiler's choice: 129 VGPRs, 3 waves). Measured on
+// the idx bench (M lookups/s): 3 waves 155.6, 4 189.3, 5 199.0, 6 21.2 (3393 scratch ops in the probe
+// loop), 8 228.9 (64 VGPRs, 384 B scratch, 281 scratch ops). The spill placement is the compiler's and
+// changes with the bound; re-measure after touching this kernel.
+#ifndef RIO_IDX_OCC
+#define RIO_IDX_OCC 8
+#endif
+#if RIO_IDX_OCC
+__global__ void __launch_bounds__(256, RIO_IDX_OCC) k_index_search(
+#else
+__global__ void __launch_bounds__(256) k_index_search(
+#endif
+    const uint8_t* f, uint64_t len, uint64_t seek_len, const uint8_t* keys, const uint64_t* key_off, uint64_t nq,
+    const uint32_t* perm, rio_index_hit* hits) {
     __shared__ uint32_t T[1024];  // CRC-32C tables (T[0..255] = the byte table)
     crc32c_tab_init(T);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
