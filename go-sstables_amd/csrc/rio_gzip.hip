@@ -24,8 +24,8 @@
 // buffer, tables read from LDS as broadcasts); the lanes split the wide work: loading the input
 // into an LDS ring 1 KiB at a time, building the decode tables (ballot-based counting and
 // sorting), match copies (64 bytes per round, `k mod dist` for overlapping copies) and flushing
-// the LDS output window to HBM 1 KiB at a time. Two instantiations: records decoding to <= 2 KiB
-// keep the whole record in a 2 KiB window (many waves per CU), larger ones use the 32 KiB DEFLATE
+// the LDS output window to HBM 1 KiB at a time. Three instantiations: records decoding to <= 1 KiB and <= 2 KiB
+// keep the whole record in a 1 / 2 KiB window (7 / 5 waves per SIMD), larger ones use the 32 KiB DEFLATE
 // window.
 // k_gzip_crc: one lane per record, CRC-32/IEEE of the decoded bytes against the trailer.
 #include <hip/hip_runtime.h>
@@ -38,6 +38,8 @@ namespace rio {
 namespace {
 constexpr uint32_t kGzWaves = 4;          // waves per workgroup
 constexpr uint32_t kGzIn = 2048;          // LDS input ring per wave (two 1 KiB refill blocks)
+constexpr uint32_t kGzTinyIn = 1024;      // tiny class: two 512-B refill blocks
+constexpr uint32_t kGzTinyWin = 1024;     // records with decoded size <= this: whole record in 1 KiB
 constexpr uint32_t kGzSmallWin = 2048;    // records with decoded size <= this: whole record in LDS
 constexpr uint32_t kGzLargeWin = 32768;   // DEFLATE window (maximum distance)
 constexpr uint32_t kFastBits = 9;         // decode-table bits
@@ -58,10 +60,10 @@ struct GzTables {
     uint8_t lens[288 + 32 + 8];  // code lengths being read (litlen then distance)
 };
 
-template <uint32_t kWin>
+template <uint32_t kWin, uint32_t kIn>
 struct GzLds {
     GzTables t;
-    uint8_t in[kGzIn] __attribute__((aligned(16)));
+    uint8_t in[kIn] __attribute__((aligned(16)));
     uint8_t win[kWin] __attribute__((aligned(16)));
 };
 
@@ -71,12 +73,15 @@ __device__ __forceinline__ uint32_t lane_mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Wave-uniform bit reader over the record's DEFLATE stream [0, slen), staged through the LDS ring.
+// Wave-uniform bit reader over the record's DEFLATE stream [0, slen), staged through an LDS ring of
+// kIn bytes refilled kIn / 2 bytes at a time.
+template <uint32_t kIn>
 struct BitIn {
+    static constexpr uint32_t kBlk = kIn / 2;
     const uint8_t* src;  // stream start in HBM
     uint8_t* ring;
     uint32_t slen;
-    uint32_t loaded;  // stream bytes [loaded - kGzIn, loaded) are in the ring
+    uint32_t loaded;  // stream bytes [loaded - kIn, loaded) are in the ring
     uint32_t pos;     // next stream byte pulled into bb
     uint64_t bb;
     uint32_t nb;
@@ -84,13 +89,13 @@ struct BitIn {
     // bits consumed so far (read-ahead past slen is zero-filled; overrun is checked by the caller)
     __device__ __forceinline__ uint64_t consumed() const { return 8ull * pos - nb; }
 
-    // make stream bytes [p, p + 8) resident (1 KiB blocks, every lane loads 16 bytes)
+    // make stream bytes [p, p + 8) resident (kBlk-byte blocks, 16 bytes per lane)
     __device__ void stage(uint32_t p, uint32_t lane) {
-        if (p >= loaded || p + kGzIn < loaded) loaded = p & ~1023u;  // jump (stored block skip)
+        if (p >= loaded || p + kIn < loaded) loaded = p & ~(kBlk - 1);  // jump (stored block skip)
         while (loaded < p + 8 && loaded < slen) {
             const uint32_t off = loaded + lane * 16;
-            if (off < slen) *reinterpret_cast<uint4*>(ring + (off & (kGzIn - 1))) = ldu16(src + off);
-            loaded += 1024;
+            if (lane * 16 < kBlk && off < slen) *reinterpret_cast<uint4*>(ring + (off & (kIn - 1))) = ldu16(src + off);
+            loaded += kBlk;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -98,8 +103,8 @@ struct BitIn {
         while (nb <= 32) {
             stage(pos, lane);
             const uint32_t a = pos & ~3u;
-            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(ring + (a & (kGzIn - 1)));
-            const uint32_t w1 = *reinterpret_cast<const uint32_t*>(ring + ((a + 4) & (kGzIn - 1)));
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(ring + (a & (kIn - 1)));
+            const uint32_t w1 = *reinterpret_cast<const uint32_t*>(ring + ((a + 4) & (kIn - 1)));
             uint32_t v = uni(__builtin_amdgcn_alignbyte(w1, w0, pos & 3u));
             const uint32_t valid = pos < slen ? slen - pos : 0u;
             if (valid < 4) v &= valid == 0 ? 0u : (0xFFFFFFFFu >> (32u - 8u * valid));
@@ -190,7 +195,8 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
 }
 
 // One symbol; -1 if the bits match no code (incomplete / empty code).
-__device__ __forceinline__ int gz_sym(BitIn& B, const uint16_t* fast, const uint16_t* cnt, const uint16_t* sym) {
+template <uint32_t kIn>
+__device__ __forceinline__ int gz_sym(BitIn<kIn>& B, const uint16_t* fast, const uint16_t* cnt, const uint16_t* sym) {
     const uint32_t e = uni(fast[(uint32_t)B.bb & (kFastSize - 1)]);
     if (e) {
         B.bits(e >> 9);
@@ -228,11 +234,14 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t s, uint32_t& eb) {  // s 
 enum : int { kGzOk = 0, kGzCorrupt = 1, kGzUnsupported = 2 };
 
 // Inflate one record's single gzip member into `out` (exactly dlen bytes announced by ISIZE).
-template <uint32_t kWin>
-__device__ int gz_record(GzLds<kWin>& S, const uint8_t* src, uint32_t slen, uint8_t* out, uint32_t dlen,
+// kWhole: the window holds the whole record (flushed once at the end; decoding past it hands the file
+// back, see the header).
+template <uint32_t kWin, uint32_t kIn>
+__device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen, uint8_t* out, uint32_t dlen,
                          uint32_t lane) {
+    constexpr bool kWhole = kWin < kGzLargeWin;
     GzTables& T = S.t;
-    BitIn B{src, S.in, slen, 0, 0, 0ull, 0};
+    BitIn<kIn> B{src, S.in, slen, 0, 0, 0ull, 0};
     B.refill(lane);
     // ---- member header (gzip reader.go readHeader) ----
     if (slen < 10) return kGzCorrupt;
@@ -311,14 +320,14 @@ __device__ int gz_record(GzLds<kWin>& S, const uint8_t* src, uint32_t slen, uint
             if (B.overrun() || (ln ^ 0xFFFFu) != nl) return kGzCorrupt;
             const uint32_t p0 = p + 4;
             if (ln > slen - min(slen, p0)) return kGzCorrupt;
-            if (kWin == kGzSmallWin && d + ln > kWin) return kGzUnsupported;
+            if (kWhole && d + ln > kWin) return kGzUnsupported;
             // 1 KiB at a time, flushing in between: the window never overruns unflushed bytes
             for (uint32_t k0 = 0; k0 < ln; k0 += 1024) {
                 const uint32_t m = min(1024u, ln - k0);
                 for (uint32_t k = lane; k < m; k += 64) S.win[(d + k) & (kWin - 1)] = src[p0 + k0 + k];
                 __builtin_amdgcn_wave_barrier();
                 d += m;
-                if (kWin != kGzSmallWin && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
+                if (!kWhole && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
             }
             B.pos = p0 + ln;
             B.nb = 0;
@@ -390,7 +399,7 @@ __device__ int gz_record(GzLds<kWin>& S, const uint8_t* src, uint32_t slen, uint
             const int s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
             if (s < 0 || B.overrun()) return kGzCorrupt;
             if (s < 256) {
-                if (kWin == kGzSmallWin && d >= kWin) return kGzUnsupported;
+                if (kWhole && d >= kWin) return kGzUnsupported;
                 if (lane == 0) S.win[d & (kWin - 1)] = (uint8_t)s;
                 d++;
             } else if (s == 256) {
@@ -405,7 +414,7 @@ __device__ int gz_record(GzLds<kWin>& S, const uint8_t* src, uint32_t slen, uint
                 uint32_t deb;
                 const uint32_t dist = dist_base((uint32_t)ds, deb) + B.bits(deb);
                 if (B.overrun() || dist > d) return kGzCorrupt;
-                if (kWin == kGzSmallWin && d + len > kWin) return kGzUnsupported;
+                if (kWhole && d + len > kWin) return kGzUnsupported;
                 // source bytes all precede d: k mod dist repeats the last `dist` bytes
                 const float rc = 1.0f / (float)dist;
                 for (uint32_t k0 = 0; k0 < len; k0 += 64) {
@@ -423,7 +432,7 @@ __device__ int gz_record(GzLds<kWin>& S, const uint8_t* src, uint32_t slen, uint
                 d += len;
             }
             __builtin_amdgcn_wave_barrier();
-            if (kWin != kGzSmallWin && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
+            if (!kWhole && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
         }
     }
     // ---- trailer: byte-aligned CRC-32 + ISIZE ending the payload (one member per record) ----
@@ -447,27 +456,38 @@ __device__ __forceinline__ void gz_fail(const FrameParams& P, uint64_t i, int rc
 }
 }  // namespace
 
+// waves per SIMD the LDS allows: tiny 5.1 KB per wave -> 7 workgroups of 4 waves, small 7.2 KB -> 5
+#ifndef RIO_GZ_TINY_WGS
+#define RIO_GZ_TINY_WGS 7
+#endif
 template <uint32_t kWin>
-__global__ void __launch_bounds__(64 * kGzWaves, kWin == kGzSmallWin ? 5 : 1) k_gzip_inflate(FrameParams P) {
+constexpr int gz_wgs() { return kWin == kGzTinyWin ? RIO_GZ_TINY_WGS : kWin == kGzSmallWin ? 5 : 1; }
+template <uint32_t kWin>
+constexpr uint32_t gz_in() { return kWin == kGzTinyWin ? kGzTinyIn : kGzIn; }
+
+template <uint32_t kWin>
+__global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(FrameParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const ScanState* st = P.state;
     if (!gzip_active(P, st)) return;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    GzLds<kWin>& S = *reinterpret_cast<GzLds<kWin>*>(lds + wv * sizeof(GzLds<kWin>));
+    using Lds = GzLds<kWin, gz_in<kWin>()>;
+    Lds& S = *reinterpret_cast<Lds*>(lds + wv * sizeof(Lds));
     const uint64_t n = st->n_records;
     const uint64_t waves = (uint64_t)gridDim.x * kGzWaves;
     for (uint64_t i = (uint64_t)blockIdx.x * kGzWaves + wv; i < n; i += waves) {
         if (P.flags[i] & RIO_FLAG_NIL) continue;
         const uint64_t o0 = P.out_off[i], dlen = P.out_off[i + 1] - o0;
-        // size classes: the small window takes records it holds whole
-        if ((kWin == kGzSmallWin) != (dlen <= kGzSmallWin)) continue;
+        // size classes: (0, 1 KiB], (1 KiB, 2 KiB] held whole in LDS, larger ones through the DEFLATE window
+        const uint32_t cls = dlen <= kGzTinyWin ? kGzTinyWin : dlen <= kGzSmallWin ? kGzSmallWin : kGzLargeWin;
+        if (cls != kWin) continue;
         const uint64_t pay = P.rec_pay[i];
         const uint64_t slen = pay >> 8;
         if (slen >= 0xFFFFFFF0ull || dlen >= 0xFFFFFFF0ull) {
             if (lane == 0) gz_fail(P, i, kGzUnsupported);
             continue;
         }
-        const int rc = gz_record<kWin>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen, P.out + o0,
+        const int rc = gz_record<kWin, gz_in<kWin>()>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen, P.out + o0,
                                        (uint32_t)dlen, lane);
         if (rc != kGzOk && lane == 0) gz_fail(P, i, rc);
     }
@@ -511,10 +531,12 @@ __global__ void __launch_bounds__(256) k_gzip_crc(FrameParams P) {
 }
 
 hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_gzip_inflate<kGzTinyWin>, dim3(256 * gz_wgs<kGzTinyWin>()), dim3(64 * kGzWaves),
+                       kGzWaves * sizeof(GzLds<kGzTinyWin, kGzTinyIn>), s, P);
     hipLaunchKernelGGL(k_gzip_inflate<kGzSmallWin>, dim3(1280), dim3(64 * kGzWaves),
-                       kGzWaves * sizeof(GzLds<kGzSmallWin>), s, P);
+                       kGzWaves * sizeof(GzLds<kGzSmallWin, kGzIn>), s, P);
     hipLaunchKernelGGL(k_gzip_inflate<kGzLargeWin>, dim3(256), dim3(64 * kGzWaves),
-                       kGzWaves * sizeof(GzLds<kGzLargeWin>), s, P);
+                       kGzWaves * sizeof(GzLds<kGzLargeWin, kGzIn>), s, P);
     hipLaunchKernelGGL(k_gzip_crc, dim3(512), dim3(256), 0, s, P);
     return hipGetLastError();
 }
