@@ -52,8 +52,13 @@ __device__ __forceinline__ uint32_t header_fields_fast(const uint8_t* f, uint64_
 // ---- 16-byte values: unaligned global access (gfx950 unaligned mode), byte shifts -----------
 typedef uint4 __attribute__((aligned(1))) u4u;
 
+// HIP_vector_type's copy operators take 16-aligned references; the access itself is the 1-aligned
+// u4u (one global_load/store_dwordx4 in unaligned mode), which is what -Walign-mismatch flags
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Walign-mismatch"
 __device__ __forceinline__ uint4 ldu16(const uint8_t* p) { return *reinterpret_cast<const u4u*>(p); }
 __device__ __forceinline__ void stu16(uint8_t* p, uint4 v) { *reinterpret_cast<u4u*>(p) = v; }
+#pragma clang diagnostic pop
 // non-temporal (streaming) 16-byte access: bytes touched once should not displace lines the
 // kernel comes back to (the decoder's input lines)
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));

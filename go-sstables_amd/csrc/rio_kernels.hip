@@ -980,7 +980,6 @@ __global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
     const ScanState* st = P.state;
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_NONE) return;
     const uint64_t n = st->n_records;
-    const uint32_t ver = st->version;
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
