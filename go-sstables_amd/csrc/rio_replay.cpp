@@ -3,12 +3,14 @@
 // wal.Replayer.Replay (wal/replayer.go:18-77) walks the WAL directory, sorts the *.wal paths and reads
 // each file to its end through a ReaderI before opening the next one, calling `process` for every
 // record in order. Here worker threads, each with its own rio_ctx (own stream, arenas and pinned
-// staging), map file k+1.. and run the device decode (rio_frame + rio_decode) while the caller is
-// still consuming file k. Decoded files are handed out strictly in list order, at most `depth` of them
-// held ahead, and the staged H2D of one file overlaps the decode and D2H of another. Nothing decodes
-// on the host: a file the device path does not handle shows up as RIO_ERR_UNSUPPORTED in its info and
-// the Go adapter re-reads that file with the reference reader. Files are read into, and records
-// returned in, page-locked host buffers from a process-wide cache (PinnedPool below).
+// staging; contexts pooled across replays, CtxPool below), read file k+1.. and run the device decode
+// (framing + rio_decode) while the caller is still consuming file k. Decoded files are handed out
+// strictly in list order, at most `depth` of them held ahead, and the H2D of one file overlaps the
+// decode and D2H of another. Nothing decodes on the host: a file the device path does not handle shows
+// up as RIO_ERR_UNSUPPORTED in its info and the Go adapter re-reads that file with the reference
+// reader. Files are pread straight into the context's staging pieces (rio::frame_fill); records are
+// returned in page-locked blocks from a process-wide cache (PinnedPool below). The second half of the
+// file is the windowed decode of one large file (rio_stream_*).
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <sys/stat.h>
