@@ -12,7 +12,7 @@
 //     beyond the member's output so far is corrupt.
 // Every failure is the codec-error class (RIO_ERR_DECOMPRESS). Where this path cannot follow the
 // reader it hands the file back: a record holding more than one gzip member (Go's multistream
-// reader would go on reading), or a record announced as <= 2 KiB that decodes past the small
+// reader would go on reading), or a record announced as <= 1 / 2 KiB that decodes past its class's
 // window, ends the sequence with RIO_ERR_UNSUPPORTED and the adapter keeps the reference reader.
 // Bytes decoded past the announced size are never stored; the member then fails its ISIZE check
 // exactly like Go's (gzip.ErrChecksum).
