@@ -761,7 +761,8 @@ def main():
                    "parallelism": f"file-sharded x{world}, no data-path collectives"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": DECODE_KERNEL[comp],
+                     # ref-random records are each one literal: the copy path (k_snappy_literal) decodes them
+                     "kernel": "k_snappy_literal" if (comp == 2 and kind == 0) else DECODE_KERNEL[comp],
                      "kernel_ms": round(decode_ms, 4), "alg_bytes_per_launch": alg_bytes},
         "stages_ms": {"walk": round(stage[0], 4), "scan": round(stage[1], 4), "place": round(stage[2], 4),
                       "decode": round(stage[3], 4)} if len(stage) == 4 else None,
