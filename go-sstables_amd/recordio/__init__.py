@@ -3,8 +3,8 @@
 Reader API (ReaderI / ReadAtI) and constants follow recordio/recordio.go; all decoding runs in the
 HIP kernels of librio.so (go-sstables_amd/csrc). See DESIGN.md and INTEGRATION.md.
 """
-from .errors import (EOF, ErrCorrupt, ErrUnexpectedEOF, GoError, HeaderChecksumMismatchErr,  # noqa: F401
-                     MagicNumberMismatchErr, errors_is, errors_unwrap)
+from .errors import (EOF, ErrCorrupt, ErrUnexpectedEOF, ErrVarintOverflow, GoError,  # noqa: F401
+                     HeaderChecksumMismatchErr, MagicNumberMismatchErr, errors_is, errors_unwrap)
 from .reader import (CompressionTypeGZIP, CompressionTypeLzw, CompressionTypeNone,  # noqa: F401
                      CompressionTypeSnappy, FileHeaderSizeBytes, FileReader, MMapReader, NewFileReader,
                      NewFileReaderWithPath, NewMemoryMappedReaderWithPath)

@@ -212,7 +212,10 @@ class MMapReader(_Reader):
                 return 0, None, EOF
             if rc == L.RIO_ERR_UNSUPPORTED:
                 return 0, None, GoError("unsupported on files with version lower than v2")
-            return 0, None, self._err(rc, offset)
+            if rc == L.RIO_ERR_INVALID_OFFSET:  # mmap_reader.go:70-83: ReadAt's error, unwrapped
+                return 0, None, GoError(f"mmap: invalid ReadAt offset {offset}")
+            # any other error is the failing trial ReadNextAt's, at the trial offset (:105-114)
+            return 0, None, self._err(rc, ro.value)
         if nil.value:
             return ro.value, None, None
         return ro.value, (ctypes.string_at(data.value, n.value) if n.value else b""), None

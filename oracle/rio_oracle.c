@@ -527,6 +527,7 @@ int orc_seek_next(const uint8_t* f, uint64_t len, uint64_t offset, uint64_t seek
                     i = ix;
                     continue;
                 }
+                *rec_offset = trial; /* the failing trial (the reference returns 0 and its error) */
                 return e;
             }
             *rec_offset = trial;

@@ -42,7 +42,8 @@ void orc_file_result_free(orc_file_result* res);
 /* MMapReader.ReadNextAt (mmap_reader.go:130-203 v4, 298-356 v3). *out is malloc'd (NULL for nil). */
 int orc_read_next_at(const uint8_t* f, uint64_t len, uint64_t offset, uint8_t** out,
                      uint64_t* out_len, int* is_nil, uint64_t* detail0, uint64_t* detail1);
-/* MMapReader.SeekNext (mmap_reader.go:58-128) with window seek_len (4096 by default, :370) */
+/* MMapReader.SeekNext (mmap_reader.go:58-128) with window seek_len (4096 by default, :370); on a
+ * trial ReadNextAt error *rec_offset is that trial's offset */
 int orc_seek_next(const uint8_t* f, uint64_t len, uint64_t offset, uint64_t seek_len,
                   uint64_t* rec_offset, uint8_t** out, uint64_t* out_len, int* is_nil);
 /* snappy.Decode of golang/snappy v1.0.0 (decode.go + decode_other.go). *out malloc'd. */

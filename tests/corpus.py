@@ -158,6 +158,21 @@ def cases():
     v3 = v3_file(mixed_records(800, 9), 0)
     out.append(("v3_zero_tail", v3 + bytes(9000)))
     out.append(("v3_trunc", v3[: len(v3) - 7]))
+    # small files damaged in several places (every failure class of ReadNextAt / SeekNext within a
+    # few KiB): a flipped CRC byte, an overflowing size varint, a header longer than 36 bytes, a
+    # truncated header at the end; snappy variant with a corrupt element stream in the middle
+    for comp in (0, 2):
+        recs = [asc(17 * i % 200) for i in range(40)]
+        img, offs = encode_file(recs, comp), []
+        b = bytearray(img)
+        starts = [i for i in range(8, len(b) - 2) if b[i:i + 3] == b"\x91\x8d\x4c"]
+        b[starts[6] + 6] ^= 0x10  # inside record 6's header (its CRC no longer matches)
+        b[starts[14] + 4:starts[14] + 14] = b"\xff" * 10  # record 14: u varint overflows
+        if comp == 2:
+            p0 = starts[22] + len(header_v4(len(recs[22]), 0))
+            b[p0 + 3] = 0x05  # record 22: an element becomes a copy with an offset past its output
+        damaged = bytes(b) + long_h + b"ZZ"
+        out.append((f"damaged_small_c{comp}", damaged + header_v4(3, 0)[:5]))
     # larger synthetic workloads (several chunks / blocks)
     out.append(("text_snappy_1k", generate(3000, 1024, 2, kind=1, seed=1).tobytes()))
     out.append(("random_snappy_1k", generate(2000, 1024, 2, kind=2, seed=2).tobytes()))

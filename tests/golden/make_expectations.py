@@ -16,12 +16,17 @@ ASC_255 = [{"asc": i} for i in range(255)]
 
 
 def common(v):
-    eof_single = 8 + (11 if v == 4 else 6) + 13
+    # mmap_reader_test.go:93-106 (v3: mmap_reader_v3compat_test.go:91-104): EOF right after the
+    # record at 8 + hl + 13; then the magic mismatch read at FileHeaderSizeBytes + (hl - 1) + len(bytes)
+    # where `bytes` is the nil returned by that EOF read, i.e. offset 8 + hl - 1 (18 for v4, 13 for v3:
+    # the last header byte of the record). 8 + hl - 1 + 13 (inside its payload) is checked as well.
+    hl = 11 if v == 4 else 6
+    eof_single = 8 + hl + 13
     d = {
         "recordio_UncompressedSingleRecord": {
             "records": [{"asc": 13}], "end": "EOF",
             "read_at": [[8, {"asc": 13}], [9, "MAGIC"], [42000, "INVALID_OFFSET"],
-                        [eof_single, "EOF"], [eof_single - 1, "MAGIC"]],
+                        [eof_single, "EOF"], [8 + hl - 1, "MAGIC"], [eof_single - 1, "MAGIC"]],
         },
         "recordio_UncompressedWriterMultiRecord_asc": {"records": ASC_255, "end": "EOF"},
         "recordio_SnappyWriterMultiRecord_asc": {"records": ASC_255, "end": "EOF", "compression": 2},

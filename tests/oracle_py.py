@@ -112,7 +112,8 @@ def file_reader_decode_arrays(data) -> dict:
     return res
 
 
-def read_next_at(data: bytes, offset: int):
+def read_next_at(data: bytes, offset: int, details: bool = False):
+    """(status, record) of MMapReader.ReadNextAt; with details=True also (detail0, detail1)."""
     b, n = _buf(data)
     out, ol, nil, d0, d1 = c_void_p(), c_uint64(), c_int(), c_uint64(), c_uint64()
     st = lib().orc_read_next_at(b, n, offset, byref(out), byref(ol), byref(nil), byref(d0), byref(d1))
@@ -121,10 +122,11 @@ def read_next_at(data: bytes, offset: int):
         rec = ctypes.string_at(out.value, ol.value) if ol.value else b""
     if out.value:
         lib().orc_free(out)
-    return st, rec
+    return (st, rec, d0.value, d1.value) if details else (st, rec)
 
 
 def seek_next(data: bytes, offset: int, seek_len: int = 4096):
+    """(status, record offset — the failing trial's on a trial error —, record)"""
     b, n = _buf(data)
     ro, out, ol, nil = c_uint64(), c_void_p(), c_uint64(), c_int()
     st = lib().orc_seek_next(b, n, offset, seek_len, byref(ro), byref(out), byref(ol), byref(nil))

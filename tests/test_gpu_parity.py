@@ -88,8 +88,48 @@ def test_chunk_size_independent(chunk, monkeypatch):
         L.lib().rio_ctx_destroy(h)
 
 
-@pytest.mark.parametrize("name", ["mixed_c0", "mixed_c2", "v3_mixed_snappy", "nil_snappy", "mixed_c2_trunc3"])
+def _handle_read_next_at(r, off):
+    """C-ABI status and details of the reader handle's ReadNextAt (rio_reader_read_next_at)."""
+    import ctypes
+
+    from recordio import _lib as L
+
+    data, n, nil = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_int()
+    rc = L.lib().rio_reader_read_next_at(r._h, off, ctypes.byref(data), ctypes.byref(n), ctypes.byref(nil))
+    d0, d1, eo = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    L.lib().rio_reader_last_detail(r._h, ctypes.byref(d0), ctypes.byref(d1), ctypes.byref(eo))
+    return rc, d0.value, d1.value
+
+
+def _handle_seek_next(r, off):
+    import ctypes
+
+    from recordio import _lib as L
+
+    data, n, nil, ro = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_uint64()
+    rc = L.lib().rio_reader_seek_next(r._h, off, ctypes.byref(ro), ctypes.byref(data), ctypes.byref(n),
+                                      ctypes.byref(nil))
+    return rc, ro.value
+
+
+def _offsets(img, k=150):
+    """Every offset of a small file, else a seeded sample plus the boundaries."""
+    import random
+
+    if len(img) <= 8192:
+        return list(range(len(img) + 3))
+    rng = random.Random(1)
+    return [rng.randint(0, len(img) + 3) for _ in range(k)] + [len(img), len(img) - 1, len(img) + 1, 0, 7, 8]
+
+
+@pytest.mark.parametrize("name", ["mixed_c0", "mixed_c2", "v3_mixed_snappy", "nil_snappy", "mixed_c2_trunc3",
+                                  "mixed_c2_flip", "damaged_small_c0", "damaged_small_c2", "header_too_long",
+                                  "size_overflow", "snappy_corrupt_mid", "huge_u"])
 def test_read_next_at_every_record_start_and_random_offsets(name, tmp_path):
+    """ReadNextAt at record starts and at random offsets: the record, or exactly the oracle's status
+    class (and CRC details), and through the mirror the reference's error value (message, sentinel,
+    wrap depth: mmap_reader.go:130-203)."""
+    from go_errors import assert_go_error, expect_read_next_at
     from recordio import NewMemoryMappedReaderWithPath
 
     img = dict(CASES)[name]
@@ -101,21 +141,30 @@ def test_read_next_at_every_record_start_and_random_offsets(name, tmp_path):
     for off, rec in list(zip(o["rec_off"], o["records"]))[::7]:
         got, err = r.ReadNextAt(off)
         assert err is None and got == rec, off
-    import random
-
-    rng = random.Random(1)
-    for off in [rng.randint(0, len(img) + 3) for _ in range(150)] + [len(img), len(img) - 1, len(img) + 1]:
-        st, want = orc.read_next_at(img, off)
+    n_fail = 0
+    for off in _offsets(img):
+        st, want, d0, d1 = orc.read_next_at(img, off, details=True)
+        rc, g0, g1 = _handle_read_next_at(r, off)
+        assert rc == st, (off, rc, st)
         got, err = r.ReadNextAt(off)
         if st == 0:
             assert err is None and got == want, off
-        else:
-            assert err is not None, (off, st)
+            continue
+        n_fail += 1
+        if st == STATUS["HEADER_CRC"]:
+            assert (g0, g1) == (d0, d1), off
+        assert got is None
+        assert_go_error(err, expect_read_next_at(st, off, str(p), d0, d1))
+    assert n_fail > 0
     r.Close()
 
 
-@pytest.mark.parametrize("name", ["asc_none", "nil_snappy", "v3_mixed_none"])
+@pytest.mark.parametrize("name", ["asc_none", "nil_snappy", "v3_mixed_none", "damaged_small_c0", "damaged_small_c2",
+                                  "snappy_corrupt_mid"])
 def test_seek_next_matches_oracle_on_every_offset(name, tmp_path):
+    """SeekNext from every third offset: the record and its offset, or exactly the oracle's status
+    (with the failing trial's offset), and the reference's error value through the mirror."""
+    from go_errors import assert_go_error, expect_seek_next
     from recordio import NewMemoryMappedReaderWithPath
 
     img = dict(CASES)[name][:6000]
@@ -125,13 +174,18 @@ def test_seek_next_matches_oracle_on_every_offset(name, tmp_path):
     r.Open()
     for seek_len in (4096, 10):
         r.seekLen = seek_len
-        for off in range(0, len(img) + 1, 3):
+        for off in list(range(0, len(img) + 1, 3)) + [len(img) + 1]:
             st, ro, want = orc.seek_next(img, off, seek_len)
+            rc, g_ro = _handle_seek_next(r, off)
+            assert rc == st, (off, seek_len, rc, st)
             g_off, got, err = r.SeekNext(off)
             if st == 0:
                 assert err is None and (g_off, got) == (ro, want), (off, seek_len)
-            else:
-                assert err is not None, (off, st)
+                continue
+            if st not in (STATUS["EOF"], STATUS["INVALID_OFFSET"]):
+                assert g_ro == ro, (off, seek_len)  # the failing trial
+            assert (g_off, got) == (0, None)
+            assert_go_error(err, expect_seek_next(st, off, ro, str(p)))
     r.Close()
 
 
@@ -144,11 +198,12 @@ def test_full_size_headline_workload_exact():
     assert_same_as_oracle(g, o, "C2")
 
 
-def test_full_size_properties_64b_records():
-    """C3 shape (header-bound, 64 B records): counts, sortedness and a checksum of checksums."""
-    img = corpus.generate(2_000_000, 64, 2, kind=1, seed=3)
+def test_full_size_c3_10m_64b_records_exact():
+    """C3 at full size (10M x 64 B snappy text-like, seed 3 as bench.py): sortedness and sizes, then
+    every byte and offset against the oracle."""
+    img = corpus.generate(10_000_000, 64, 2, kind=1, seed=3)
     g = gpu_decode_arrays(img)
-    assert g["status"] == STATUS["EOF"] and g["n_records"] == 2_000_000
+    assert g["status"] == STATUS["EOF"] and g["n_records"] == 10_000_000
     assert np.all(np.diff(g["rec_off"]) > 0) and np.all(np.diff(g["out_off"]) == 64)
     o = orc.file_reader_decode_arrays(img)
-    assert_same_as_oracle(g, o, "C3-2M")
+    assert_same_as_oracle(g, o, "C3-10M")

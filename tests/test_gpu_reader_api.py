@@ -188,7 +188,10 @@ def test_mmap_small_varint_header_eof(vd):  # :93-106
     r = mm(vd, "recordio_UncompressedSingleRecord")
     b, err = r.ReadNextAt(FileHeaderSizeBytes + hl + 13)
     assert b is None and err is EOF
-    b, err = r.ReadNextAt(FileHeaderSizeBytes + hl - 1 + 13)
+    # the reference's `bytes` is the nil of the EOF read above, so len(bytes) = 0: offset 18 (v4) / 13 (v3)
+    b, err = r.ReadNextAt(FileHeaderSizeBytes + hl - 1 + len(b or b""))
+    assert b is None and str(errors_unwrap(err)) == "magic number mismatch"
+    b, err = r.ReadNextAt(FileHeaderSizeBytes + hl - 1 + 13)  # inside the payload: also a mismatch
     assert b is None and str(errors_unwrap(err)) == "magic number mismatch"
 
 
