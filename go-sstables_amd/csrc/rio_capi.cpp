@@ -163,7 +163,8 @@ struct rio_ctx {
         ev_cursor = 0;
     }
     // framing arenas
-    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, sink, chunks, block_runs, chunk_excl, place, block_excl, state, info;
+    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, sink, fail_lanes, chunks, block_runs, chunk_excl, place,
+        block_excl, state, info;
     // host-API arenas
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
     // rio_sst_open: parsed index fields (4 x n), per-entry CRC-64, kernel results
@@ -203,7 +204,9 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     HIP_TRY(ctx->state.ensure(sizeof(ScanState)));
     HIP_TRY(ctx->info.ensure(sizeof(rio_file_info)));
     HIP_TRY(ctx->sink.ensure(kSinkBytes));
+    HIP_TRY(ctx->fail_lanes.ensure(2 * kFailLanes * sizeof(uint64_t)));
     P.sink = ctx->sink.as<uint8_t>();
+    P.fail_lanes = ctx->fail_lanes.as<uint64_t>();
     P.scratch_off = ctx->scratch_off.as<uint64_t>();
     P.scratch_len = ctx->scratch_len.as<uint64_t>();
     P.scratch_pay = ctx->scratch_pay.as<uint64_t>();
@@ -248,7 +251,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->rec_desc, &c->sink, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
+    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->rec_desc, &c->sink, &c->fail_lanes, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
                       &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
                       &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res, &c->enc_scr, &c->enc_scr_off, &c->enc_clen, &c->enc_tab,
                       &c->enc_hdr, &c->enc_size, &c->enc_tmp, &c->enc_cub, &c->enc_rec, &c->enc_rec_off, &c->enc_flags, &c->enc_out,
@@ -782,6 +785,14 @@ extern "C" int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_
     if ((rc = view_advance(r, have))) return rc;
     if (!have) return terminal(r);
     const uint64_t i = r->cursor++;
+    // a record whose payload does not decompress: ReadNext returns the codec error (or gzip's bare
+    // io.EOF for an empty payload) and the next call goes on with the record after it
+    if (r->w_flags[i] & (RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) {
+        r->det0 = r->det1 = 0;
+        r->err_off = r->info.status_offset;
+        // gzip's io.EOF comes back unwrapped (file_reader.go:119-121): the bare-EOF status class
+        return (r->w_flags[i] & RIO_FLAG_EOF) ? RIO_EOF_ZERO_TAIL : RIO_ERR_DECOMPRESS;
+    }
     if (data) *data = r->w_out + r->w_off[i];
     if (len) *len = r->w_off[i + 1] - r->w_off[i];
     if (is_nil) *is_nil = (r->w_flags[i] & RIO_FLAG_NIL) ? 1 : 0;
@@ -808,8 +819,7 @@ extern "C" int rio_reader_skip_next(rio_reader* r) {
     switch (s) {
     case RIO_EOF_ZERO_TAIL: return RIO_ERR_MAGIC;  // SkipNext does not test for a zero tail
     case RIO_EOF_PAYLOAD:
-    case RIO_ERR_UNEXPECTED_EOF:
-    case RIO_ERR_DECOMPRESS:  // header parsed fine: SkipNext seeks past the payload
+    case RIO_ERR_UNEXPECTED_EOF:  // header parsed fine: SkipNext seeks past the payload
         r->past_end = true;
         return RIO_OK;
     default: return s;
@@ -1022,6 +1032,12 @@ extern "C" int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, 
         if (value_len) *value_len = 0;
         if (is_nil) *is_nil = 0;
         return t->info.data.status == RIO_OK ? RIO_EOF : t->info.data.status;
+    }
+    if (t->data_flags[i] & (RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) {  // the scan's ReadNext error for this value
+        if (value) *value = nullptr;
+        if (value_len) *value_len = 0;
+        if (is_nil) *is_nil = 0;
+        return (t->data_flags[i] & RIO_FLAG_EOF) ? RIO_EOF_ZERO_TAIL : RIO_ERR_DECOMPRESS;
     }
     const bool nil = (t->data_flags[i] & RIO_FLAG_NIL) != 0;
     if (value) *value = nil ? nullptr : t->data.data() + t->data_off[i];

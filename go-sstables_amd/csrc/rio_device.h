@@ -8,7 +8,13 @@
 namespace rio {
 
 constexpr uint64_t kNone = ~0ull;       // "no speculative entry found in this chunk"
-constexpr uint64_t kNilBit = 1ull << 63;  // scratch out_len | kNilBit => nil record
+// scratch_len: decoded length | flag bits
+constexpr uint64_t kNilBit = 1ull << 63;  // nil record
+constexpr uint64_t kBadBit = 1ull << 62;  // payload fails already at framing (codec preamble / size)
+constexpr uint64_t kEofBit = 1ull << 61;  // gzip: empty payload (gzip.NewReader's io.EOF)
+constexpr uint64_t kLenMask = kEofBit - 1;
+// lanes of the Snappy lane decoder that met a corrupt record are listed for k_snappy_verify
+constexpr uint32_t kFailLanes = 1024;
 
 // Snappy decode launch shape (k_snappy_pipe): every wave owns one 64-byte sink line that absorbs
 // the pipeline's placeholder loads and stores.
@@ -62,7 +68,10 @@ struct ScanState {
     uint64_t det0, det1;
     uint64_t zero_from;     // zero-tail check range start (kNone = no check)
     uint64_t n_repairs;
-    uint64_t decode_err_rec;  // min 2 * record + (1: cannot be placed -> unsupported) that failed (kNone = none)
+    uint64_t first_bad;        // first record flagged RIO_FLAG_CORRUPT / RIO_FLAG_EOF (kNone = none)
+    uint64_t n_bad;            // records so flagged
+    uint64_t unsupported_rec;  // first record the device path hands back (gzip: several members)
+    uint32_t n_fail_lanes;     // Snappy lane-decoder lanes listed in fail_lanes (> kFailLanes: all)
     uint32_t capacity_fail;
     uint32_t huge_streams;  // a record stream exceeds 32-bit positions: k_snappy_global runs
     uint32_t any_mixed;     // snappy: some record is not one literal covering its output (k_place);
@@ -97,6 +106,7 @@ struct FrameParams {
     // element stream (lo, hi), z = stream length, w = decoded length
     uint4* rec_desc;
     uint8_t* sink;           // [kSinkBytes] placeholder-store target of the Snappy decode pipeline
+    uint64_t* fail_lanes;    // [2 * kFailLanes] record ranges [r0, r1) of lanes that met a corrupt record
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)
     RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix
@@ -135,5 +145,15 @@ struct EncParams {
     uint64_t* out_len;         // [1] file length
     uint32_t lds_small;        // records <= 1 KiB on the LDS-table kernel
 };
+
+#ifdef __HIPCC__
+// A record whose payload does not decode: flag it for ReadNext (RIO_FLAG_CORRUPT) and count it.
+// Only the thread that decoded record i writes its flag byte.
+__device__ inline void mark_bad(const FrameParams& P, uint64_t i, uint8_t flag = RIO_FLAG_CORRUPT) {
+    P.flags[i] = (uint8_t)(P.flags[i] | flag);
+    atomicMin((unsigned long long*)&P.state->first_bad, (unsigned long long)i);
+    atomicAdd((unsigned long long*)&P.state->n_bad, 1ull);
+}
+#endif
 
 }  // namespace rio

@@ -449,10 +449,14 @@ __device__ __forceinline__ bool gzip_active(const FrameParams& P, const ScanStat
     return st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_GZIP;
 }
 
+// a record that does not inflate is flagged (ReadNext returns the gzip reader's error for it and goes
+// on); one the device does not handle (several members) ends the sequence for the reference reader
 __device__ __forceinline__ void gz_fail(const FrameParams& P, uint64_t i, int rc) {
     P.rec_pay[i] |= kPayFail;
-    atomicMin((unsigned long long*)&P.state->decode_err_rec,
-              (unsigned long long)(2 * i + (rc == kGzUnsupported ? 1u : 0u)));
+    if (rc == kGzUnsupported)
+        atomicMin((unsigned long long*)&P.state->unsupported_rec, (unsigned long long)i);
+    else
+        mark_bad(P, i);
 }
 }  // namespace
 
@@ -476,7 +480,7 @@ __global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(
     const uint64_t n = st->n_records;
     const uint64_t waves = (uint64_t)gridDim.x * kGzWaves;
     for (uint64_t i = (uint64_t)blockIdx.x * kGzWaves + wv; i < n; i += waves) {
-        if (P.flags[i] & RIO_FLAG_NIL) continue;
+        if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;  // nil / failed at framing
         const uint64_t o0 = P.out_off[i], dlen = P.out_off[i + 1] - o0;
         // size classes: (0, 1 KiB], (1 KiB, 2 KiB] held whole in LDS, larger ones through the DEFLATE window
         const uint32_t cls = dlen <= kGzTinyWin ? kGzTinyWin : dlen <= kGzSmallWin ? kGzSmallWin : kGzLargeWin;
@@ -507,7 +511,7 @@ __global__ void __launch_bounds__(256) k_gzip_crc(FrameParams P) {
     const uint64_t n = st->n_records;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (P.flags[i] & RIO_FLAG_NIL) continue;
+        if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
         const uint64_t pay = P.rec_pay[i];
         if (pay & kPayFail) continue;
         const uint64_t slen = (pay & ~kPayFail) >> 8;
@@ -525,8 +529,7 @@ __global__ void __launch_bounds__(256) k_gzip_crc(FrameParams P) {
             for (int j = 0; j < 16; j++) c = tab[(c ^ (w[j >> 2] >> (8 * (j & 3)))) & 0xFFu] ^ (c >> 8);
         }
         for (; k < len; k++) c = tab[(c ^ o[k]) & 0xFFu] ^ (c >> 8);
-        if ((c ^ 0xFFFFFFFFu) != want)
-            atomicMin((unsigned long long*)&P.state->decode_err_rec, (unsigned long long)(2 * i));
+        if ((c ^ 0xFFFFFFFFu) != want) mark_bad(P, i);  // gzip.ErrChecksum
     }
 }
 

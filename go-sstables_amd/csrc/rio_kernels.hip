@@ -205,9 +205,13 @@ __device__ void crc32c_tab_init(uint32_t* T) {
 // Common records (canonical magic, header + preamble inside 32 bytes, valid) are parsed from two
 // 16-byte loads; everything else (and every failure, for its exact classification) takes the
 // byte-wise ReadUvarint restatement.
+// A payload whose codec preamble / size already fails (snappy: unusable preamble; gzip: empty, too
+// short, or an ISIZE no DEFLATE stream reaches) frames normally: FileReader consumed it, and its
+// ReadNext fails without ending the file. `lflags` then carries kBadBit / kEofBit and out_len 0.
 __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t ver, uint32_t comp,
-                            Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay,
+                            Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay, uint64_t& lflags,
                             const uint32_t* crct = nullptr) {
+    lflags = 0;
     if (p + 32 <= len) {
         const uint4 a = ldu16(f + p), b = ldu16(f + p + 16);
         const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -279,32 +283,42 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
     uint64_t avail = len - p - h.hdr_len;
     if (plen > avail) return avail == 0 ? RIO_EOF_PAYLOAD : RIO_ERR_UNEXPECTED_EOF;
     uint64_t k = 0;
+    next = p + h.hdr_len + plen;
     if (comp == RIO_COMP_SNAPPY) {
         uint64_t d = 0;
         const int kk = uvarint_buf(f + p + h.hdr_len, plen, d);
         // snappy decodedLen: n<=0 or > 0xffffffff => ErrCorrupt; a preamble above 22x the element
         // bytes cannot be produced (max 64 output bytes per 3-byte tagCopy2) => ErrCorrupt later.
-        if (kk <= 0 || d > 0xFFFFFFFFull || d > 22ull * (plen - (uint64_t)kk) + 64) return RIO_ERR_DECOMPRESS;
+        if (kk <= 0 || d > 0xFFFFFFFFull || d > 22ull * (plen - (uint64_t)kk) + 64) {
+            out_len = 0;
+            pay = h.hdr_len;
+            lflags = kBadBit;
+            return RIO_OK;
+        }
         out_len = d;
         k = (uint64_t)kk;
     } else if (comp == RIO_COMP_GZIP) {
         // gzip.NewReader on an empty payload returns a bare io.EOF, which ReadNext passes through
         // unwrapped (file_reader.go:118-121, gzip_compression.go:56-59)
-        if (plen == 0) return RIO_EOF_PAYLOAD;
         // decoded size = ISIZE, the payload's last four bytes (trailer of its only member; more
-        // members -> RIO_ERR_UNSUPPORTED at decode). Above DEFLATE's maximum ratio (258 bytes per
-        // 2 bits) no valid stream ends this way: the reader fails on it => codec error here.
+        // members -> RIO_ERR_UNSUPPORTED at decode). A member is at least 18 bytes, and above
+        // DEFLATE's maximum ratio (258 bytes per 2 bits) no valid stream ends this way: the reader
+        // fails on either.
         uint64_t isz = 0;
         if (plen >= 18) {
             const uint8_t* t = f + p + h.hdr_len + plen - 4;
             isz = t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
-            if (isz > 1032ull * plen + 64) return RIO_ERR_DECOMPRESS;
+        }
+        if (plen == 0 || plen < 18 || isz > 1032ull * plen + 64) {
+            out_len = 0;
+            pay = h.hdr_len;
+            lflags = plen == 0 ? kEofBit : kBadBit;
+            return RIO_OK;
         }
         out_len = isz;
     } else {
         out_len = plen;
     }
-    next = p + h.hdr_len + plen;
     pay = ((plen - k) << 8) | (h.hdr_len + k);
     return RIO_OK;
 }
@@ -324,7 +338,10 @@ __global__ void k_header(FrameParams P) {
     st->zero_from = kNone;
     st->zero_nonzero = 0;
     st->n_repairs = 0;
-    st->decode_err_rec = kNone;
+    st->first_bad = kNone;
+    st->n_bad = 0;
+    st->unsupported_rec = kNone;
+    st->n_fail_lanes = 0;
     st->capacity_fail = 0;
     st->huge_streams = 0;
     st->any_mixed = 0;
@@ -380,8 +397,8 @@ __device__ uint64_t find_entry(const FrameParams& P, uint64_t cs, uint64_t ce, u
                 if (p < cs || p >= ce || p + 2 >= P.len) continue;
                 if (f[p + 1] != 0x8D || f[p + 2] != 0x4C) continue;
                 Hdr h;
-                uint64_t nx, ol, pd;
-                if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd) == RIO_OK) return p;
+                uint64_t nx, ol, pd, lf;
+                if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd, lf) == RIO_OK) return p;
             }
         }
     }
@@ -397,8 +414,8 @@ __device__ void walk_from(const FrameParams& P, uint64_t c, uint64_t p, uint32_t
     uint64_t* sp = P.scratch_pay + c * P.slots;
     while (p < ce) {
         Hdr h;
-        uint64_t next = 0, olen = 0, pd = 0;
-        int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd);
+        uint64_t next = 0, olen = 0, pd = 0, lf = 0;
+        int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd, lf);
         if (e) {
             s.status = e;
             s.err_off = p;
@@ -414,7 +431,7 @@ __device__ void walk_from(const FrameParams& P, uint64_t c, uint64_t p, uint32_t
         }
         if (s.count < P.slots) {
             so[s.count] = p;
-            sl[s.count] = olen | (h.nil ? kNilBit : 0);
+            sl[s.count] = olen | lf | (h.nil ? kNilBit : 0);
             sp[s.count] = pd;
         }
         s.count++;
@@ -601,9 +618,9 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         const uint64_t cpos = have ? L.pos[lane] : kNone;
         Hdr h;
         h.nil = false;
-        uint64_t nx = 0, ol = 0, pd = 0;
+        uint64_t nx = 0, ol = 0, pd = 0, lf = 0;
         int e = RIO_ERR_MAGIC;
-        if (have) e = frame_record(f, P.len, cpos, ver, comp, h, nx, ol, pd, crct);
+        if (have) e = frame_record(f, P.len, cpos, ver, comp, h, nx, ol, pd, lf, crct);
         const bool ok = have && e == RIO_OK;
         const uint64_t ok_mask = __ballot(ok);
         const uint64_t succ_pos = __shfl_down(cpos, 1);  // next candidate's position
@@ -640,7 +657,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         const uint64_t mylen = slot != ~0u ? ol : 0;
         if (slot != ~0u && slot < P.slots) {
             so[slot] = cpos;
-            sl[slot] = ol | (h.nil ? kNilBit : 0);
+            sl[slot] = ol | lf | (h.nil ? kNilBit : 0);
             sp[slot] = pd;
         }
         bytes += __shfl(wave_excl_scan(mylen, lane) + mylen, 63);
@@ -914,7 +931,7 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     for (uint64_t k0 = 0; k0 < pl.owned; k0 += 64) {
         const uint64_t k = k0 + lane;
         const bool v = k < pl.owned;
-        const uint64_t l = v ? sl[k] : 0, len = l & ~kNilBit;
+        const uint64_t l = v ? sl[k] : 0, len = l & kLenMask;
         const uint64_t excl = wave_excl_scan(len, lane);
         if (v) {
             const uint64_t i = pl.base_idx + k;
@@ -922,12 +939,18 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
             P.rec_off[i] = ro;
             P.rec_pay[i] = pay;
             P.out_off[i] = carry + excl;
-            P.flags[i] = (l & kNilBit) ? RIO_FLAG_NIL : 0;
+            const uint8_t fl = ((l & kNilBit) ? RIO_FLAG_NIL : 0) | ((l & kBadBit) ? RIO_FLAG_CORRUPT : 0) |
+                               ((l & kEofBit) ? RIO_FLAG_EOF : 0);
+            P.flags[i] = fl;
+            if (fl & (RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) {  // failed at framing (stream length 0)
+                atomicMin((unsigned long long*)&P.state->first_bad, (unsigned long long)i);
+                atomicAdd((unsigned long long*)&P.state->n_bad, 1ull);
+            }
             P.rec_desc[i] = make_uint4((uint32_t)start, (uint32_t)(start >> 32), (uint32_t)slen, (uint32_t)len);
             if ((slen | len) > 0xFFFFFFFFull) atomicOr(&P.state->huge_streams, 1u);
             // a snappy stream that is exactly one literal element of the record's whole length
             // (what golang/snappy emits for incompressible input) decodes as a copy
-            if (snappy && !(l & kNilBit)) mixed |= !snappy_single_literal(P.file + start, slen, len);
+            if (snappy && fl == 0) mixed |= !snappy_single_literal(P.file + start, slen, len);
         }
         carry += __shfl(excl + len, 63);
     }
@@ -1037,6 +1060,8 @@ __global__ void k_finalize(FrameParams P) {
     info.n_repairs = st->n_repairs;
     info.detail0 = 0;
     info.detail1 = 0;
+    info.first_bad = kNone;
+    info.n_bad = 0;
     if (st->hdr_status != RIO_OK) {
         info.n_records = 0;
         info.total_out_bytes = 0;
@@ -1056,15 +1081,24 @@ __global__ void k_finalize(FrameParams P) {
         info.status = RIO_EOF_ZERO_TAIL;
         info.detail0 = 0;
     }
+    info.first_bad = kNone;
+    info.n_bad = 0;
     if (st->capacity_fail) {
         info.status = RIO_ERR_CAPACITY;
-    } else if (st->decode_err_rec != kNone && (st->decode_err_rec >> 1) < st->n_records) {
-        const uint64_t r = st->decode_err_rec >> 1;
-        info.n_records = r;
-        info.total_out_bytes = P.out_off[r];
-        info.status = (st->decode_err_rec & 1) ? RIO_ERR_UNSUPPORTED : RIO_ERR_DECOMPRESS;
-        info.status_offset = P.rec_off[r];
-        info.detail0 = info.detail1 = 0;
+    } else {
+        // a record the device path hands back ends the sequence there (the adapter re-reads the file)
+        const uint64_t u = st->unsupported_rec;
+        if (u != kNone && u < st->n_records) {
+            info.n_records = u;
+            info.total_out_bytes = P.out_off[u];
+            info.status = RIO_ERR_UNSUPPORTED;
+            info.status_offset = P.rec_off[u];
+            info.detail0 = info.detail1 = 0;
+        }
+        if (st->first_bad < info.n_records) {
+            info.first_bad = st->first_bad;
+            info.n_bad = st->n_bad;  // (records past a hand-back point never reach this kernel's view)
+        }
     }
     *P.info = info;
 }

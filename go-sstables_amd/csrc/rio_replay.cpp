@@ -362,7 +362,8 @@ extern "C" void rio_replay_free(rio_replay* r) {
 //   * raised at p = s_k (no record completed): a truncation-type status (the EOF family,
 //     io.ErrUnexpectedEOF; the zero-tail test reads to the end of the file) doubles the window;
 //     any other status depends only on bytes inside the window and is the file's.
-// A record that fails to decompress ends the file at that window whatever the cut. The driver
+// A record that fails to decompress is flagged in whichever window holds it (its bytes are inside
+// the window, so the cut cannot change the codec's verdict); first_bad is a file record index. The driver
 // thread reads and frames window k+1 on one context while a worker runs window k's decode and D2H
 // on the other, so the file's H2D overlaps its D2H. Records, offsets and statuses are those of the
 // whole-file decode: rec_off and status_offset are file offsets, out_off is window-relative.
@@ -480,8 +481,9 @@ struct rio_stream {
             rio_file_info& fi = w->d.info;
             const uint64_t shift = j.s - RIO_FILE_HEADER_BYTES;  // window offset -> file offset
             for (uint64_t i = 0; !w->d.rc && shift && i < fi.n_records; i++) w->d.rec_off[i] += shift;
-            // a record the decode rejects (does not decompress, cannot be placed) ends the file
-            // here, whatever the cut
+            if (fi.n_bad) fi.first_bad += j.first_record;  // a file record index, like first_record
+            // a record the decode hands back (RIO_ERR_UNSUPPORTED truncates the window) ends the
+            // file here, whatever the cut; one that does not decompress is only flagged
             w->terminal = j.terminal || w->d.rc || fi.n_records < j.fi.n_records || fi.status != j.fi.status;
             if (w->terminal) {
                 fi.status_offset += shift;

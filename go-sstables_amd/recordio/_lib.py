@@ -41,6 +41,8 @@ RIO_ERR_PROTO = 21
 EOF_CLASS = (RIO_EOF, RIO_EOF_ZERO_TAIL, RIO_EOF_HEADER, RIO_EOF_PAYLOAD)
 
 RIO_FLAG_NIL = 1
+RIO_FLAG_CORRUPT = 2
+RIO_FLAG_EOF = 4
 RIO_DEVICE_PAD = 64
 COMP_NONE, COMP_GZIP, COMP_SNAPPY, COMP_LZW = 0, 1, 2, 3
 
@@ -58,6 +60,8 @@ class FileInfo(ctypes.Structure):
         ("detail1", c_uint64),
         ("n_chunks", c_uint64),
         ("n_repairs", c_uint64),
+        ("first_bad", c_uint64),
+        ("n_bad", c_uint64),
     ]
 
     def as_dict(self):

@@ -18,7 +18,7 @@ import os
 from dataclasses import dataclass
 
 from recordio import _lib as L
-from recordio.errors import GoError
+from recordio.errors import EOF, ErrCorrupt, GoError, wrap
 
 from . import proto
 from .disk_index import DiskIndexLoader, DiskKeyIndex, IndexVal  # noqa: F401
@@ -118,8 +118,18 @@ class _DeviceTable:
                 raise UnsupportedError(f"{what} file of '{base}' is not decoded on the device (recordio v"
                                        f"{info['version']}, compression {info['compression']})")
         self.index_info, self.data_info = ii, di
-        n = self.n_index = ii["n_records"]
+        n = ii["n_records"]
+        # an index record that does not decompress: Load's ReadNext fails there, or ends the index
+        # for gzip's bare io.EOF (slice_key_index.go:117-126)
+        self.index_bad = _NONE
+        if ii["n_bad"]:
+            if int(self.ib.flags[ii["first_bad"]].item()) & L.RIO_FLAG_CORRUPT:
+                self.index_bad = ii["first_bad"]
+            n = ii["first_bad"]
+        self.n_index = n
         self.n_data = di["n_records"]
+        # first entry whose value does not decompress (entry i = data record i in the writer's layout)
+        self.value_bad = di["first_bad"] if di["n_bad"] and di["first_bad"] < n else _NONE
         self.key_off = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         self.key_len = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         self.value_off = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
@@ -161,6 +171,14 @@ class _DeviceTable:
             return None
         return self.h_data[self.h_data_off[j]:self.h_data_off[j + 1]]
 
+    def value_failed(self, j) -> bool:
+        """Data record j does not decompress (RIO_FLAG_CORRUPT / RIO_FLAG_EOF)."""
+        return bool(self.h_data_flags[j] & (L.RIO_FLAG_CORRUPT | L.RIO_FLAG_EOF))
+
+    def codec_error(self, j):
+        """The reader's error for data record j: snappy/gzip's error, or gzip's bare io.EOF."""
+        return EOF if self.h_data_flags[j] & L.RIO_FLAG_EOF else ErrCorrupt
+
 
 class SSTableReader:
     def __init__(self, opts: _Opts, meta: proto.MetaData, table: _DeviceTable):
@@ -181,6 +199,10 @@ class SSTableReader:
     def _value_at(self, i, skip_check):
         """getValueAtOffset (sstable_reader.go:80-117) for index entry i (the writer's layout)."""
         t = self.t
+        if t.value_failed(i):  # dataReader.ReadNextAt's error (mmap_reader.go:186-191), wrapped at :90-94
+            vo, path = t.h_value_off[i], os.path.join(self.opts.basePath, DataFileName)
+            inner = wrap(f"failed decompressing record at offset {vo} in mmap reader for '{path}'", t.codec_error(i))
+            return None, wrap(f"error in sstable '{self.opts.basePath}' while getting value at offset {vo}", inner)
         v = t.value(i)
         if skip_check:
             return v, None
@@ -231,6 +253,8 @@ class _FullScanIterator:
         if i >= t.n_data:  # dataReader.ReadNext error (end of data file before end of index)
             return None, None, GoError(f"data file of '{self.r.opts.basePath}' ended at record {i}: "
                                        f"{L.strerror(t.data_info['status'])}")
+        if t.value_failed(i):  # dataReader.ReadNext's codec error, returned as is (sstable_iterator.go:87-90)
+            return None, None, t.codec_error(i)
         v = t.value(i)
         if self.skip:
             return key, v, None
@@ -259,14 +283,19 @@ def NewSSTableReader(*options):  # noqa: N802
     if t.index_info["status"] not in L.EOF_CLASS:
         return None, GoError(f"error while reading index of sstable in '{o.basePath}': "
                              f"{L.strerror(t.index_info['status'])}")
+    if t.index_bad != _NONE and (t.bad_proto == _NONE or t.index_bad <= t.bad_proto):
+        ip = os.path.join(o.basePath, IndexFileName)
+        return None, wrap(f"error while reading index records of sstable in '{ip}'", ErrCorrupt)
     if t.bad_proto != _NONE:
         return None, GoError(f"error while reading index of sstable in '{o.basePath}': proto: cannot parse "
                              f"invalid wire-format data (record {t.bad_proto})")
     if t.unplaced != _NONE:
         return None, UnsupportedError(f"sstable '{o.basePath}': index entry {t.unplaced} is not in the writer's layout")
     r = SSTableReader(o, meta, t)
-    if not o.skipHashCheckOnLoad and t.bad_crc != _NONE:
-        i = t.bad_crc
+    if not o.skipHashCheckOnLoad and (t.bad_crc != _NONE or t.value_bad != _NONE):
+        # validateDataFile stops at the first entry whose value fails to read or to hash; a value
+        # that does not decompress has no meaningful CRC, so on a tie it is the read error
+        i = min(t.bad_crc, t.value_bad)
         _, e = r._value_at(i, False)
         return None, GoError(f"validateDataFile error loading value '{o.basePath}' at key "
                              f"[{_fmt_key(t.key(i))}]: {e}", wrapped=e)

@@ -175,9 +175,11 @@ class Replayer:
                     # the adapter re-reads such a file with the reference reader before delivering
                     # any of its records; this mirror has none, so it stops here
                     return wrap(f"error while reading WAL records under '{path}'", ErrUnsupported)
-                err = self._deliver(info, out.value, off.value, flags.value, path, process)
+                err, stopped = self._deliver(info, out.value, off.value, flags.value, path, process)
                 if err is not None:
                     return err
+                if stopped:  # gzip's bare io.EOF for an empty payload ends this file (replayer.go:60-63)
+                    continue
                 if st not in _EOF_CLASS:
                     err = read_next_error(st, path, info.detail0, info.detail1)
                     if not errors_is(err, EOF):
@@ -187,20 +189,28 @@ class Replayer:
 
     @staticmethod
     def _deliver(info, out_p, off_p, flags_p, path, process):
+        """process() every record up to the first one that does not decompress: its ReadNext error
+        ends the replay (snappy / gzip error) or, for gzip's bare io.EOF, this file. -> (err, stopped)"""
         n = info.n_records
         if n == 0:
-            return None
+            return None, False
         offs = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(off_p)).tolist()
         fl = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(flags_p))
         arena = ctypes.string_at(out_p, offs[n]) if offs[n] else b""
         nil = (fl & L.RIO_FLAG_NIL).nonzero()[0].tolist() if fl.any() else []
         nil_set = set(nil)
-        for i in range(n):
+        bad = info.first_bad if info.n_bad else n
+        for i in range(min(n, bad)):
             rec = None if i in nil_set else arena[offs[i]:offs[i + 1]]
             err = process(rec)
             if err is not None:
-                return wrap(f"error while processing WAL record under '{path}'", err)
-        return None
+                return wrap(f"error while processing WAL record under '{path}'", err), False
+        if bad < n:
+            if fl[bad] & L.RIO_FLAG_EOF:
+                return None, True
+            return wrap(f"error while reading WAL records under '{path}'",
+                        read_next_error(L.RIO_ERR_DECOMPRESS, path, 0, 0)), False
+        return None, False
 
 
 def NewReplayer(opts: Options):  # noqa: N802

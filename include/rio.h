@@ -59,8 +59,9 @@ typedef enum rio_status {
     /* header read hit EOF before its first byte: FileReader wraps io.EOF once
      * (file_reader.go:93), MMapReader.ReadNextAt returns a bare io.EOF (mmap_reader.go:153-155) */
     RIO_EOF = 1,
-    /* FileReader only: magic mismatch and every byte after the consumed magic varint is zero
-     * (DirectIO padding) -> bare io.EOF (file_reader.go:76-91) */
+    /* FileReader only: a bare io.EOF. Magic mismatch and every byte after the consumed magic varint
+     * is zero (DirectIO padding, file_reader.go:76-91); or, from rio_reader_read_next / rio_sst_entry,
+     * a RIO_FLAG_EOF record (gzip's io.EOF passed through unwrapped, :119-121) */
     RIO_EOF_ZERO_TAIL = 2,
     /* io.EOF on the first byte of a later header field (nil byte / u / c / crc varint) */
     RIO_EOF_HEADER = 3,
@@ -97,6 +98,12 @@ const char* rio_build_info(void);
 /* Sequential semantics: `n_records` records are delivered in file order, then `status`.       */
 /* A clean end is one of the RIO_EOF family. Records with index < n_records are valid even if   */
 /* status is an error: the reference's ReadNext loop returns them before the error.            */
+/* A record whose payload fails to decompress does not end the sequence: FileReader.ReadNext     */
+/* returns the codec error for it and the next call reads the record after it (the payload was   */
+/* consumed, file_reader.go:101-125), so such a record is delivered with RIO_FLAG_CORRUPT (or    */
+/* RIO_FLAG_EOF for gzip's empty payload) and the records after it are decoded. Its slice of     */
+/* `out` has the length its payload announced (snappy preamble, gzip ISIZE; 0 when that is       */
+/* unusable) and unspecified bytes. first_bad / n_bad summarise the flagged records.             */
 /* ------------------------------------------------------------------------------------------ */
 typedef struct rio_file_info {
     uint32_t version;         /* file header version (1..4) */
@@ -110,10 +117,16 @@ typedef struct rio_file_info {
     uint64_t detail1;         /* HEADER_CRC: actual crc */
     uint64_t n_chunks;        /* framing chunks used (diagnostic) */
     uint64_t n_repairs;       /* chunks whose speculative entry had to be re-walked (diagnostic) */
+    uint64_t first_bad;       /* first record flagged RIO_FLAG_CORRUPT / RIO_FLAG_EOF (~0: none) */
+    uint64_t n_bad;           /* records so flagged (< n_records) */
 } rio_file_info;
 
 /* Per-record flag bits (rio_decode `flags`) */
-#define RIO_FLAG_NIL 0x1u /* record written as nil: ReadNext returns nil, not []byte{} */
+#define RIO_FLAG_NIL 0x1u     /* record written as nil: ReadNext returns nil, not []byte{} */
+#define RIO_FLAG_CORRUPT 0x2u /* the payload does not decompress: ReadNext returns the codec error
+                                 (snappy ErrCorrupt / the gzip reader's error) for this record */
+#define RIO_FLAG_EOF 0x4u     /* gzip: empty payload, gzip.NewReader's bare io.EOF for this record
+                                 (gzip_compression.go:56-59, passed through by file_reader.go:118-121) */
 
 /* ------------------------------------------------------------------------------------------ */
 /* Context: one HIP device + stream + device arenas + pinned staging. NOT thread-safe: use one  */
@@ -132,8 +145,8 @@ int rio_device_count(int* out);
  *   out      [>= info->total_out_bytes]  concatenated record bytes
  *   out_off  [n_records + 1]             record i = out[out_off[i] .. out_off[i+1])
  *   rec_off  [n_records]                 file offset of record i's header (ReadNextAt offset)
- *   flags    [n_records]                 RIO_FLAG_NIL
- * rio_decode may lower info->n_records (a record that fails to decompress ends the sequence). */
+ *   flags    [n_records]                 RIO_FLAG_NIL / RIO_FLAG_CORRUPT / RIO_FLAG_EOF
+ * rio_decode fills info->first_bad / n_bad (records that fail to decompress are flagged, not cut). */
 int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_file_info* info);
 int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, uint64_t* rec_off,
                uint8_t* flags, uint64_t rec_cap, rio_file_info* info);
@@ -186,7 +199,10 @@ int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_
  * handle is returned and `info` says which of the reference's load errors applies: index/data status
  * outside the EOF family (reading error), first_bad_proto (proto.Unmarshal error, slice_key_index.go:
  * 107-110), first_unplaced (not the writer's layout: keep the reference reader), first_bad_crc
- * (validateDataFile's ChecksumError, sstable_reader.go:205-238, unless SkipHashCheckOnLoad). */
+ * (validateDataFile's ChecksumError, sstable_reader.go:205-238, unless SkipHashCheckOnLoad), and
+ * data.first_bad (a value that does not decompress: validateDataFile's ReadNextAt error). Of
+ * first_bad_crc and data.first_bad the smaller entry is the one validateDataFile stops at; on a tie it
+ * is the read error (a flagged value's CRC is not meaningful). */
 typedef struct rio_sst_info {
     rio_file_info index;      /* ReadNext loop over index.rio */
     rio_file_info data;       /* ReadNext loop over data.rio */
@@ -200,8 +216,9 @@ int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, co
                  uint64_t data_len, rio_sst** out, rio_sst_info* info);
 /* Entry i in index order (SSTableFullScanIterator.Next, sstable_iterator.go:77-111): key, the value of
  * data record i (is_nil for a nil record), the stored valueOffset and checksum and the value's CRC-64.
- * Returns RIO_OK, RIO_ERR_ARG for i >= n_entries, or the data file's terminal status when data record i
- * does not exist (the scan's dataReader.ReadNext error; key and checksum are still filled). */
+ * Returns RIO_OK, RIO_ERR_ARG for i >= n_entries, the data file's terminal status when data record i
+ * does not exist (the scan's dataReader.ReadNext error; key and checksum are still filled), or
+ * RIO_ERR_DECOMPRESS / RIO_EOF_ZERO_TAIL when data record i is flagged RIO_FLAG_CORRUPT / RIO_FLAG_EOF. */
 int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, uint64_t* key_len, const uint8_t** value,
                   uint64_t* value_len, int* is_nil, uint64_t* value_offset, uint64_t* checksum, uint64_t* crc);
 void rio_sst_free(rio_sst* t);
@@ -263,7 +280,9 @@ void rio_index_free(rio_index* idx);
  * RIO_EOF after the last one; otherwise that file's rc (RIO_OK, RIO_ERR_IO when it cannot be opened or
  * mapped, RIO_ERR_HIP) with `info` and the arrays of rio_decode (out / out_off[n+1] / flags[n]), valid
  * until the next rio_replay_next or rio_replay_free. Deliver records < info.n_records, then map
- * info.status like FileReader.ReadNext's terminal error. A file with info.status RIO_ERR_UNSUPPORTED
+ * info.status like FileReader.ReadNext's terminal error; when info.n_bad, stop at record
+ * info.first_bad instead: RIO_FLAG_EOF ends this file (replayer.go:60-63), RIO_FLAG_CORRUPT ends the
+ * replay with the codec error (:65-67). A file with info.status RIO_ERR_UNSUPPORTED
  * must be re-read whole by the reference reader before any of its records is delivered. */
 typedef struct rio_replay rio_replay;
 int rio_replay_open(int device, const char* const* paths, uint64_t n_paths, uint32_t depth, uint32_t workers,
@@ -283,7 +302,8 @@ void rio_replay_free(rio_replay* r);
  * `first_record`, the file-wide index of its first record. info.status is RIO_OK while more windows
  * follow; the last window carries the file's terminal status as the whole-file rio_frame /
  * rio_decode pair reports it (status_offset a file offset; the failing record's index is
- * first_record + info.n_records). RIO_EOF after the last window. RIO_ERR_UNSUPPORTED: the adapter
+ * first_record + info.n_records). info.first_bad / n_bad cover the window's flagged records
+ * (first_bad a file-wide index). RIO_EOF after the last window. RIO_ERR_UNSUPPORTED: the adapter
  * continues with the reference reader after SkipNext over the records already delivered.
  * rio_stream_open_host reads from host memory instead of a path (the caller keeps it alive until
  * rio_stream_free). */
@@ -319,7 +339,8 @@ int rio_reader_header(rio_reader* r, uint32_t* version, uint32_t* compression);
 uint64_t rio_reader_size(rio_reader* r);
 /* detail values of the last error (HEADER_CRC: expected/actual; VERSION etc.: value) */
 void rio_reader_last_detail(rio_reader* r, uint64_t* detail0, uint64_t* detail1, uint64_t* offset);
-/* ReaderI */
+/* ReaderI. read_next on a record that does not decompress returns RIO_ERR_DECOMPRESS (RIO_EOF_ZERO_TAIL
+ * for gzip's empty payload) and the next call returns the record after it; skip_next passes over it. */
 int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil);
 int rio_reader_skip_next(rio_reader* r);
 /* ReadAtI (thread-safe in the reference; here serialised per handle) */

@@ -371,14 +371,34 @@ static void arena_push(arena_t* a, uint64_t rec_off, const uint8_t* data, uint64
     a->out_off[a->n] = a->out_len;
 }
 
+/* Output bytes reserved for a record whose payload does not decompress (the device sizes every
+ * record before decoding any): snappy's preamble when decodedLen accepts it and a stream of this
+ * length can reach it (orc_snappy_decode's first two checks); gzip's ISIZE trailer when the payload
+ * holds a whole member (>= 18 bytes) and DEFLATE's maximum ratio (258 bytes per 2 bits) can reach
+ * it; otherwise 0. Not a reference behaviour: the reference returns no bytes for such a record. */
+static uint64_t bad_reserve(uint32_t comp, const uint8_t* pay, uint64_t plen) {
+    if (comp == RIO_COMP_SNAPPY) {
+        uint64_t d = 0;
+        const int k = go_uvarint(pay, plen, &d);
+        if (k <= 0 || d > 0xFFFFFFFFull || d > 22ull * (plen - (uint64_t)k) + 64) return 0;
+        return d;
+    }
+    if (plen < 18) return 0;
+    const uint8_t* t = pay + plen - 4;
+    const uint64_t isz = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
+    return isz > 1032ull * plen + 64 ? 0 : isz;
+}
+
 int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res) {
     memset(res, 0, sizeof *res);
+    res->first_bad = UINT64_MAX;
     int e = orc_file_header(f, len, &res->version, &res->compression, &res->detail0);
     if (e) { res->status = e; return e; }
     arena_t a;
     memset(&a, 0, sizeof a);
     a.out_off = (uint64_t*)calloc(1, sizeof(uint64_t));
     uint64_t p = RIO_FILE_HEADER_BYTES;
+    uint64_t first_bad = UINT64_MAX, n_bad = 0;
     int status = RIO_OK;
     for (;;) {
         brd r = {f + p, len - p, 0, res->version == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : UINT64_MAX};
@@ -418,6 +438,18 @@ int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res)
             uint8_t* dec = NULL;
             uint64_t dlen = 0;
             e = decompress(res->compression, pay, plen, &dec, &dlen);
+            if (e == RIO_ERR_DECOMPRESS || (e == RIO_EOF_PAYLOAD && res->compression == RIO_COMP_GZIP)) {
+                /* ReadNext returns the codec error; the payload is consumed and the loop goes on */
+                const uint64_t rsv = bad_reserve(res->compression, pay, plen);
+                uint8_t* z = (uint8_t*)calloc(rsv ? rsv : 1, 1);
+                arena_push(&a, p, z, rsv, 0);
+                free(z);
+                a.flags[a.n - 1] = e == RIO_ERR_DECOMPRESS ? RIO_FLAG_CORRUPT : RIO_FLAG_EOF;
+                if (!n_bad) first_bad = a.n - 1;
+                n_bad++;
+                p += h.hdr_len + plen;
+                continue;
+            }
             if (e) { status = e; break; }
             arena_push(&a, p, dec, dlen, 0);
             free(dec);
@@ -434,6 +466,8 @@ int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res)
     res->out_off = a.out_off;
     res->rec_off = a.rec_off;
     res->flags = a.flags;
+    res->first_bad = first_bad;
+    res->n_bad = n_bad;
     return RIO_OK;
 }
 

@@ -28,15 +28,21 @@ typedef struct orc_file_result {
     uint8_t* out;       /* malloc'd, total_out_bytes */
     uint64_t* out_off;  /* malloc'd, n_records + 1 */
     uint64_t* rec_off;  /* malloc'd, n_records */
-    uint8_t* flags;     /* malloc'd, n_records */
+    uint8_t* flags;     /* malloc'd, n_records: RIO_FLAG_NIL / CORRUPT / EOF */
+    uint64_t first_bad; /* first record whose payload does not decompress (UINT64_MAX: none) */
+    uint64_t n_bad;
 } orc_file_result;
 
 uint32_t orc_crc32c(const uint8_t* p, uint64_t n);
 /* readFileHeaderFromBuffer (common_reader.go:22-44) on the first 8 bytes */
 int orc_file_header(const uint8_t* f, uint64_t len, uint32_t* version, uint32_t* compression,
                     uint64_t* detail);
-/* FileReader Open + ReadNext loop until the first non-nil error (file_reader.go:26-131, 389-447;
- * v1/v2 legacy paths :282-360, read only so the reference's SSTable fixtures can pin the checker) */
+/* FileReader Open + ReadNext loop until the first error that is not a codec error (file_reader.go:
+ * 26-131, 389-447; v1/v2 legacy paths :282-360, read only so the reference's SSTable fixtures can pin
+ * the checker). A payload that does not decompress was consumed before the codec ran (:113-122,
+ * :430-439), so the loop goes on: such a record gets RIO_FLAG_CORRUPT (RIO_FLAG_EOF for gzip's empty
+ * payload) and the output length the device reserves for it (usable snappy preamble / plausible gzip
+ * ISIZE, else 0), filled with zeros. */
 int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res);
 void orc_file_result_free(orc_file_result* res);
 /* MMapReader.ReadNextAt (mmap_reader.go:130-203 v4, 298-356 v3). *out is malloc'd (NULL for nil). */

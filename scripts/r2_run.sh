@@ -11,6 +11,7 @@ if [ "$TESTS" != "none" ]; then
   rc=$?; echo "tests rc=$rc"; tail -15 "$OUT/tests.log"
   if fatal $rc; then exit $rc; fi
 fi
+[ "$CFGS" = none ] && { echo done; exit 0; }
 for c in $CFGS; do
   echo "== bench $c ($(date +%T))"
   timeout -k 10 300 python bench.py --config $c --no-e2e --no-cpu-baseline > "$OUT/bench_$c.log" 2>&1

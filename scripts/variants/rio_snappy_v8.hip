@@ -32,6 +32,8 @@
 #include "rio_device.h"
 #include "rio_dev_util.h"
 
+// round-1 decoder (rio_snappy.hip at 88cb848) kept for A/B timing (scripts/variants/build.sh)
+
 namespace rio {
 
 namespace {
@@ -286,10 +288,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             pd += n;
             eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
             islit = lit1;
-            // a record that does not decode is not the end of the lane: its remaining input is skipped
-            // and the rest of its announced output is filled (16-byte ring pieces of unspecified
-            // bytes), then the next record starts; k_snappy_verify flags it
-            s = badn ? s_end : s;
+            pdone = pdone || badn;
             // record boundary: stream consumed -> the record must be complete; switch to the next
             // (its descriptor landed) or finish the range
             const bool at_end = !pdone && rem == 0 && s == s_end;
@@ -297,11 +296,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const bool more = k + 1 < r1;
             const bool sw = at_end && !bad_len && more && nds == 2;
             bad = bad || bad_len;
-            const bool fill = bad_len;  // (rd_end > pd: output room is checked per element)
-            rem = fill ? rd_end - pd : rem;
-            eff = fill ? 16u : eff;
-            islit = islit && !fill;
-            pdone = pdone || (at_end && !bad_len && !more);
+            pdone = pdone || bad_len || (at_end && !more);
             k += sw ? 1u : 0u;
             const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
             s = sw ? (uint32_t)(nstart - base) : s;
@@ -324,7 +319,11 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         {
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn < a + kInCh;
+#ifdef RIO_IN_NT
+            S.in = ldu16_nt(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
+#else
             S.in = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
+#endif
             S.in_c = take ? cn : kNoChunk;
             cn += take ? 1u : 0u;
         }
@@ -348,7 +347,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         else
             st_partial(gout + q, v, d - q);
     }
-    *bad_rec = r0;
+    *bad_rec = k;
     return !bad;
 }
 
@@ -371,15 +370,8 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     if ((t & ~63ull) * rpl >= n) return;  // the whole wave is idle (wave-uniform exit)
     uint8_t* sink = P.sink + (t >> 6) * 64;  // the wave's placeholder line
     uint64_t bad_rec = 0;
-    if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
-        // a record of this lane did not decode: k_snappy_verify re-decodes the lane's records one
-        // thread each and flags the failing ones
-        const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
-        if (at < kFailLanes) {
-            P.fail_lanes[2 * at] = r0;
-            P.fail_lanes[2 * at + 1] = r1;
-        }
-    }
+    if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec))
+        atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)(2 * bad_rec));
 }
 
 // Files beyond the lane-stream kernel's 32-bit positions (>= 4 GiB of input or output, or a
@@ -392,41 +384,18 @@ __global__ void __launch_bounds__(256) k_snappy_global(FrameParams P) {
     const uint64_t n = st->n_records;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
+        if (P.flags[i] & RIO_FLAG_NIL) continue;
         const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
         const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
         if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), slen, P.out + o0, o1 - o0))
-            mark_bad(P, i);
+            atomicMin((unsigned long long*)&st->decode_err_rec, (unsigned long long)(2 * i));
     }
-}
-
-// Records of lanes that met a corrupt record (or of every lane when more than kFailLanes did): one
-// thread per record decodes it again in place (a record that decoded is rewritten with the same
-// bytes) and flags the ones that fail, exactly where golang/snappy's Decode returns ErrCorrupt.
-__global__ void __launch_bounds__(256) k_snappy_verify(FrameParams P) {
-    ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || st->n_fail_lanes == 0)
-        return;
-    auto verify = [&](uint64_t i) {
-        if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) return;
-        const uint64_t pay = P.rec_pay[i], o0 = P.out_off[i], o1 = P.out_off[i + 1];
-        if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), pay >> 8, P.out + o0, o1 - o0))
-            mark_bad(P, i);
-    };
-    if (st->n_fail_lanes > kFailLanes) {  // the list overflowed: every record
-        const uint64_t n = st->n_records, stride = (uint64_t)gridDim.x * blockDim.x;
-        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) verify(i);
-        return;
-    }
-    for (uint64_t l = blockIdx.x; l < st->n_fail_lanes; l += gridDim.x)
-        for (uint64_t i = P.fail_lanes[2 * l] + threadIdx.x; i < P.fail_lanes[2 * l + 1]; i += blockDim.x) verify(i);
 }
 
 hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s) {
     // 4 waves x 20 KiB = 80 KiB per workgroup: 2 workgroups (8 waves) per CU
     hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, P);
     hipLaunchKernelGGL(k_snappy_global, dim3(64), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_snappy_verify, dim3(256), dim3(256), 0, s, P);
     return hipGetLastError();
 }
 

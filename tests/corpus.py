@@ -148,6 +148,18 @@ def cases():
     pre = uvarint(5000) + b"\x00a"
     out.append(("snappy_huge_preamble", encode_file([b"ok"] * 3, 2) + header_v4(5000, len(pre)) + pre))
     out.append(("snappy_empty_payload", encode_file([b"ok"] * 3, 2) + header_v4(0, 0)))
+    # payloads that do not decompress in the middle of a file: ReadNext returns snappy's error for
+    # that record and goes on (file_reader.go:113-122). Unusable preamble (varint overflow), preamble
+    # above / below what the elements produce, empty payload; each followed by more records.
+    lit160 = b"\xf0\x9f" + bytes(range(160))  # tagLiteral, 1-byte length: 160 bytes
+    for name, pay in (("snappy_bad_preamble_mid", b"\xff" * 11 + b"abc"),
+                      ("snappy_short_mid", uvarint(170) + lit160),
+                      ("snappy_long_mid", uvarint(100) + lit160),
+                      ("snappy_empty_mid", b"")):
+        before = encode_file([asc(40 + i) for i in range(30)], 2)
+        after = encode_file([asc(60 + i) for i in range(30)] + [None, b""], 2)[8:]
+        bad = header_v4(160, len(pay)) + pay
+        out.append((name, before + bad + after + bad + after))
     # nil records in a compressed file with c != 0 (file_writer.go:198-219)
     out.append(("nil_snappy", encode_file([None, b"a", None, None, b"", b"bb"] * 100, 2)))
     # payload length beyond the file (the reference would panic in bufferPool.Get; we report EOF)

@@ -15,8 +15,28 @@ class OrcFileResult(ctypes.Structure):
         ("version", c_uint32), ("compression", c_uint32), ("n_records", c_uint64), ("total_out_bytes", c_uint64),
         ("status", ctypes.c_int32), ("status_offset", c_uint64), ("detail0", c_uint64), ("detail1", c_uint64),
         ("out", POINTER(c_uint8)), ("out_off", POINTER(c_uint64)), ("rec_off", POINTER(c_uint64)),
-        ("flags", POINTER(c_uint8)),
+        ("flags", POINTER(c_uint8)), ("first_bad", c_uint64), ("n_bad", c_uint64),
     ]
+
+
+class BadRecord:
+    """A record whose payload does not decompress: ReadNext returns the codec error (kind
+    "corrupt") or gzip's bare io.EOF (kind "eof") for it, and goes on with the next record."""
+
+    def __init__(self, kind: str):
+        self.kind = kind
+
+    def __eq__(self, other):
+        return isinstance(other, BadRecord) and other.kind == self.kind
+
+    def __hash__(self):
+        return hash(self.kind)
+
+    def __repr__(self):
+        return f"BadRecord({self.kind!r})"
+
+
+NONE = (1 << 64) - 1
 
 
 _lib = None
@@ -75,7 +95,11 @@ def file_reader_decode(data: bytes) -> dict:
     recs, rec_off = [], []
     for i in range(r.n_records):
         lo, hi = r.out_off[i], r.out_off[i + 1]
-        if r.flags[i] & 1:
+        if r.flags[i] & 2:
+            recs.append(BadRecord("corrupt"))
+        elif r.flags[i] & 4:
+            recs.append(BadRecord("eof"))
+        elif r.flags[i] & 1:
             recs.append(None)
         elif hi > lo:
             recs.append(ctypes.string_at(ctypes.addressof(r.out.contents) + lo, hi - lo))
@@ -84,7 +108,8 @@ def file_reader_decode(data: bytes) -> dict:
         rec_off.append(r.rec_off[i])
     res = {"version": r.version, "compression": r.compression, "n_records": r.n_records,
            "total_out_bytes": r.total_out_bytes, "status": r.status, "status_offset": r.status_offset,
-           "detail0": r.detail0, "detail1": r.detail1, "records": recs, "rec_off": rec_off}
+           "detail0": r.detail0, "detail1": r.detail1, "records": recs, "rec_off": rec_off,
+           "first_bad": r.first_bad, "n_bad": r.n_bad}
     lib().orc_file_result_free(byref(r))
     return res
 
@@ -105,7 +130,7 @@ def file_reader_decode_arrays(data) -> dict:
         return np.ctypeslib.as_array(ptr, shape=(count,)).astype(dt, copy=True)
 
     res = {"status": r.status, "status_offset": r.status_offset, "n_records": n, "total_out_bytes": nb,
-           "detail0": r.detail0, "detail1": r.detail1,
+           "detail0": r.detail0, "detail1": r.detail1, "first_bad": r.first_bad, "n_bad": r.n_bad,
            "out": cp(r.out, nb, np.uint8), "out_off": cp(r.out_off, n + 1, np.int64),
            "rec_off": cp(r.rec_off, n, np.int64), "flags": cp(r.flags, n, np.uint8)}
     lib().orc_file_result_free(byref(r))
@@ -174,14 +199,17 @@ def sstable_oracle(base: str) -> dict:
     idx = file_reader_decode(open(os.path.join(base, "index.rio"), "rb").read())
     data_img = open(os.path.join(base, "data.rio"), "rb").read()
     dat = file_reader_decode(data_img)
-    entries, bad_proto = [], None
+    entries, bad_proto, index_bad = [], None, None
     for i, r in enumerate(idx["records"]):
+        if isinstance(r, BadRecord):  # Load's ReadNext error; gzip's bare io.EOF ends the loop
+            index_bad = i if r.kind == "corrupt" else None
+            break
         e = index_entry(r)
         if e is None:
             bad_proto = i
             break
         entries.append(e)
-    first_bad = unplaced = None
+    first_bad = unplaced = value_bad = None
     crcs = []
     at = {o: j for j, o in enumerate(dat["rec_off"])}  # ReadNextAt at a record start = that record
     for i, (k, vo, cs) in enumerate(entries):
@@ -189,13 +217,18 @@ def sstable_oracle(base: str) -> dict:
         if j != i and unplaced is None:
             unplaced = i
         val = dat["records"][j] if j is not None else None
+        if isinstance(val, BadRecord):  # getValueAtOffset's ReadNextAt error (sstable_reader.go:90-94)
+            crcs.append(None)
+            if value_bad is None:
+                value_bad = i
+            continue
         c = crc64_iso(val or b"")
         crcs.append(c)
         if first_bad is None and cs != 0 and c != cs:
             first_bad = i
     return {"index_status": idx["status"], "data_status": dat["status"], "entries": entries,
-            "bad_proto": bad_proto, "values": dat["records"], "crcs": crcs, "first_bad": first_bad,
-            "unplaced": unplaced}
+            "bad_proto": bad_proto, "index_bad": index_bad, "values": dat["records"], "crcs": crcs,
+            "first_bad": first_bad, "value_bad": value_bad, "unplaced": unplaced}
 
 
 def disk_index_search(index: bytes, key: bytes, seek_len: int = 4096):

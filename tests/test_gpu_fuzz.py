@@ -107,13 +107,17 @@ def test_sstable_damage(tmp_path, seed):
     # the mirror's checks in order (sstables/__init__.py NewSSTableReader): index reading error,
     # malformed IndexEntry, index not in the writer's layout (handed back), value checksum mismatch
     fails = (o["index_status"] not in (1, 2, 3, 4) or o["bad_proto"] is not None or o["unplaced"] is not None
-             or o["first_bad"] is not None)
+             or o["first_bad"] is not None or o["index_bad"] is not None or o["value_bad"] is not None)
     assert (r is None) == fails, (o["index_status"], o["bad_proto"], o["unplaced"], o["first_bad"], err)
     if fails:
         assert err is not None
-        if o["index_status"] in (1, 2, 3, 4) and o["bad_proto"] is None and o["unplaced"] is None:
-            i = o["first_bad"]
-            assert f"Checksum mismatch: expected {o['entries'][i][2]:x}, got {o['crcs'][i]:x}" in str(err)
+        if (o["index_status"] in (1, 2, 3, 4) and o["bad_proto"] is None and o["unplaced"] is None
+                and o["index_bad"] is None):
+            i, vb = o["first_bad"], o["value_bad"]
+            if vb is not None and (i is None or vb <= i):  # validateDataFile meets the read error first
+                assert f"while getting value at offset {o['entries'][vb][1]}: failed decompressing" in str(err)
+            else:
+                assert f"Checksum mismatch: expected {o['entries'][i][2]:x}, got {o['crcs'][i]:x}" in str(err)
         return
     got, serr = T.scan_all(r)
     n = len(o["entries"])

@@ -58,7 +58,9 @@ def stream_all(data: bytes, window: int, depth: int = 2, path: str | None = None
             f = ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint8))
             for i in range(n):
                 lo, hi = o[i], o[i + 1]
-                if f[i] & 1:
+                if f[i] & (L.RIO_FLAG_CORRUPT | L.RIO_FLAG_EOF):
+                    recs.append(orc.BadRecord("corrupt" if f[i] & L.RIO_FLAG_CORRUPT else "eof"))
+                elif f[i] & 1:
                     recs.append(None)
                 else:
                     recs.append(ctypes.string_at(out.value + lo, hi - lo) if hi > lo else b"")
@@ -164,9 +166,10 @@ def test_zero_tail_spans_windows(tmp_path, window):
         assert reader_loop(str(p), window) == reader_loop(str(p), NEVER)
 
 
-def test_corrupt_record_mid_file_ends_at_its_window():
-    """A header CRC failure and a snappy ErrCorrupt in the middle of a long file: the stream ends
-    there with the whole-file status, whatever window the record falls in."""
+def test_corrupt_record_mid_file_in_any_window():
+    """A header CRC failure in the middle of a long file ends the stream there with the whole-file
+    status, whatever window the record falls in; a snappy ErrCorrupt is that record's alone (flagged,
+    the stream goes on) in every window layout."""
     recs = mixed_records(400, 11, max_len=900)
     data = bytearray(encode_file(recs, 2))
     exp = orc.file_reader_decode(bytes(data))

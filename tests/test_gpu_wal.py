@@ -34,10 +34,18 @@ def replay(opts, stop_after=None):
 
 
 def expected(base):
-    """Oracle: sorted *.wal files, each decoded by the FileReader restatement; stop at a non-EOF end."""
+    """Oracle: sorted *.wal files, each decoded by the FileReader restatement; stop at a non-EOF end.
+    A record that does not decompress ends the replay (its ReadNext error), or only its file when the
+    error is gzip's bare io.EOF (replayer.go:59-67)."""
     recs = []
     for p in W._wal_files(base):
         o = orc.file_reader_decode(open(p, "rb").read())
+        bad = [i for i, r in enumerate(o["records"]) if isinstance(r, orc.BadRecord)]
+        if bad:
+            recs += o["records"][:bad[0]]
+            if o["records"][bad[0]].kind == "eof":
+                continue
+            return recs, p, o
         recs += o["records"]
         if o["status"] not in EOF_CLASS:
             return recs, p, o

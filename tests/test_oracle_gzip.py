@@ -47,12 +47,22 @@ def test_valid_gzip_files_decode_to_sources(name):
 
 @pytest.mark.parametrize("name", ["gz_bad_hcrc", "gz_bad_magic", "gz_bad_cm", "gz_bad_crc", "gz_isize_plus1",
                                   "gz_isize_huge", "gz_btype3", "gz_trailing_garbage"])
-def test_gzip_corruption_ends_at_record(name):
+def test_gzip_corruption_flags_the_record(name):
+    """The gzip reader's error comes back for record 7 alone; ReadNext then reads record 8
+    (the payload was consumed before the codec ran, file_reader.go:113-122)."""
     o = orc.file_reader_decode_arrays(_records(name))
-    assert o["status"] == STATUS["DECOMPRESS"] and o["n_records"] == 7
+    assert o["status"] == STATUS["EOF"] and o["n_records"] == 20
+    assert o["flags"][7] == 2 and (o["first_bad"], o["n_bad"]) == (7, 1)
+    full = orc.file_reader_decode_arrays(_records("gz_text_small"))
+    for k in (6, 8, 19):  # neighbours decode as in the clean file (same text records)
+        a, b = o["out_off"][k], full["out_off"][k]
+        ln = o["out_off"][k + 1] - a
+        assert bytes(o["out"][a:a + ln]) == bytes(full["out"][b:b + ln])
 
 
 def test_gzip_empty_payload_is_eof_class():
-    # gzip.NewReader(empty) -> bare io.EOF, returned unwrapped by ReadNext (file_reader.go:118-121)
+    # gzip.NewReader(empty) -> bare io.EOF, returned unwrapped by ReadNext (file_reader.go:118-121);
+    # the loop can go on past it
     o = orc.file_reader_decode_arrays(_records("gz_empty_payload"))
-    assert o["status"] == STATUS["EOF_PAYLOAD"] and o["n_records"] == 7
+    assert o["status"] == STATUS["EOF"] and o["n_records"] == 20
+    assert o["flags"][7] == 4 and o["out_off"][8] == o["out_off"][7]
