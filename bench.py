@@ -49,6 +49,8 @@ CONFIGS = {
                                  "(1.25M entries), one lane per key"),
     "enc": (1_000_000, 1024, 2, 1, "Encode: 1M x 1 KiB text-like records -> recordio v4 snappy file image "
                                     "(FileWriter.Write batch), device-resident"),
+    "readat": (1_000_000, 1024, 2, 1, "ReadAtI: ReadNextAt / SeekNext on the C2 file from host threads "
+                                      "(MMapReader, mmap_reader.go:58-203)"),
     "c5": (1_250_000, 1024, 2, 0, "C5: SSTable load + validateDataFile + full scan, 1.25M SHA1 keys x 1 KiB values "
                                   "(data.rio snappy v4 + index.rio v4), one table per GPU (10M keys over 8 GPUs)"),
 }
@@ -635,6 +637,92 @@ def run_encode(args, world, rank, local, device):
         print(json.dumps(line), flush=True)
 
 
+def run_readat(args, world, rank, local, device):
+    """ReadAtI lookups (MMapReader.ReadNextAt / SeekNext, mmap_reader.go:58-203) from host threads on
+    one device-backed reader over the C2 file: the reader decodes the file once on the GPU, then
+    every ReadNextAt at a record start is a binary search over the decoded record offsets on the
+    calling thread (no kernel launch, no lock). Measured by go-sstables_amd/rio_readat_bench (C++
+    over the C-ABI, the shape of a cgo caller); a step = one lookup."""
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    from recordio import generate
+    from recordio.device import DeviceDecoder, to_device_file
+
+    n_rec, rec_len, comp, kind, desc = CONFIGS["readat"]
+    image = generate(n_rec, rec_len, comp, kind=kind, seed=rank_seed(rank), threads=min(16, os.cpu_count() or 1))
+    d_file, length = to_device_file(image, local)
+    b, info = DeviceDecoder(local).decode(d_file, length)
+    rec_off = b.rec_off[:info["n_records"]].cpu().numpy().astype(np.uint64)
+    del d_file, b
+    exe = os.path.join(HERE, "go-sstables_amd", "rio_readat_bench")
+    tmp = tempfile.mkdtemp(prefix=f"readat_r{rank}_")
+    try:
+        fpath, opath = os.path.join(tmp, "c2.rio"), os.path.join(tmp, "offsets.u64")
+        image.tofile(fpath)
+        rec_off.tofile(opath)
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(local))
+
+        def drive(threads, k, mode):
+            out = subprocess.run([exe, fpath, opath, str(threads), str(k), mode], capture_output=True, text=True,
+                                 timeout=300, env=env)
+            if out.returncode:
+                raise RuntimeError(f"readat driver ({mode}, {threads} threads): rc {out.returncode} {out.stderr[-500:]}")
+            return json.loads(out.stdout.strip().splitlines()[-1])
+
+        per_thread = max(1, args.steps) * 10_000
+        at = {t: drive(t, per_thread, "at") for t in (1, 4, 16)}
+        seek = {t: drive(t, per_thread // 10, "seek") for t in (1, 16)}
+    finally:
+        import shutil
+
+        shutil.rmtree(tmp, ignore_errors=True)
+    best = at[16]
+    line = {
+        "metric": "ReadNextAt lookups/s (16 host threads, one device-decoded MMapReader)",
+        "value": round(best["lookups_per_s"], 1), "unit": "lookups/s", "n_gpus": 1, "steps": int(best["lookups"]),
+        "warmup": 1, "ms_per_step": round(best["seconds"] * 1e3 / best["lookups"], 6), "higher_is_better": True,
+        "scaling": "replicas", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: the C2 file (1M x 1 KiB text-like snappy records), random record starts",
+        "config": {"workload": desc, "records": int(info["n_records"]), "file_bytes": length,
+                   "parallelism": "host threads on one reader; replicas only across GPUs"},
+        "roofline": None,
+        "roofline_note": "no kernel per lookup: the one-time decode is the C2 decode (see the c2 line); a "
+                         "lookup is a binary search over 8-byte offsets plus a pointer into the decoded arena",
+        "us_per_lookup": {f"{t}_threads": round(v["us_per_lookup_per_thread"], 4) for t, v in at.items()},
+        "lookups_per_s": {f"{t}_threads": round(v["lookups_per_s"], 1) for t, v in at.items()},
+        "seek_next": {f"{t}_threads": {"lookups_per_s": round(v["lookups_per_s"], 1),
+                                       "us_per_lookup": round(v["us_per_lookup_per_thread"], 4)}
+                      for t, v in seek.items()},
+        "first_call_ms": round(at[1]["first_call_ms"], 3),
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        import oracle_py as orc
+
+        olib = orc.lib()
+        out, ol, nil, d0, d1 = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        rng = np.random.default_rng(5)
+        picks = rec_off[rng.integers(0, len(rec_off), 200_000)]
+        t1, m = time.perf_counter(), 0
+        while m < len(picks) and time.perf_counter() - t1 < 10.0:
+            st = olib.orc_read_next_at(image.ctypes.data, length, int(picks[m]), ctypes.byref(out), ctypes.byref(ol),
+                                       ctypes.byref(nil), ctypes.byref(d0), ctypes.byref(d1))
+            if st:
+                raise RuntimeError("oracle ReadNextAt failed")
+            olib.orc_free(out)
+            m += 1
+        t_cpu = time.perf_counter() - t1
+        line["cpu_baseline"] = {"value": round(m / t_cpu, 1), "unit": "lookups/s", "cores": 1, "kind": "port",
+                                "sample": f"{m} random record starts, oracle ReadNextAt restatement (header parse + "
+                                f"snappy decode of one record per lookup, ctypes call overhead included), "
+                                f"{_cpu_model()}"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -657,8 +745,8 @@ def main():
 
         dist.init_process_group(backend="nccl", device_id=device)
 
-    if args.config in ("c5", "wal", "idx", "enc"):
-        {"c5": run_sstable, "wal": run_wal, "idx": run_index, "enc": run_encode}[args.config](
+    if args.config in ("c5", "wal", "idx", "enc", "readat"):
+        {"c5": run_sstable, "wal": run_wal, "idx": run_index, "enc": run_encode, "readat": run_readat}[args.config](
             args, world, rank, local, device)
         if world > 1:
             torch.distributed.destroy_process_group()

@@ -15,6 +15,8 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -49,6 +51,9 @@ uint64_t enc_table_bytes();
 size_t enc_cub_bytes(uint64_t n);
 hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t* out, uint64_t out_cap,
                           ReadAtResult* res, hipStream_t s);
+int build_seek_map(const uint8_t* f, uint64_t len, const uint64_t* rec_off, const uint8_t* flags, uint64_t n,
+                   std::vector<uint64_t>& P, std::vector<uint64_t>& R, hipStream_t s);
+constexpr uint64_t kSeekOther = ~0ull >> 1;  // rio_kernels.hip
 hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
                             uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off, hipStream_t s);
 }  // namespace rio
@@ -82,12 +87,13 @@ extern "C" const char* rio_strerror(int s) {
     case RIO_ERR_STATE: return "reader state error";
     case RIO_ERR_IO: return "I/O error";
     case RIO_ERR_PROTO: return "proto: cannot parse invalid wire-format data";
+    case RIO_EOF_CODEC: return "EOF from the codec (empty gzip payload)";
     default: return "unknown status";
     }
 }
 
 extern "C" int rio_status_is_eof(int s) {
-    return s == RIO_EOF || s == RIO_EOF_ZERO_TAIL || s == RIO_EOF_HEADER || s == RIO_EOF_PAYLOAD;
+    return s == RIO_EOF || s == RIO_EOF_ZERO_TAIL || s == RIO_EOF_HEADER || s == RIO_EOF_PAYLOAD || s == RIO_EOF_CODEC;
 }
 
 extern "C" const char* rio_build_info(void) { return "librio gfx950 recordio v3/v4 decode"; }
@@ -167,6 +173,8 @@ struct rio_ctx {
         block_excl, state, info;
     // host-API arenas
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
+    // reader handles sharing this ctx take this around every device use (rio_reader_*)
+    std::mutex mu;
     // rio_sst_open: parsed index fields (4 x n), per-entry CRC-64, kernel results
     DevBuf sst_fields, sst_crc, sst_res;
     // rio_device_encode: compressed payloads, their offsets and lengths, hash tables, headers,
@@ -548,11 +556,40 @@ extern "C" int rio_device_read_at(rio_ctx* ctx, const uint8_t* d_file, uint64_t 
 // ------------------------------------------------------------------------------------------
 // reader handles
 // ------------------------------------------------------------------------------------------
+// MMapReader's view of a decoded file: the FileReader sequence of records (rio_frame + rio_decode,
+// once per reader) and the SeekNext map (build_seek_map, rio_kernels.hip: every 0x91 position P[k]
+// and the record R[k] a SeekNext walk reaching it ends at). ReadNextAt at a record start and SeekNext
+// whose walk ends at a decoded record are answered from here by binary search on the calling thread:
+// no kernel, no lock, no copy (the data pointer stays valid until rio_reader_free).
+struct ReadAtIndex {
+    std::vector<uint8_t> out, flags;
+    std::vector<uint64_t> out_off, rec_off, P, R;
+    uint64_t n = 0;
+    // record index i with rec_off[i] == off, or n
+    uint64_t find(uint64_t off) const {
+        const uint64_t i = lower(off);
+        return i < n && rec_off[i] == off ? i : n;
+    }
+    uint64_t lower(uint64_t off) const {
+        return (uint64_t)(std::lower_bound(rec_off.begin(), rec_off.begin() + n, off) - rec_off.begin());
+    }
+    // ReadNextAt's result for record i (mmap_reader.go:130-203; the FileReader decoded the same bytes)
+    int record(uint64_t i, const uint8_t** data, uint64_t* len, int* is_nil) const {
+        if (flags[i] & RIO_FLAG_CORRUPT) return RIO_ERR_DECOMPRESS;
+        if (flags[i] & RIO_FLAG_EOF) return RIO_EOF_CODEC;
+        const bool nil = (flags[i] & RIO_FLAG_NIL) != 0;
+        if (is_nil) *is_nil = nil ? 1 : 0;
+        if (len) *len = nil ? 0 : out_off[i + 1] - out_off[i];
+        if (data) *data = out.data() + out_off[i];
+        return RIO_OK;
+    }
+};
+
 struct rio_reader {
     rio_ctx* ctx = nullptr;
     std::string path;
     bool mmap_mode = false;
-    bool open = false, closed = false;
+    std::atomic<bool> open{false}, closed{false};
     int fd = -1;
     const uint8_t* map = nullptr;
     uint64_t size = 0;
@@ -579,11 +616,17 @@ struct rio_reader {
     // MMAP mode
     bool on_device = false;
     DevBuf dfile;
-    std::vector<uint8_t> rec_buf;
-    uint64_t seek_len = 4096;
-    // last error details
-    uint64_t det0 = 0, det1 = 0, err_off = 0;
+    std::atomic<uint64_t> seek_len{4096};
+    // MMAP mode: the decoded file (built on the first ReadNextAt / SeekNext, then read-only)
+    std::atomic<const ReadAtIndex*> ix{nullptr};
+    std::unique_ptr<ReadAtIndex> ix_own;
 };
+
+// details of the last failed reader call, per calling thread (ReadAtI is used concurrently)
+struct LastDetail {
+    uint64_t d0 = 0, d1 = 0, off = 0;
+};
+static thread_local LastDetail tl_det;
 
 static int reader_new(rio_ctx* ctx, const char* path, bool mm, rio_reader** out) {
     if (!ctx || !path || !out) return RIO_ERR_ARG;
@@ -627,11 +670,11 @@ extern "C" int rio_reader_open(rio_reader* r) {
     r->version = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
     r->compression = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
     if (r->version > RIO_VERSION4 || r->version < RIO_VERSION1) {
-        r->det0 = r->version;
+        tl_det.d0 = r->version;
         return RIO_ERR_VERSION;
     }
     if (r->compression > RIO_COMP_LZW) {
-        r->det0 = r->compression;
+        tl_det.d0 = r->compression;
         return RIO_ERR_COMPRESSION_TYPE;
     }
     r->open = true;
@@ -671,9 +714,9 @@ extern "C" uint64_t rio_reader_size(rio_reader* r) { return r ? r->size : 0; }
 
 extern "C" void rio_reader_last_detail(rio_reader* r, uint64_t* d0, uint64_t* d1, uint64_t* off) {
     if (!r) return;
-    if (d0) *d0 = r->det0;
-    if (d1) *d1 = r->det1;
-    if (off) *off = r->err_off;
+    if (d0) *d0 = tl_det.d0;
+    if (d1) *d1 = tl_det.d1;
+    if (off) *off = tl_det.off;
 }
 
 constexpr uint64_t kAutoWindowFrom = 256ull << 20, kAutoWindow = 128ull << 20;
@@ -715,6 +758,7 @@ static int file_decode(rio_reader* r) {
         return r->decode_rc = rc;
     }
     rio_file_info fi{};
+    std::lock_guard<std::mutex> cg(r->ctx->mu);
     int rc = rio_frame(r->ctx, r->map, r->size, &fi);
     if (rc) return r->decode_rc = rc;
     if (fi.status == RIO_ERR_UNSUPPORTED) return r->decode_rc = RIO_ERR_UNSUPPORTED;
@@ -765,9 +809,9 @@ extern "C" int rio_reader_file_info(rio_reader* r, rio_file_info* info) {
 
 // terminal status as ReadNext reports it
 static int terminal(rio_reader* r) {
-    r->det0 = r->info.detail0;
-    r->det1 = r->info.detail1;
-    r->err_off = r->info.status_offset;
+    tl_det.d0 = r->info.detail0;
+    tl_det.d1 = r->info.detail1;
+    tl_det.off = r->info.status_offset;
     return r->info.status;
 }
 
@@ -788,10 +832,9 @@ extern "C" int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_
     // a record whose payload does not decompress: ReadNext returns the codec error (or gzip's bare
     // io.EOF for an empty payload) and the next call goes on with the record after it
     if (r->w_flags[i] & (RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) {
-        r->det0 = r->det1 = 0;
-        r->err_off = r->info.status_offset;
-        // gzip's io.EOF comes back unwrapped (file_reader.go:119-121): the bare-EOF status class
-        return (r->w_flags[i] & RIO_FLAG_EOF) ? RIO_EOF_ZERO_TAIL : RIO_ERR_DECOMPRESS;
+        tl_det.d0 = tl_det.d1 = 0;
+        tl_det.off = r->info.status_offset;
+        return (r->w_flags[i] & RIO_FLAG_EOF) ? RIO_EOF_CODEC : RIO_ERR_DECOMPRESS;
     }
     if (data) *data = r->w_out + r->w_off[i];
     if (len) *len = r->w_off[i + 1] - r->w_off[i];
@@ -826,6 +869,48 @@ extern "C" int rio_reader_skip_next(rio_reader* r) {
     }
 }
 
+// ---- ReadAtI (MMapReader.ReadNextAt / SeekNext, mmap_reader.go:58-203) -----------------------
+// The file is decoded once (rio_frame + rio_decode on the reader's ctx) into a ReadAtIndex. A
+// ReadNextAt at a record start, and a SeekNext whose scan meets only bytes that cannot form a marker
+// before a record's header, are answered from it on the calling thread (binary search, no kernel, no
+// lock). Everything else (offsets inside records or past the decoded sequence, scans over 0x91
+// bytes) runs the single-record kernels (k_read_at / k_seek_next) under the reader's lock, exactly
+// as before; for gzip files those kernels locate the record and the host serves the payload from the
+// index when the offset is a record start.
+static void build_readat_index(rio_reader* r, ReadAtIndex& x) {
+    rio_ctx* ctx = r->ctx;
+    std::lock_guard<std::mutex> cg(ctx->mu);
+    rio_file_info fi{};
+    if (rio_frame(ctx, r->map, r->size, &fi) != RIO_OK) return;
+    const uint64_t n0 = fi.n_records;
+    x.out.assign(fi.total_out_bytes + 1, 0);
+    x.out_off.assign(n0 + 1, 0);
+    x.rec_off.assign(n0 + 1, 0);
+    x.flags.assign(n0 + 1, 0);
+    if (rio_decode(ctx, x.out.data(), fi.total_out_bytes, x.out_off.data(), x.rec_off.data(), x.flags.data(), n0, &fi) !=
+        RIO_OK)
+        return;
+    if (fi.status == RIO_ERR_VERSION || fi.status == RIO_ERR_COMPRESSION_TYPE || fi.status == RIO_ERR_SHORT_FILE_HEADER)
+        return;
+    const uint64_t n = std::min<uint64_t>(fi.n_records, n0);
+    // the device file, record offsets and flags of the decode are still in the ctx arenas
+    if (build_seek_map(ctx->file.as<uint8_t>(), r->size, ctx->rec_off.as<uint64_t>(), ctx->flags.as<uint8_t>(), n, x.P,
+                       x.R, ctx->stream))
+        return;
+    x.n = n;  // published only complete: a failed build leaves n = 0 (every call takes the kernels)
+}
+
+static const ReadAtIndex* readat_index(rio_reader* r) {
+    if (const ReadAtIndex* x = r->ix.load(std::memory_order_acquire)) return x;
+    std::lock_guard<std::mutex> g(r->mu);
+    if (const ReadAtIndex* x = r->ix.load(std::memory_order_relaxed)) return x;
+    auto x = std::make_unique<ReadAtIndex>();
+    if (r->open && !r->closed) build_readat_index(r, *x);
+    r->ix.store(x.get(), std::memory_order_release);
+    r->ix_own = std::move(x);
+    return r->ix_own.get();
+}
+
 static int ensure_on_device(rio_reader* r) {
     if (r->on_device) return RIO_OK;
     HIP_TRY(hipSetDevice(r->ctx->device));
@@ -838,64 +923,92 @@ static int ensure_on_device(rio_reader* r) {
     return RIO_OK;
 }
 
-static int fetch_result(rio_reader* r, const ReadAtResult& res, const uint8_t** data, uint64_t* len, int* is_nil) {
-    r->det0 = res.det0;
-    r->det1 = res.det1;
+// record bytes of a kernel-path result: valid until this thread's next ReadNextAt / SeekNext
+static thread_local std::vector<uint8_t> tl_rec;
+
+// the single-record kernels (ReadNextAt at `offset`, or SeekNext scanning from it)
+static int readat_kernel(rio_reader* r, uint64_t offset, bool seek, uint64_t seek_len, uint64_t* ro_out,
+                         const uint8_t** data, uint64_t* len, int* is_nil) {
+    std::lock_guard<std::mutex> g(r->mu);
+    if (!r->open || r->closed) return RIO_ERR_STATE;
+    std::lock_guard<std::mutex> cg(r->ctx->mu);
+    int rc = ensure_on_device(r);
+    if (rc) return rc;
+    ReadAtResult res{};
+    uint64_t ro = 0;
+    rc = read_at_impl(r->ctx, r->dfile.as<uint8_t>(), r->size, offset, seek, seek_len, &res, seek ? &ro : nullptr);
+    if (rc) return rc;
+    if (ro_out) *ro_out = ro;
+    tl_det.d0 = res.det0;
+    tl_det.d1 = res.det1;
     if (res.status != RIO_OK) return res.status;
     if (is_nil) *is_nil = res.nil;
     if (len) *len = res.nil ? 0 : res.len;
-    r->rec_buf.resize(res.len + 1);
-    if (!res.nil && res.len) {
-        HIP_TRY(hipMemcpy(r->rec_buf.data(), r->ctx->readat_out.p, res.len, hipMemcpyDeviceToHost));
-    }
-    if (data) *data = r->rec_buf.data();
+    tl_rec.resize(res.len + 1);
+    if (!res.nil && res.len) HIP_TRY(hipMemcpy(tl_rec.data(), r->ctx->readat_out.p, res.len, hipMemcpyDeviceToHost));
+    if (data) *data = tl_rec.data();
+    return RIO_OK;
+}
+
+static int readat_check(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil) {
+    if (data) *data = nullptr;
+    if (len) *len = 0;
+    if (is_nil) *is_nil = 0;
+    if (!r->open || r->closed) return RIO_ERR_STATE;
+    if (r->version < RIO_VERSION3 || r->compression == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;
     return RIO_OK;
 }
 
 extern "C" int rio_reader_read_next_at(rio_reader* r, uint64_t offset, const uint8_t** data, uint64_t* len,
                                        int* is_nil) {
     if (!r) return RIO_ERR_ARG;
-    std::lock_guard<std::mutex> g(r->mu);
-    if (data) *data = nullptr;
-    if (len) *len = 0;
-    if (is_nil) *is_nil = 0;
-    if (!r->open || r->closed) return RIO_ERR_STATE;
-    if (r->version < RIO_VERSION3 || r->compression == RIO_COMP_GZIP || r->compression == RIO_COMP_LZW)
-        return RIO_ERR_UNSUPPORTED;
-    int rc = ensure_on_device(r);
-    if (rc) return rc;
-    ReadAtResult res{};
-    rc = read_at_impl(r->ctx, r->dfile.as<uint8_t>(), r->size, offset, false, 0, &res, nullptr);
-    if (rc) return rc;
-    r->err_off = offset;
-    return fetch_result(r, res, data, len, is_nil);
+    if (int rc = readat_check(r, data, len, is_nil)) return rc;
+    tl_det = LastDetail{0, 0, offset};
+    const ReadAtIndex* x = readat_index(r);
+    const uint64_t i = x->find(offset);
+    if (i < x->n) return x->record(i, data, len, is_nil);
+    return readat_kernel(r, offset, false, 0, nullptr, data, len, is_nil);
 }
 
 extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, const uint8_t** data,
                                     uint64_t* len, int* is_nil) {
     if (!r) return RIO_ERR_ARG;
-    std::lock_guard<std::mutex> g(r->mu);
-    if (data) *data = nullptr;
-    if (len) *len = 0;
-    if (is_nil) *is_nil = 0;
     if (rec_offset) *rec_offset = 0;
-    if (!r->open || r->closed) return RIO_ERR_STATE;
-    if (r->version < RIO_VERSION3 || r->compression == RIO_COMP_GZIP || r->compression == RIO_COMP_LZW)
-        return RIO_ERR_UNSUPPORTED;
-    int rc = ensure_on_device(r);
-    if (rc) return rc;
-    ReadAtResult res{};
-    uint64_t ro = 0;
-    rc = read_at_impl(r->ctx, r->dfile.as<uint8_t>(), r->size, offset, true, r->seek_len, &res, &ro);
-    if (rc) return rc;
-    if (rec_offset) *rec_offset = ro;
-    return fetch_result(r, res, data, len, is_nil);
+    if (int rc = readat_check(r, data, len, is_nil)) return rc;
+    tl_det = LastDetail{0, 0, offset};
+    const uint64_t seek_len = r->seek_len.load(std::memory_order_relaxed);
+    const ReadAtIndex* x = readat_index(r);
+    uint64_t s = offset;  // the scan's position: a fresh SeekNext from s continues it exactly
+    // with windows of >= 3 bytes the walk is fixed by the first 0x91 at or after s (build_seek_map)
+    if (seek_len >= 3 && s <= r->size && x->n) {
+        const uint64_t k = (uint64_t)(std::lower_bound(x->P.begin(), x->P.end(), s) - x->P.begin());
+        if (k < x->P.size() && x->R[k] != kSeekOther) {
+            const uint64_t i = x->R[k];
+            if (rec_offset) *rec_offset = x->rec_off[i];
+            tl_det.off = x->rec_off[i];
+            return x->record(i, data, len, is_nil);
+        }
+    }
+    for (;;) {
+        uint64_t ro = 0;
+        const int rc = readat_kernel(r, s, true, seek_len, &ro, data, len, is_nil);
+        if (rec_offset) *rec_offset = ro;
+        tl_det.off = rc == RIO_ERR_INVALID_OFFSET ? offset : ro;
+        // gzip: the kernel stops at a trial whose payload needs inflating; a record start is served
+        // from the decoded index (an io.EOF-class one continues the scan), anything else is handed back
+        const uint64_t i = rc == RIO_ERR_UNSUPPORTED && r->compression == RIO_COMP_GZIP ? x->find(ro) : x->n;
+        if (i == x->n) return rc;
+        if (x->flags[i] & RIO_FLAG_EOF) {
+            s = ro + 3;
+            continue;
+        }
+        return x->record(i, data, len, is_nil);
+    }
 }
 
 extern "C" int rio_reader_set_seek_len(rio_reader* r, uint64_t seek_len) {
     if (!r || seek_len == 0) return RIO_ERR_ARG;
-    std::lock_guard<std::mutex> g(r->mu);
-    r->seek_len = seek_len;
+    r->seek_len.store(seek_len, std::memory_order_relaxed);
     return RIO_OK;
 }
 
@@ -1037,7 +1150,7 @@ extern "C" int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, 
         if (value) *value = nullptr;
         if (value_len) *value_len = 0;
         if (is_nil) *is_nil = 0;
-        return (t->data_flags[i] & RIO_FLAG_EOF) ? RIO_EOF_ZERO_TAIL : RIO_ERR_DECOMPRESS;
+        return (t->data_flags[i] & RIO_FLAG_EOF) ? RIO_EOF_CODEC : RIO_ERR_DECOMPRESS;
     }
     const bool nil = (t->data_flags[i] & RIO_FLAG_NIL) != 0;
     if (value) *value = nil ? nullptr : t->data.data() + t->data_off[i];

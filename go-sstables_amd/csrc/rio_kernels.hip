@@ -17,6 +17,8 @@
 // Byte/integer work only: no MFMA. All offsets 64-bit.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "rio_device.h"
 #include "rio_dev_util.h"
 #include "rio_pb.h"
@@ -1151,6 +1153,12 @@ __device__ int read_at_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_
         for (uint64_t k = 0; k < plen; k++) out[k] = pay[k];
         return RIO_OK;
     }
+    if (comp == RIO_COMP_GZIP) {
+        // gzip.NewReader on an empty payload: io.EOF (mmap_reader.go:189-191 wraps it). A payload to
+        // inflate is the host's: it serves record starts from the reader's decoded index and hands
+        // anything else back (r.payload_off / r.len locate it)
+        return plen == 0 ? RIO_EOF_CODEC : RIO_ERR_UNSUPPORTED;
+    }
     uint64_t dl = 0;
     const int k = uvarint_buf(pay, plen, dl);
     if (k <= 0 || dl > 0xFFFFFFFFull || dl > 22ull * (plen - (uint64_t)k) + 64) return RIO_ERR_DECOMPRESS;
@@ -1173,7 +1181,7 @@ __global__ void k_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t*
         comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
         if (ver > RIO_VERSION4 || ver < RIO_VERSION1) e = RIO_ERR_VERSION;
         else if (comp > RIO_COMP_LZW) e = RIO_ERR_COMPRESSION_TYPE;
-        else if (ver < RIO_VERSION3 || comp == RIO_COMP_GZIP || comp == RIO_COMP_LZW) e = RIO_ERR_UNSUPPORTED;
+        else if (ver < RIO_VERSION3 || comp == RIO_COMP_LZW) e = RIO_ERR_UNSUPPORTED;
     }
     if (e == RIO_OK) e = read_at_dev(f, len, ver, comp, off, out, out_cap, r, true);
     r.status = e;
@@ -1212,7 +1220,7 @@ __device__ __forceinline__ int seek_next_t(B& get, uint64_t len, uint64_t off, u
             const uint64_t at = next + i;
             const int te = trial(at);
             if (te != RIO_OK && (te == RIO_ERR_HEADER_CRC || te == RIO_ERR_MAGIC || te == RIO_EOF ||
-                                 te == RIO_EOF_HEADER || te == RIO_EOF_PAYLOAD)) {
+                                 te == RIO_EOF_HEADER || te == RIO_EOF_PAYLOAD || te == RIO_EOF_CODEC)) {
                 i = ix;
                 continue;
             }
@@ -1239,7 +1247,7 @@ __device__ __forceinline__ int file_header_dev(const uint8_t* f, uint64_t len, u
     comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
     if (ver > RIO_VERSION4 || ver < RIO_VERSION1) return RIO_ERR_VERSION;
     if (comp > RIO_COMP_LZW) return RIO_ERR_COMPRESSION_TYPE;
-    if (ver < RIO_VERSION3 || comp == RIO_COMP_GZIP || comp == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;
+    if (ver < RIO_VERSION3 || comp == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;
     return RIO_OK;
 }
 
@@ -1254,6 +1262,208 @@ __global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64
     r.status = e;
     *rec_off = ro;
     *res = r;
+}
+
+// ------------------------------------------------------------------------------------------
+// SeekNext map of a decoded file (rio_reader_seek_next). MMapReader.SeekNext (mmap_reader.go:58-128)
+// visits positions from its offset one by one; only a 0x91 byte changes the walk: 91 X (X != 8d)
+// jumps to p+2, 91 8d Y (Y != 4c) to p+3, and a marker 91 8d 4c runs a trial ReadNextAt whose
+// io.EOF / magic / header-CRC class continues at p+3 while anything else ends the call. With windows
+// of >= 3 bytes the walk does not depend on where windows start (a marker cut by a window end is
+// re-read from its start). So the answer from offset s is fixed by the first 0x91 at or after s:
+// P = every 0x91 position in file order, R[k] = the walk's end from P[k] — a record j of the decoded
+// sequence (its trial is record j, answered from the decoded arena) or kSeekOther (a trial outside
+// the sequence that ends the walk, a partial marker at the file end, or a walk that runs off the
+// last 0x91: the single-record kernel answers those). Built once per reader:
+//   k_count91 / k_scan_segs / k_list91: P (a wave per 4 KiB segment, ballot-free lane prefix);
+//   k_seek_step: each position's own step (terminal, or the index of the next 0x91 visited);
+//   k_seek_jump: pointer jumping to each walk's end (log2 of the longest walk rounds).
+// ------------------------------------------------------------------------------------------
+constexpr uint64_t kSeekOther = ~0ull >> 1;
+constexpr uint64_t kSeekTerm = 1ull << 63;
+constexpr uint32_t kSegBytes = 4096;
+
+__device__ __forceinline__ uint32_t count91(const uint8_t* f, uint64_t at, uint64_t len, uint32_t* mask4) {
+    // bytes [at, at + 64) equal to 0x91 (bounded by len); mask4[q]: bit j = byte 16q + j. Loads stay
+    // below len + RIO_DEVICE_PAD: a lane starting at or past len reads nothing
+    uint32_t c = 0;
+    if (at >= len) {
+        mask4[0] = mask4[1] = mask4[2] = mask4[3] = 0;
+        return 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 v = *reinterpret_cast<const uint4*>(f + at + 16 * q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                m |= (((w[t] >> (8 * j)) & 0xFFu) == 0x91u ? 1u : 0u) << (4 * t + j);
+        const uint64_t base = at + 16 * q;
+        if (base + 16 > len) m &= base >= len ? 0u : ((1u << (len - base)) - 1u);
+        mask4[q] = m;
+        c += __builtin_popcount(m);
+    }
+    return c;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t& total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += lane >= (uint32_t)d ? y : 0u;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__global__ void __launch_bounds__(256) k_count91(const uint8_t* f, uint64_t len, uint64_t nseg, uint64_t* cnt) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t seg = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (seg >= nseg) return;
+    uint32_t m[4];
+    const uint32_t c = count91(f, seg * kSegBytes + lane * 64, len, m);
+    uint32_t total;
+    (void)wave_excl_sum(c, lane, total);
+    if (lane == 0) cnt[seg] = total;
+}
+
+// exclusive prefix sum of cnt[0, n) in place, one block; cnt[n] = the total
+__global__ void __launch_bounds__(1024) k_scan_segs(uint64_t* cnt, uint64_t n) {
+    __shared__ uint64_t part[1024];
+    const uint64_t per = (n + 1023) / 1024, a = threadIdx.x * per, b = a + per < n ? a + per : n;
+    uint64_t sum = 0;
+    for (uint64_t i = a; i < b; i++) sum += cnt[i];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[threadIdx.x] - sum;
+    for (uint64_t i = a; i < b; i++) {
+        const uint64_t c = cnt[i];
+        cnt[i] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) cnt[n] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_list91(const uint8_t* f, uint64_t len, uint64_t nseg, const uint64_t* base,
+                                                uint64_t* P) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t seg = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (seg >= nseg) return;
+    const uint64_t at = seg * kSegBytes + lane * 64;
+    uint32_t m[4];
+    const uint32_t c = count91(f, at, len, m);
+    uint32_t total;
+    uint64_t o = base[seg] + wave_excl_sum(c, lane, total);
+    for (int q = 0; q < 4; q++)
+        for (uint32_t x = m[q]; x; x &= x - 1) P[o++] = at + 16 * q + __builtin_ctz(x);
+}
+
+__device__ __forceinline__ uint64_t lower_u64(const uint64_t* a, uint64_t n, uint64_t key) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) k_seek_step(const uint8_t* f, uint64_t len, const uint64_t* P, uint64_t K,
+                                                   const uint64_t* rec_off, const uint8_t* flags, uint64_t n,
+                                                   uint64_t* step) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t ver = 0, comp = 0;
+    const int he = file_header_dev(f, len, ver, comp);
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
+        const uint64_t p = P[k];
+        uint64_t out = kSeekTerm | kSeekOther, c = 0;
+        if (he == RIO_OK && p + 1 < len) {
+            if (f[p + 1] != 0x8D) {
+                c = p + 2;
+            } else if (p + 2 < len) {
+                if (f[p + 2] != 0x4C) {
+                    c = p + 3;
+                } else {
+                    const uint64_t j = lower_u64(rec_off, n, p);
+                    if (j < n && rec_off[j] == p) {
+                        if (flags[j] & RIO_FLAG_EOF) c = p + 3;  // its trial is io.EOF class: the walk goes on
+                        else out = kSeekTerm | j;
+                    } else {  // a marker outside the decoded sequence: its own trial, as the reference runs it
+                        ReadAtResult r{};
+                        Hdr h;
+                        RawBytes raw{f};
+                        const int te = read_at_locate(raw, len, ver, comp, p, r, h);
+                        const bool benign = te == RIO_ERR_HEADER_CRC || te == RIO_ERR_MAGIC || te == RIO_EOF ||
+                                            te == RIO_EOF_HEADER || te == RIO_EOF_PAYLOAD ||
+                                            (te == RIO_OK && !r.nil && comp == RIO_COMP_GZIP && r.len == 0);
+                        if (benign) c = p + 3;
+                    }
+                }
+            }
+        }
+        if (c) {
+            const uint64_t nk = lower_u64(P, K, c);
+            out = nk < K ? nk : (kSeekTerm | kSeekOther);  // no 0x91 left: the walk reaches the file end
+        }
+        step[k] = out;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_seek_jump(const uint64_t* in, uint64_t* out, uint64_t K) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
+        const uint64_t v = in[k];
+        out[k] = (v & kSeekTerm) ? v : in[v];
+    }
+}
+
+// P and R (host vectors) of a device-resident file and its decoded record offsets / flags
+int build_seek_map(const uint8_t* f, uint64_t len, const uint64_t* rec_off, const uint8_t* flags, uint64_t n,
+                   std::vector<uint64_t>& P, std::vector<uint64_t>& R, hipStream_t s) {
+    P.clear();
+    R.clear();
+    const uint64_t nseg = (len + kSegBytes - 1) / kSegBytes;
+    if (nseg == 0) return 0;
+    uint64_t *cnt = nullptr, *dP = nullptr, *a = nullptr, *b = nullptr;
+    auto done = [&](int rc) {
+        if (cnt) (void)hipFree(cnt);
+        if (dP) (void)hipFree(dP);
+        if (a) (void)hipFree(a);
+        if (b) (void)hipFree(b);
+        return rc;
+    };
+    if (hipMalloc(&cnt, (nseg + 1) * 8) != hipSuccess) return done(-1);
+    const unsigned gs = (unsigned)((nseg + 3) / 4);
+    hipLaunchKernelGGL(k_count91, dim3(gs), dim3(256), 0, s, f, len, nseg, cnt);
+    hipLaunchKernelGGL(k_scan_segs, dim3(1), dim3(1024), 0, s, cnt, nseg);
+    uint64_t K = 0;
+    if (hipMemcpyAsync(&K, cnt + nseg, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return done(-1);
+    if (K == 0) return done(0);
+    if (hipMalloc(&dP, K * 8) != hipSuccess || hipMalloc(&a, K * 8) != hipSuccess || hipMalloc(&b, K * 8) != hipSuccess)
+        return done(-1);
+    hipLaunchKernelGGL(k_list91, dim3(gs), dim3(256), 0, s, f, len, nseg, cnt, dP);
+    hipLaunchKernelGGL(k_seek_step, dim3(1024), dim3(256), 0, s, f, len, dP, K, rec_off, flags, n, a);
+    for (int round = 0; round < 40; round++) {  // walks of up to 2^40 steps
+        hipLaunchKernelGGL(k_seek_jump, dim3(1024), dim3(256), 0, s, a, b, K);
+        std::swap(a, b);
+    }
+    P.resize(K);
+    R.resize(K);
+    if (hipMemcpyAsync(P.data(), dP, K * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(R.data(), a, K * 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return done(-1);
+    for (uint64_t& r : R) r = (r & kSeekTerm) ? (r & ~kSeekTerm) : kSeekOther;  // unfinished walks: the kernel
+    return done(hipGetLastError() == hipSuccess ? 0 : -1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1296,7 +1506,7 @@ __device__ __forceinline__ int index_find_at(WinBytes& wb, uint64_t len, uint32_
 }
 
 __device__ __forceinline__ bool eof_class(int e) {
-    return e == RIO_EOF || e == RIO_EOF_ZERO_TAIL || e == RIO_EOF_HEADER || e == RIO_EOF_PAYLOAD;
+    return e == RIO_EOF || e == RIO_EOF_ZERO_TAIL || e == RIO_EOF_HEADER || e == RIO_EOF_PAYLOAD || e == RIO_EOF_CODEC;
 }
 
 // minimum waves per SIMD for k_index_search (0 = the compiler's choice: 129 VGPRs, 3 waves). Measured on

@@ -370,7 +370,7 @@ extern "C" void rio_replay_free(rio_replay* r) {
 namespace {
 
 bool cut_type(int st) {
-    return st == RIO_EOF || st == RIO_EOF_ZERO_TAIL || st == RIO_EOF_HEADER || st == RIO_EOF_PAYLOAD ||
+    return st == RIO_EOF || st == RIO_EOF_ZERO_TAIL || st == RIO_EOF_HEADER || st == RIO_EOF_PAYLOAD || st == RIO_EOF_CODEC ||
            st == RIO_ERR_UNEXPECTED_EOF;
 }
 

@@ -37,8 +37,9 @@ RIO_ERR_HIP = 18
 RIO_ERR_STATE = 19
 RIO_ERR_IO = 20
 RIO_ERR_PROTO = 21
+RIO_EOF_CODEC = 22
 
-EOF_CLASS = (RIO_EOF, RIO_EOF_ZERO_TAIL, RIO_EOF_HEADER, RIO_EOF_PAYLOAD)
+EOF_CLASS = (RIO_EOF, RIO_EOF_ZERO_TAIL, RIO_EOF_HEADER, RIO_EOF_PAYLOAD, RIO_EOF_CODEC)
 
 RIO_FLAG_NIL = 1
 RIO_FLAG_CORRUPT = 2

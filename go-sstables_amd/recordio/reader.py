@@ -23,7 +23,7 @@ FileHeaderSizeBytes = 8
 
 def _base_error(status: int, d0: int = 0, d1: int = 0) -> GoError:
     """The innermost error value the reference produces for a status class."""
-    if status in (L.RIO_EOF, L.RIO_EOF_HEADER, L.RIO_EOF_PAYLOAD, L.RIO_EOF_ZERO_TAIL):
+    if status in (L.RIO_EOF, L.RIO_EOF_HEADER, L.RIO_EOF_PAYLOAD, L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_CODEC):
         return EOF
     if status == L.RIO_ERR_UNEXPECTED_EOF:
         return ErrUnexpectedEOF
@@ -60,8 +60,8 @@ def _open_error(status: int, path: str, d0: int, what: str, size: int = -1) -> G
 
 def read_next_error(rc: int, path: str, d0: int, d1: int) -> GoError:
     """FileReader.ReadNext's error for a terminal status of the whole-file decode (file_reader.go:61-131)."""
-    if rc == L.RIO_EOF_ZERO_TAIL:
-        return EOF  # file_reader.go:89-90: bare io.EOF
+    if rc in (L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_CODEC):
+        return EOF  # file_reader.go:89-90 (zero tail) / :119-121 (gzip's io.EOF): bare io.EOF
     if rc == L.RIO_ERR_MAGIC:
         return wrap(f"error while parsing record header for zeros towards the file end of '{path}'",
                     MagicNumberMismatchErr)
@@ -189,9 +189,9 @@ class MMapReader(_Reader):
                         GoError(f"mmap: invalid ReadAt offset {offset}"))
         if rc == L.RIO_EOF_PAYLOAD:
             return wrap(f"failed reading record at offset {offset} in mmap reader for '{self.path}'", EOF)
-        if rc == L.RIO_ERR_DECOMPRESS:
+        if rc in (L.RIO_ERR_DECOMPRESS, L.RIO_EOF_CODEC):  # mmap_reader.go:189-191
             return wrap(f"failed decompressing record at offset {offset} in mmap reader for '{self.path}'",
-                        ErrCorrupt)
+                        ErrCorrupt if rc == L.RIO_ERR_DECOMPRESS else EOF)
         return wrap(f"failed reading record header at offset {offset} in mmap reader for '{self.path}'",
                     _base_error(rc, d0, d1))
 

@@ -28,7 +28,7 @@ from recordio.writer import NewFileWriter
 DefaultMaxWalSize = 128 * 1024 * 1024  # write_ahead_log.go:9
 defaultWalSuffix = ".wal"  # appender.go:10
 defaultWalFilePattern = "%06d" + defaultWalSuffix  # appender.go:11
-_EOF_CLASS = (L.RIO_OK, L.RIO_EOF, L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_HEADER, L.RIO_EOF_PAYLOAD)
+_EOF_CLASS = (L.RIO_OK, L.RIO_EOF, L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_HEADER, L.RIO_EOF_PAYLOAD, L.RIO_EOF_CODEC)
 
 
 @dataclass

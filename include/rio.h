@@ -59,9 +59,8 @@ typedef enum rio_status {
     /* header read hit EOF before its first byte: FileReader wraps io.EOF once
      * (file_reader.go:93), MMapReader.ReadNextAt returns a bare io.EOF (mmap_reader.go:153-155) */
     RIO_EOF = 1,
-    /* FileReader only: a bare io.EOF. Magic mismatch and every byte after the consumed magic varint
-     * is zero (DirectIO padding, file_reader.go:76-91); or, from rio_reader_read_next / rio_sst_entry,
-     * a RIO_FLAG_EOF record (gzip's io.EOF passed through unwrapped, :119-121) */
+    /* FileReader only: magic mismatch and every byte after the consumed magic varint is zero
+     * (DirectIO padding) -> bare io.EOF (file_reader.go:76-91) */
     RIO_EOF_ZERO_TAIL = 2,
     /* io.EOF on the first byte of a later header field (nil byte / u / c / crc varint) */
     RIO_EOF_HEADER = 3,
@@ -86,7 +85,11 @@ typedef enum rio_status {
     RIO_ERR_STATE = 19,           /* reader not opened / already closed / already opened */
     RIO_ERR_IO = 20,              /* file open / mmap / read failure */
     RIO_ERR_PROTO = 21,           /* proto.Unmarshal of an IndexEntry failed (invalid wire format) */
-    RIO_STATUS_COUNT_ = 21
+    /* the codec returned io.EOF: gzip.NewReader on an empty payload (gzip_compression.go:56-59).
+     * FileReader.ReadNext returns it bare (file_reader.go:119-121), MMapReader.ReadNextAt wraps it
+     * once ("failed decompressing record", mmap_reader.go:189-191); errors.Is(err, io.EOF) holds */
+    RIO_EOF_CODEC = 22,
+    RIO_STATUS_COUNT_ = 22
 } rio_status;
 
 const char* rio_strerror(int status);
@@ -218,7 +221,7 @@ int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, co
  * data record i (is_nil for a nil record), the stored valueOffset and checksum and the value's CRC-64.
  * Returns RIO_OK, RIO_ERR_ARG for i >= n_entries, the data file's terminal status when data record i
  * does not exist (the scan's dataReader.ReadNext error; key and checksum are still filled), or
- * RIO_ERR_DECOMPRESS / RIO_EOF_ZERO_TAIL when data record i is flagged RIO_FLAG_CORRUPT / RIO_FLAG_EOF. */
+ * RIO_ERR_DECOMPRESS / RIO_EOF_CODEC when data record i is flagged RIO_FLAG_CORRUPT / RIO_FLAG_EOF. */
 int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, uint64_t* key_len, const uint8_t** value,
                   uint64_t* value_len, int* is_nil, uint64_t* value_offset, uint64_t* checksum, uint64_t* crc);
 void rio_sst_free(rio_sst* t);
@@ -339,7 +342,7 @@ int rio_reader_header(rio_reader* r, uint32_t* version, uint32_t* compression);
 uint64_t rio_reader_size(rio_reader* r);
 /* detail values of the last error (HEADER_CRC: expected/actual; VERSION etc.: value) */
 void rio_reader_last_detail(rio_reader* r, uint64_t* detail0, uint64_t* detail1, uint64_t* offset);
-/* ReaderI. read_next on a record that does not decompress returns RIO_ERR_DECOMPRESS (RIO_EOF_ZERO_TAIL
+/* ReaderI. read_next on a record that does not decompress returns RIO_ERR_DECOMPRESS (RIO_EOF_CODEC
  * for gzip's empty payload) and the next call returns the record after it; skip_next passes over it. */
 int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil);
 int rio_reader_skip_next(rio_reader* r);

@@ -281,7 +281,7 @@ static int gzip_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* 
     *out_len = 0;
     /* gzip.NewReader(empty) returns a bare io.EOF (gzip_compression.go:56-59), which ReadNext
      * passes through unwrapped (file_reader.go:118-121) and ReadNextAt wraps once: io.EOF class */
-    if (n == 0) return RIO_EOF_PAYLOAD;
+    if (n == 0) return RIO_EOF_CODEC;
     uint64_t cap = n * 4 + 64, used = 0;
     uint8_t* dst = (uint8_t*)malloc(cap);
     z_stream z;
@@ -438,7 +438,7 @@ int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res)
             uint8_t* dec = NULL;
             uint64_t dlen = 0;
             e = decompress(res->compression, pay, plen, &dec, &dlen);
-            if (e == RIO_ERR_DECOMPRESS || (e == RIO_EOF_PAYLOAD && res->compression == RIO_COMP_GZIP)) {
+            if (e == RIO_ERR_DECOMPRESS || e == RIO_EOF_CODEC) {
                 /* ReadNext returns the codec error; the payload is consumed and the loop goes on */
                 const uint64_t rsv = bad_reserve(res->compression, pay, plen);
                 uint8_t* z = (uint8_t*)calloc(rsv ? rsv : 1, 1);
@@ -626,7 +626,7 @@ uint64_t orc_parallel_read_at(const uint8_t* f, uint64_t len, const uint64_t* re
 /* status helpers shared with the product's vocabulary (rio.h); the oracle keeps its own copy so
  * the library under test is never linked into the checker. */
 int rio_status_is_eof(int s) {
-    return s == RIO_EOF || s == RIO_EOF_ZERO_TAIL || s == RIO_EOF_HEADER || s == RIO_EOF_PAYLOAD;
+    return s == RIO_EOF || s == RIO_EOF_ZERO_TAIL || s == RIO_EOF_HEADER || s == RIO_EOF_PAYLOAD || s == RIO_EOF_CODEC;
 }
 
 /* ---------------------------------------------------------------------------------------- */

@@ -15,6 +15,7 @@ STATUS = {
     "OK": 0, "EOF": 1, "EOF_ZERO_TAIL": 2, "EOF_HEADER": 3, "EOF_PAYLOAD": 4, "UNEXPECTED_EOF": 5, "MAGIC": 6,
     "HEADER_CRC": 7, "VARINT_OVERFLOW": 8, "HEADER_TOO_LONG": 9, "DECOMPRESS": 10, "VERSION": 11,
     "COMPRESSION_TYPE": 12, "SHORT_FILE_HEADER": 13, "INVALID_OFFSET": 14, "UNSUPPORTED": 15, "CAPACITY": 16,
+    "EOF_CODEC": 22,
 }
 
 

@@ -37,6 +37,8 @@ def expect_read_next_at(status: int, offset: int, path: str, d0: int = 0, d1: in
         return f"failed reading record {where}: EOF", EOF, 1
     if status == L.RIO_ERR_DECOMPRESS:  # :189-191
         return f"failed decompressing record {where}: snappy: corrupt input", ErrCorrupt, 1
+    if status == L.RIO_EOF_CODEC:  # :189-191 around gzip.NewReader's io.EOF (empty payload)
+        return f"failed decompressing record {where}: EOF", EOF, 1
     raise AssertionError(f"status {status} is not a ReadNextAt error")
 
 

@@ -29,7 +29,7 @@ def test_status_vocabulary():
     lib = L.lib()
     assert lib.rio_strerror(L.RIO_ERR_MAGIC) == b"magic number mismatch"
     assert lib.rio_strerror(L.RIO_ERR_HEADER_CRC) == b"header checksum mismatch"
-    for s in (L.RIO_EOF, L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_HEADER, L.RIO_EOF_PAYLOAD):
+    for s in (L.RIO_EOF, L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_HEADER, L.RIO_EOF_PAYLOAD, L.RIO_EOF_CODEC):
         assert lib.rio_status_is_eof(s)
     for s in (L.RIO_OK, L.RIO_ERR_UNEXPECTED_EOF, L.RIO_ERR_MAGIC, L.RIO_ERR_HEADER_CRC):
         assert not lib.rio_status_is_eof(s)
