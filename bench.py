@@ -41,7 +41,8 @@ CONFIGS = {
     "c2r": (1_000_000, 1024, 2, 0, "C2-ref-random: recordio v4, 1M x 1 KiB snappy records (incompressible)"),
     "c1": (100_000, 1024, 0, 0, "C1: recordio v4, 100k x 1 KiB uncompressed records (ref generator)"),
     "c3": (10_000_000, 64, 2, 1, "C3: recordio v4, 10M x 64 B snappy records (header-bound)"),
-    "c4": (16_384, 65536, 2, 1, "C4: recordio v4, 16384 x 64 KiB snappy records (decompress-bound), one file per GPU"),
+    "c4": (16_384, 65536, 2, 1, "C4: recordio v4, 8 files x 16384 x 64 KiB snappy records (decompress-bound), "
+                                "sharded over the GPUs"),
     "c2g": (1_000_000, 1024, 1, 1, "C2-gzip: recordio v4, 1M x 1 KiB gzip records (text-like), one file per GPU"),
     "wal": (WAL_FILES * WAL_RECORDS_PER_FILE, 1024, 2, 1, "WAL replay: 8 x ~128 MiB snappy WAL files (1 KiB "
                                                           "text-like records) per GPU, sorted, delivered in order"),
@@ -60,6 +61,9 @@ IDX_METRIC = "DiskKeyIndex lookups/s (device-resident index.rio, batched Get)"
 ENC_METRIC = "recordio v4 encode GiB/s of records (device-resident, golang/snappy block format)"
 PCIE_PEAK_GBPS = 128.0  # PCIe Gen5 x16, both directions (64 GB/s each)
 DECODE_KERNEL = {0: "k_decode_copy", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
+# configs decoded as a fixed file set sharded over the ranks: name -> (files, first seed)
+MULTI_FILE = {"c4": (8, 100)}
+SST_TABLES = 8  # C5: 10M keys in 8 tables of 1.25M
 
 
 def dist_env():
@@ -74,24 +78,25 @@ def shard_files(n_files: int, world: int, rank: int) -> list[int]:
     return [f for f in range(n_files) if f % world == rank]
 
 
-def reduce_max(value: float, world: int, device) -> float:
+def reduce_max(value: float, world: int, device=None) -> float:
+    """Max over ranks of a host float: gloo on the CPU (the data path has no collective at all)."""
     if world == 1:
         return value
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def reduce_sum(value: float, world: int, device) -> float:
+def reduce_sum(value: float, world: int, device=None) -> float:
     if world == 1:
         return value
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -110,30 +115,76 @@ def rank_seed(rank: int) -> int:
     return 1 + rank
 
 
-def cpu_baseline(image, n_records: int, budget_s: float = 20.0) -> dict:
-    """The oracle (oracle/rio_oracle.c, a C restatement of FileReader.ReadNext) on host cores:
-    sequential whole-file decode on 1 core, repeated within a bounded time budget."""
+def host_cores() -> int:
+    """Host threads the CPU baseline may use: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the
+    GPU pool), not the machine's whole count that os.cpu_count() reports there."""
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    n = os.cpu_count() or 1
+    return max(1, min(n, share) if share else n)
+
+
+def cpu_baseline(images, rec_offs=None, n_records=None, budget_s: float = 20.0) -> dict:
+    """The oracle (oracle/rio_oracle.c, a C restatement of the reference reader) on host cores, timed
+    on a bounded sample of the same workload:
+      one core  — FileReader.ReadNext loop over one file (orc_file_reader_decode), sequential;
+      all cores — one file: MMapReader.ReadNextAt record-parallel over its known offset table
+                  (orc_parallel_read_at); several files: file-sharded, one whole-file loop per thread."""
+    import threading
+
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import oracle_py as orc
 
     lib = orc.lib()
-    res = orc.OrcFileResult()
+    image = images[0]
+
+    def one_file(img):
+        res = orc.OrcFileResult()
+        lib.orc_file_reader_decode(img.ctypes.data, img.shape[0], ctypes.byref(res))
+        n = res.n_records
+        lib.orc_file_result_free(ctypes.byref(res))
+        return n
+
     runs, t_total = 0, 0.0
     while runs < 5 and t_total < budget_s:
         t0 = time.perf_counter()
-        lib.orc_file_reader_decode(image.ctypes.data, image.shape[0], ctypes.byref(res))
-        dt = time.perf_counter() - t0
-        ok = res.n_records == n_records
-        lib.orc_file_result_free(ctypes.byref(res))
-        if not ok:
-            raise RuntimeError("oracle baseline decoded a different record count")
+        got = one_file(image)
+        t_total += time.perf_counter() - t0
         runs += 1
-        t_total += dt
-    gib = image.shape[0] / 2**30
-    return {"value": round(gib * runs / t_total, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"full file ({image.shape[0]} B, {n_records} records) x{runs} runs, sequential "
-                      f"FileReader.ReadNext-loop restatement, {os.cpu_count()} host cpus visible, "
-                      f"{_cpu_model()}"}
+        if n_records is not None and got != n_records:
+            raise RuntimeError("oracle baseline decoded a different record count")
+    one = image.shape[0] / 2**30 * runs / t_total
+    cores = host_cores()
+    if len(images) > 1:  # file-sharded over the cores
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=one_file, args=(img,)) for img in images[:cores]]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        dt = time.perf_counter() - t0
+        all_v = sum(img.shape[0] for img in images[:cores]) / 2**30 / dt
+        used = min(cores, len(images))
+        how = f"{used} files decoded concurrently, one thread each (file-sharded)"
+    else:
+        import numpy as np
+
+        ro = np.ascontiguousarray(rec_offs, dtype=np.uint64)
+        runs_a, t_a = 0, 0.0
+        while runs_a < 5 and t_a < budget_s:
+            t0 = time.perf_counter()
+            got = lib.orc_parallel_read_at(image.ctypes.data, image.shape[0], ro.ctypes.data, ro.shape[0], cores)
+            t_a += time.perf_counter() - t0
+            runs_a += 1
+            if not got:
+                raise RuntimeError("oracle parallel ReadNextAt failed")
+        all_v = image.shape[0] / 2**30 * runs_a / t_a
+        used = cores
+        how = f"ReadNextAt over the {ro.shape[0]} known record offsets, {cores} threads, x{runs_a} runs"
+    return {"value": round(all_v, 4), "unit": "GiB/s", "cores": used, "kind": "port",
+            "sample": f"{how}; {os.cpu_count()} cpus visible on the host, CPU share {cores}, {_cpu_model()}",
+            "one_core": {"value": round(one, 4), "unit": "GiB/s", "cores": 1,
+                         "sample": f"one file ({image.shape[0]} B) x{runs} runs, sequential FileReader.ReadNext-loop "
+                                   "restatement"}}
 
 
 def _cpu_model() -> str:
@@ -235,8 +286,11 @@ def sstable_images(n: int, rank: int):
 
 
 def run_sstable(args, world, rank, local, device):
-    """One step = the device work of NewSSTableReader + Scan on one table: decode index.rio, parse
-    every IndexEntry, decode data.rio, CRC-64 every value against its entry (rio_sst_*)."""
+    """One step = the device work of NewSSTableReader + Scan on every table of this rank's shard of
+    the 8-table set (BASELINE configs[4]: 10M keys in 8 tables): decode index.rio, parse every
+    IndexEntry, decode data.rio, CRC-64 every value against its entry (rio_sst_*)."""
+    import threading
+
     import numpy as np
     import torch
 
@@ -244,45 +298,57 @@ def run_sstable(args, world, rank, local, device):
     from recordio.device import DeviceDecoder, to_device_file
 
     n = CONFIGS["c5"][0]
-    index_img, data_img = sstable_images(n, rank)
-    d_index, li = to_device_file(index_img, local)
-    d_data, ld = to_device_file(data_img, local)
+    mine = shard_files(SST_TABLES, world, rank)
     dec = DeviceDecoder(local)
-    ib, ii = dec.decode(d_index, li)
-    db, di = dec.decode(d_data, ld)
-    if ii["n_records"] != n or di["n_records"] != n:
-        raise RuntimeError(f"sstable decode failed: {ii} {di}")
     lib = L.lib()
     i64 = dict(dtype=torch.int64, device=device)
-    key_off, key_len, value_off, checksum, crc = (torch.empty(n, **i64) for _ in range(5))
-    pres, vres = torch.empty(2, **i64), torch.empty(2, **i64)
     # a real stream: the null stream's handle (0) would send the calls to the ctx's own stream and
     # the stage events would not bracket them
     stream = torch.cuda.Stream(device=device)
     sp = ctypes.c_void_p(stream.cuda_stream)
+    tables = []
+    for t in mine:
+        index_img, data_img = sstable_images(n, t)
+        T = {"index_img": index_img, "data_img": data_img}
+        T["d_index"], T["li"] = to_device_file(index_img, local)
+        T["d_data"], T["ld"] = to_device_file(data_img, local)
+        T["ib"], ii = dec.decode(T["d_index"], T["li"])
+        T["db"], di = dec.decode(T["d_data"], T["ld"])
+        if ii["n_records"] != n or di["n_records"] != n:
+            raise RuntimeError(f"sstable decode failed: {ii} {di}")
+        T["nb_d"] = di["total_out_bytes"]
+        for k in ("key_off", "key_len", "value_off", "checksum", "crc"):
+            T[k] = torch.empty(n, **i64)
+        T["pres"], T["vres"] = torch.empty(2, **i64), torch.empty(2, **i64)
+        tables.append(T)
     torch.cuda.synchronize(device)
 
     def step(ev=None):
-        marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if ev is not None else None
-        if marks: marks[0].record(stream)
-        dec.launch(d_index, li, ib, stream)
-        if marks: marks[1].record(stream)
-        lib.rio_sst_index_parse(dec.ctx, ib.out.data_ptr(), ib.out_off.data_ptr(), n, key_off.data_ptr(),
-                                key_len.data_ptr(), value_off.data_ptr(), checksum.data_ptr(), pres.data_ptr(), sp)
-        if marks: marks[2].record(stream)
-        dec.launch(d_data, ld, db, stream)
-        if marks: marks[3].record(stream)
-        lib.rio_sst_validate(dec.ctx, db.out.data_ptr(), db.out_off.data_ptr(), db.rec_off.data_ptr(), n,
-                             value_off.data_ptr(), checksum.data_ptr(), n, crc.data_ptr(), vres.data_ptr(), sp)
-        if marks:
-            marks[4].record(stream)
-            ev.append(marks)
+        for T in tables:
+            marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if ev is not None else None
+            if marks: marks[0].record(stream)
+            dec.launch(T["d_index"], T["li"], T["ib"], stream)
+            if marks: marks[1].record(stream)
+            lib.rio_sst_index_parse(dec.ctx, T["ib"].out.data_ptr(), T["ib"].out_off.data_ptr(), n,
+                                    T["key_off"].data_ptr(), T["key_len"].data_ptr(), T["value_off"].data_ptr(),
+                                    T["checksum"].data_ptr(), T["pres"].data_ptr(), sp)
+            if marks: marks[2].record(stream)
+            dec.launch(T["d_data"], T["ld"], T["db"], stream)
+            if marks: marks[3].record(stream)
+            lib.rio_sst_validate(dec.ctx, T["db"].out.data_ptr(), T["db"].out_off.data_ptr(),
+                                 T["db"].rec_off.data_ptr(), n, T["value_off"].data_ptr(), T["checksum"].data_ptr(), n,
+                                 T["crc"].data_ptr(), T["vres"].data_ptr(), sp)
+            if marks:
+                marks[4].record(stream)
+                ev.append(marks)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(device)
-    if int(pres[0].item()) != -1 or int(vres[0].item()) != -1 or int(vres[1].item()) != -1:
-        raise RuntimeError(f"sstable validation failed: {pres.tolist()} {vres.tolist()}")
+    for T in tables:
+        pres, vres = T["pres"], T["vres"]
+        if int(pres[0].item()) != -1 or int(vres[0].item()) != -1 or int(vres[1].item()) != -1:
+            raise RuntimeError(f"sstable validation failed: {pres.tolist()} {vres.tolist()}")
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(device)
@@ -298,43 +364,63 @@ def run_sstable(args, world, rank, local, device):
         step(ev)
     torch.cuda.synchronize(device)
     names = ("decode_index", "parse_index", "decode_data", "validate")
-    stage = {nm: float(np.mean([m[k].elapsed_time(m[k + 1]) for m in ev])) for k, nm in enumerate(names)}
-    total_in = li + ld
+    nt = max(1, len(tables))
+    # per table (means over tables and the 3 timed passes)
+    stage = {nm: float(np.mean([m[k].elapsed_time(m[k + 1]) for m in ev])) if ev else 0.0 for k, nm in enumerate(names)}
+    total_in = sum(T["li"] + T["ld"] for T in tables)
     value, ms_per_step, _ = job_throughput(dt, total_in, args.steps, world, device)
-    nb_d = di["total_out_bytes"]
+    li = tables[0]["li"] if tables else 0
+    ld = tables[0]["ld"] if tables else 0
+    nb_d = tables[0]["nb_d"] if tables else 0
     # dominant stage: the data decode (C2-ref-random shape) or the CRC-64 pass over the values
     alg = {"decode_data": ld + nb_d + 17 * n + 8, "validate": nb_d + 8 * 5 * n}
     dom = max(alg, key=lambda k: stage[k])
-    achieved = alg[dom] / (stage[dom] * 1e-3) / 1e9
+    achieved = alg[dom] / (stage[dom] * 1e-3) / 1e9 if stage[dom] else 0.0
     line = {
         "metric": SST_METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic: SHA1 keys, one random 1 KiB value (benchmark/sstable_read_test.go shape), one table per rank",
-        "config": {"workload": CONFIGS["c5"][4], "entries": n, "index_bytes": li, "data_bytes": ld,
-                   "decoded_value_bytes": nb_d, "parallelism": f"table-sharded x{world}, no data-path collectives"},
+        "data": f"synthetic: SHA1 keys, one random 1 KiB value (benchmark/sstable_read_test.go shape), {SST_TABLES} "
+                "tables sharded over the ranks",
+        "config": {"workload": CONFIGS["c5"][4], "entries_per_table": n, "tables_this_rank": len(tables),
+                   "index_bytes": li, "data_bytes": ld, "decoded_value_bytes": nb_d,
+                   "parallelism": f"table-sharded x{world} ({SST_TABLES} tables), no data-path collectives"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": dom,
                      "kernel_ms": round(stage[dom], 4), "alg_bytes_per_launch": alg[dom]},
-        "stages_ms": {k: round(v, 4) for k, v in stage.items()},
+        "stages_ms_per_table": {k: round(v, 4) for k, v in stage.items()},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and tables:
         sys.path.insert(0, os.path.join(HERE, "tests"))
         import oracle_py as orc
 
         olib = orc.lib()
-        bad = ctypes.c_uint64()
-        runs, t_total = 0, 0.0
-        while runs < 3 and t_total < 20.0:
-            t1 = time.perf_counter()
-            got = olib.orc_sst_scan(index_img.ctypes.data, li, data_img.ctypes.data, ld, ctypes.byref(bad))
-            t_total += time.perf_counter() - t1
-            runs += 1
-            if got != n:
-                raise RuntimeError("oracle sstable scan disagreed")
-        line["cpu_baseline"] = {"value": round(total_in / 2**30 * runs / t_total, 4), "unit": "GiB/s", "cores": 1,
-                                "kind": "port", "sample": f"full table ({n} entries, {total_in} B) x{runs} runs: "
-                                f"oracle index load + CRC-64 validation + data decode, {_cpu_model()}"}
+
+        def scan(T, out):
+            bad = ctypes.c_uint64()
+            out.append(olib.orc_sst_scan(T["index_img"].ctypes.data, T["li"], T["data_img"].ctypes.data, T["ld"],
+                                         ctypes.byref(bad)))
+
+        one, t1 = [], time.perf_counter()
+        scan(tables[0], one)
+        t_one = time.perf_counter() - t1
+        cores = host_cores()
+        got, t1 = [], time.perf_counter()
+        th = [threading.Thread(target=scan, args=(T, got)) for T in tables[:cores]]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        t_all = time.perf_counter() - t1
+        if one != [n] or got != [n] * len(th):
+            raise RuntimeError("oracle sstable scan disagreed")
+        in_all = sum(T["li"] + T["ld"] for T in tables[:cores])
+        line["cpu_baseline"] = {
+            "value": round(in_all / 2**30 / t_all, 4), "unit": "GiB/s", "cores": len(th), "kind": "port",
+            "sample": f"{len(th)} tables scanned concurrently, one thread each (oracle index load + CRC-64 validation "
+                      f"+ data decode); {os.cpu_count()} cpus visible, CPU share {cores}, {_cpu_model()}",
+            "one_core": {"value": round((tables[0]["li"] + tables[0]["ld"]) / 2**30 / t_one, 4), "unit": "GiB/s",
+                         "cores": 1, "sample": f"one table ({n} entries) scanned once"}}
     if rank == 0:
         print(json.dumps(line), flush=True)
 
@@ -743,7 +829,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group(backend="nccl", device_id=device)
+        # gloo on the host: the barrier and the max/sum over ranks are the job's only collectives
+        # (the decode path has none: files are sharded, north_star "no RCCL")
+        dist.init_process_group(backend="gloo")
 
     if args.config in ("c5", "wal", "idx", "enc", "readat"):
         {"c5": run_sstable, "wal": run_wal, "idx": run_index, "enc": run_encode, "readat": run_readat}[args.config](
@@ -758,26 +846,43 @@ def main():
 
     n_rec, rec_len, comp, kind, desc = CONFIGS[args.config]
     threads = min(16, os.cpu_count() or 1)
-    # one file per GPU (rank-seeded), generated on the host, then resident in HBM
-    image = generate(n_rec, rec_len, comp, kind=kind, seed=rank_seed(rank), threads=threads)
-    d_file, length = to_device_file(image, local)
+    # C4 (BASELINE configs[3]): a fixed set of 8 files sharded over the ranks, decoded per step by
+    # one rio_device_decode_batch call; the other configs: one rank-seeded file per GPU
+    if args.config in MULTI_FILE:
+        n_files, seed0 = MULTI_FILE[args.config]
+        mine = shard_files(n_files, world, rank)
+        seeds = [seed0 + f for f in mine]
+    else:
+        mine, seeds = [rank], [rank_seed(rank)]
+    images = [generate(n_rec, rec_len, comp, kind=kind, seed=sd, threads=threads) for sd in seeds]
+    files = [to_device_file(img, local) for img in images]
     dec = DeviceDecoder(local)
-    probe = dec.alloc(0, 0)
-    dec.launch(d_file, length, probe)
-    torch.cuda.synchronize(device)
-    pi = dec.info(probe)
-    if pi["status"] != L.RIO_ERR_CAPACITY:
-        raise RuntimeError(f"unexpected probe status {pi}")
-    n, nb = pi["n_records"], pi["total_out_bytes"]
-    bufs = dec.alloc(n, nb)
     stream = torch.cuda.current_stream(device)
+    batch = args.config in MULTI_FILE
+    if batch:
+        outs = dec.decode_batch(files) if files else []
+        bufs = [b for b, _ in outs]
+
+        def step():
+            if files:
+                dec.launch_batch(files, bufs, stream)
+    else:
+        b0, _ = dec.decode(*files[0])
+        bufs = [b0]
+
+        def step():
+            dec.launch(files[0][0], files[0][1], bufs[0], stream)
 
     for _ in range(args.warmup):
-        dec.launch(d_file, length, bufs, stream)
+        step()
     torch.cuda.synchronize(device)
-    info = dec.info(bufs)
-    if info["status"] != L.RIO_EOF or info["n_records"] != n_rec:
-        raise RuntimeError(f"decode failed: {info}")
+    infos = [dec.info(b) for b in bufs]
+    for info in infos:
+        if info["status"] != L.RIO_EOF or info["n_records"] != n_rec:
+            raise RuntimeError(f"decode failed: {info}")
+    length = sum(ln for _, ln in files)  # input bytes of this rank per step
+    n = sum(i["n_records"] for i in infos)
+    nb = sum(i["total_out_bytes"] for i in infos)
 
     L.lib().rio_ctx_set_timing(dec.ctx, args.steps)
     if world > 1:
@@ -785,12 +890,12 @@ def main():
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        dec.launch(d_file, length, bufs, stream)
+        step()
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     if world > 1:
         torch.distributed.barrier()
-    stage = dec.stage_ms()  # per-stage HIP-event means over the timed steps
+    stage = dec.stage_ms() if files else []  # per-stage HIP-event means over the timed steps
     L.lib().rio_ctx_set_timing(dec.ctx, 1)
 
     value, ms_per_step, dt_max = job_throughput(dt, length, args.steps, world, device)
@@ -799,12 +904,12 @@ def main():
     # cache. A second pass writes 1 GiB between decodes (outside the per-stage HIP events) and
     # reports the cold-cache stage times beside the headline.
     mall_flushed = None
-    if length + nb < (512 << 20):
+    if files and length + nb < (512 << 20):
         evict = torch.empty(1 << 30, dtype=torch.uint8, device=device)
         L.lib().rio_ctx_set_timing(dec.ctx, args.steps)
         for _ in range(args.steps):
             evict.fill_(1)
-            dec.launch(d_file, length, bufs, stream)
+            step()
         torch.cuda.synchronize(device)
         cold = dec.stage_ms()
         L.lib().rio_ctx_set_timing(dec.ctx, 1)
@@ -818,7 +923,7 @@ def main():
     # roofline of the dominant kernel (Snappy / copy decode): algorithmic bytes per launch =
     # input file bytes (headers + payloads read once) + decoded bytes written once
     # + 8(N+1) out_off + 8N rec_off + N flags read
-    alg_bytes = length + nb + 8 * (n + 1) + 8 * n + n
+    alg_bytes = length + nb + 8 * (n + len(files)) + 8 * n + n
     decode_ms = stage[3] if len(stage) == 4 else float("nan")
     achieved = alg_bytes / (decode_ms * 1e-3) / 1e9
     traffic = None
@@ -831,6 +936,15 @@ def main():
         except (OSError, ValueError):
             traffic = None
     pipe_ms = sum(stage) if stage else float("nan")
+    if comp == 2 and kind == 0:
+        kernel = "k_snappy_literal"  # ref-random records are each one literal: the copy path decodes them
+    elif comp == 2 and rec_len >= int(os.environ.get("RIO_COOP_MIN", str(1 << 56)), 0):
+        kernel = "k_snappy_coop_batch" if batch else "k_snappy_coop"  # wave-per-record decoder (opt-in)
+    elif comp == 2 and batch:
+        kernel = "k_snappy_pipe_batch"
+    else:
+        kernel = DECODE_KERNEL[comp]
+    total_files = MULTI_FILE[args.config][0] if batch else world
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -840,31 +954,33 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if batch else "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: seeded text-like Zipf-word records (snappy ratio ~0.55), one file per rank",
+        "data": "synthetic: seeded text-like Zipf-word records (snappy ratio ~0.55)" +
+                (f", {total_files} files (seeds {MULTI_FILE[args.config][1]}..) sharded over the ranks" if batch
+                 else ", one file per rank"),
         "config": {"workload": desc, "records": n, "record_bytes": rec_len, "file_bytes": length,
                    "decoded_bytes": nb, "compression": {0: "none", 1: "gzip", 2: "snappy"}[comp],
-                   "parallelism": f"file-sharded x{world}, no data-path collectives"},
+                   "files_this_rank": len(files),
+                   "parallelism": f"file-sharded x{world} ({total_files} files), no data-path collectives"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     # ref-random records are each one literal: the copy path (k_snappy_literal) decodes them
-                     "kernel": "k_snappy_literal" if (comp == 2 and kind == 0) else DECODE_KERNEL[comp],
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": kernel,
                      "kernel_ms": round(decode_ms, 4), "alg_bytes_per_launch": alg_bytes},
         "stages_ms": {"walk": round(stage[0], 4), "scan": round(stage[1], 4), "place": round(stage[2], 4),
                       "decode": round(stage[3], 4)} if len(stage) == 4 else None,
-        "pipeline_roofline_frac": round(alg_bytes / (pipe_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "pipeline_roofline_frac": round(alg_bytes / (pipe_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if stage else None,
         # also output GiB/s and records/s (whole job, same timed region as `value`)
-        "output_GiBps": round(value * nb / length, 3),
-        "Mrecords_per_s": round(value * 2**30 / length * n / 1e6, 2),
+        "output_GiBps": round(value * nb / length, 3) if length else None,
+        "Mrecords_per_s": round(value * 2**30 / length * n / 1e6, 2) if length else None,
     }
     if mall_flushed:
         line["mall_flushed"] = mall_flushed
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(image, n_rec)
-    if rank == 0 and world == 1 and not args.no_e2e:
-        line["e2e"] = e2e_rate(image, nb)
+        rec_offs = None if batch else bufs[0].rec_off[:n].cpu().numpy()
+        line["cpu_baseline"] = cpu_baseline(images, rec_offs, n_rec)
+    if rank == 0 and world == 1 and not args.no_e2e and not batch:
+        line["e2e"] = e2e_rate(images[0], nb)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

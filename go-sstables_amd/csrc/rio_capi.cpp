@@ -33,6 +33,7 @@
 namespace rio {
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* key_off,
                             uint64_t* key_len, uint64_t* value_off, uint64_t* checksum, uint64_t* result,
                             hipStream_t s);
@@ -145,6 +146,19 @@ constexpr size_t kStage = 32ull << 20;  // pinned staging piece
 
 }  // namespace
 
+namespace {
+// framing scratch + per-record decode descriptors of one file (a ctx has one set per file of a batch)
+struct FileArenas {
+    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, fail_lanes, chunks, block_runs, chunk_excl, place,
+        block_excl, state, info;
+    void release() {
+        for (DevBuf* b : {&scratch_off, &scratch_len, &scratch_pay, &rec_pay, &rec_desc, &fail_lanes, &chunks, &block_runs,
+                          &chunk_excl, &place, &block_excl, &state, &info})
+            b->release();
+    }
+};
+}  // namespace
+
 struct rio_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -152,6 +166,7 @@ struct rio_ctx {
     std::vector<std::array<hipEvent_t, 5>> ev;
     uint64_t ev_cursor = 0;
     uint64_t chunk_bytes = 32768;
+    uint64_t coop_min = ~0ull >> 8;
     hipEvent_t* next_events() {
         if (ev.empty()) return nullptr;
         return ev[ev_cursor++ % ev.size()].data();
@@ -169,8 +184,9 @@ struct rio_ctx {
         ev_cursor = 0;
     }
     // framing arenas
-    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, sink, fail_lanes, chunks, block_runs, chunk_excl, place,
-        block_excl, state, info;
+    FileArenas fa;                                   // the single-file calls
+    std::vector<std::unique_ptr<FileArenas>> batch;  // rio_device_decode_batch: one set per file
+    DevBuf sink;
     // host-API arenas
     DevBuf file, out, out_off, rec_off, flags, readat_out, readat_res, seek_off;
     // reader handles sharing this ctx take this around every device use (rio_reader_*)
@@ -192,39 +208,40 @@ struct rio_ctx {
     rio_file_info frame_info{};
 };
 
-static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P) {
+static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P, FileArenas& A) {
     memset(&P, 0, sizeof P);
     P.file = d_file;
     P.len = len;
     P.chunk_bytes = ctx->chunk_bytes;
+    P.coop_min = ctx->coop_min;
     P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + ctx->chunk_bytes - 1) / ctx->chunk_bytes : 0;
     P.slots = ctx->chunk_bytes / 6 + 1;
     P.n_blocks = (P.n_chunks + 255) / 256;
     const uint64_t nc = std::max<uint64_t>(P.n_chunks, 1), nb = std::max<uint64_t>(P.n_blocks, 1);
-    HIP_TRY(ctx->scratch_off.ensure(nc * P.slots * 8));
-    HIP_TRY(ctx->scratch_len.ensure(nc * P.slots * 8));
-    HIP_TRY(ctx->scratch_pay.ensure(nc * P.slots * 8));
-    HIP_TRY(ctx->chunks.ensure(nc * sizeof(ChunkSum)));
-    HIP_TRY(ctx->chunk_excl.ensure(nc * sizeof(RunSum)));
-    HIP_TRY(ctx->place.ensure(nc * sizeof(ChunkPlace)));
-    HIP_TRY(ctx->block_runs.ensure(nb * sizeof(RunSum)));
-    HIP_TRY(ctx->block_excl.ensure(nb * sizeof(RunSum)));
-    HIP_TRY(ctx->state.ensure(sizeof(ScanState)));
-    HIP_TRY(ctx->info.ensure(sizeof(rio_file_info)));
+    HIP_TRY(A.scratch_off.ensure(nc * P.slots * 8));
+    HIP_TRY(A.scratch_len.ensure(nc * P.slots * 8));
+    HIP_TRY(A.scratch_pay.ensure(nc * P.slots * 8));
+    HIP_TRY(A.chunks.ensure(nc * sizeof(ChunkSum)));
+    HIP_TRY(A.chunk_excl.ensure(nc * sizeof(RunSum)));
+    HIP_TRY(A.place.ensure(nc * sizeof(ChunkPlace)));
+    HIP_TRY(A.block_runs.ensure(nb * sizeof(RunSum)));
+    HIP_TRY(A.block_excl.ensure(nb * sizeof(RunSum)));
+    HIP_TRY(A.state.ensure(sizeof(ScanState)));
+    HIP_TRY(A.info.ensure(sizeof(rio_file_info)));
     HIP_TRY(ctx->sink.ensure(kSinkBytes));
-    HIP_TRY(ctx->fail_lanes.ensure(2 * kFailLanes * sizeof(uint64_t)));
+    HIP_TRY(A.fail_lanes.ensure(2 * kFailLanes * sizeof(uint64_t)));
     P.sink = ctx->sink.as<uint8_t>();
-    P.fail_lanes = ctx->fail_lanes.as<uint64_t>();
-    P.scratch_off = ctx->scratch_off.as<uint64_t>();
-    P.scratch_len = ctx->scratch_len.as<uint64_t>();
-    P.scratch_pay = ctx->scratch_pay.as<uint64_t>();
-    P.chunks = ctx->chunks.as<ChunkSum>();
-    P.chunk_excl = ctx->chunk_excl.as<RunSum>();
-    P.place = ctx->place.as<ChunkPlace>();
-    P.block_runs = ctx->block_runs.as<RunSum>();
-    P.block_excl = ctx->block_excl.as<RunSum>();
-    P.state = ctx->state.as<ScanState>();
-    P.info = ctx->info.as<rio_file_info>();
+    P.fail_lanes = A.fail_lanes.as<uint64_t>();
+    P.scratch_off = A.scratch_off.as<uint64_t>();
+    P.scratch_len = A.scratch_len.as<uint64_t>();
+    P.scratch_pay = A.scratch_pay.as<uint64_t>();
+    P.chunks = A.chunks.as<ChunkSum>();
+    P.chunk_excl = A.chunk_excl.as<RunSum>();
+    P.place = A.place.as<ChunkPlace>();
+    P.block_runs = A.block_runs.as<RunSum>();
+    P.block_excl = A.block_excl.as<RunSum>();
+    P.state = A.state.as<ScanState>();
+    P.info = A.info.as<rio_file_info>();
     return RIO_OK;
 }
 
@@ -246,6 +263,7 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     c->device = device;
     c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 32768);
     if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
+    c->coop_min = env_u64("RIO_COOP_MIN", ~0ull >> 8);  // k_snappy_coop: wide files only
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RIO_ERR_HIP;
@@ -259,8 +277,9 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->scratch_off, &c->scratch_len, &c->scratch_pay, &c->rec_pay, &c->rec_desc, &c->sink, &c->fail_lanes, &c->chunks, &c->block_runs, &c->chunk_excl, &c->place,
-                      &c->block_excl, &c->state, &c->info, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
+    c->fa.release();
+    for (auto& a : c->batch) a->release();
+    for (DevBuf* b : {&c->sink, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
                       &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res, &c->enc_scr, &c->enc_scr_off, &c->enc_clen, &c->enc_tab,
                       &c->enc_hdr, &c->enc_size, &c->enc_tmp, &c->enc_cub, &c->enc_rec, &c->enc_rec_off, &c->enc_flags, &c->enc_out,
                       &c->enc_out_off, &c->enc_len, &c->q_pfx, &c->q_pfx_out, &c->q_idx, &c->q_perm, &c->q_tmp})
@@ -313,7 +332,7 @@ extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t l
     if ((reinterpret_cast<uintptr_t>(d_file) & 15) != 0) return RIO_ERR_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     FrameParams P;
-    int rc = ctx_frame_params(ctx, d_file, len, P);
+    int rc = ctx_frame_params(ctx, d_file, len, P, ctx->fa);
     if (rc) return rc;
     P.out = d_out;
     P.out_cap = out_cap;
@@ -322,14 +341,69 @@ extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t l
     P.flags = d_flags;
     P.rec_cap = rec_cap;
     P.info = d_info;
-    HIP_TRY(ctx->rec_pay.ensure((rec_cap + 1) * 8));
-    P.rec_pay = ctx->rec_pay.as<uint64_t>();
-    HIP_TRY(ctx->rec_desc.ensure((rec_cap + 1) * 16));
-    P.rec_desc = ctx->rec_desc.as<uint4>();
+    HIP_TRY(ctx->fa.rec_pay.ensure((rec_cap + 1) * 8));
+    P.rec_pay = ctx->fa.rec_pay.as<uint64_t>();
+    HIP_TRY(ctx->fa.rec_desc.ensure((rec_cap + 1) * 16));
+    P.rec_desc = ctx->fa.rec_desc.as<uint4>();
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     hipEvent_t* ev = ctx->next_events();
     HIP_TRY(launch_phase_a(P, s, ev));
     HIP_TRY(launch_phase_b(P, s, ev));
+    return RIO_OK;
+}
+
+// Batch of device-resident files (BASELINE configs[3]: the 8 files of a GPU's shard in one step):
+// framing per file, then the large-record Snappy decoder once over all of them, so that files of few
+// large records still fill the chip. Up to kMaxBatch files per launch group; larger batches run as
+// consecutive groups on the same stream.
+extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uint8_t* const* d_files,
+                                       const uint64_t* lens, uint8_t* const* d_out, const uint64_t* out_cap,
+                                       uint64_t* const* d_out_off, uint64_t* const* d_rec_off, uint8_t* const* d_flags,
+                                       const uint64_t* rec_cap, rio_file_info* const* d_info, void* stream) {
+    if (!ctx || (n_files && (!d_files || !lens || !d_out || !out_cap || !d_out_off || !d_rec_off || !d_flags ||
+                             !rec_cap || !d_info)))
+        return RIO_ERR_ARG;
+    for (uint32_t k = 0; k < n_files; k++)
+        if (!d_files[k] || (reinterpret_cast<uintptr_t>(d_files[k]) & 15) || !d_out_off[k] || !d_rec_off[k] ||
+            !d_flags[k] || !d_info[k])
+            return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    while (ctx->batch.size() < std::min<uint32_t>(n_files, kMaxBatch)) ctx->batch.emplace_back(new FileArenas());
+    hipEvent_t* ev = ctx->next_events();
+    for (uint32_t g = 0; g < n_files; g += kMaxBatch) {
+        FrameBatch B{};
+        B.n = std::min<uint32_t>(kMaxBatch, n_files - g);
+        for (uint32_t j = 0; j < B.n; j++) {
+            const uint32_t k = g + j;
+            FileArenas& A = *ctx->batch[j];
+            FrameParams& P = B.f[j];
+            int rc = ctx_frame_params(ctx, d_files[k], lens[k], P, A);
+            if (rc) return rc;
+            P.out = d_out[k];
+            P.out_cap = out_cap[k];
+            P.out_off = d_out_off[k];
+            P.rec_off = d_rec_off[k];
+            P.flags = d_flags[k];
+            P.rec_cap = rec_cap[k];
+            P.info = d_info[k];
+            HIP_TRY(A.rec_pay.ensure((rec_cap[k] + 1) * 8));
+            P.rec_pay = A.rec_pay.as<uint64_t>();
+            HIP_TRY(A.rec_desc.ensure((rec_cap[k] + 1) * 16));
+            P.rec_desc = A.rec_desc.as<uint4>();
+        }
+        // stage events bracket the whole batch: [0] before the first file's framing, [1..2] after
+        // the last file's walk / scan, [3] after placement, [4] after the decode kernels
+        hipEvent_t* e = (ev && g == 0) ? ev : nullptr;
+        hipEvent_t* last = (ev && g + kMaxBatch >= n_files) ? ev : nullptr;
+        if (e) HIP_TRY(hipEventRecord(e[0], s));
+        for (uint32_t j = 0; j < B.n; j++) HIP_TRY(launch_phase_a(B.f[j], s, nullptr));
+        if (last) {
+            HIP_TRY(hipEventRecord(last[1], s));
+            HIP_TRY(hipEventRecord(last[2], s));
+        }
+        HIP_TRY(launch_phase_b_batch(B, s, last));
+    }
     return RIO_OK;
 }
 
@@ -445,7 +519,7 @@ static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const u
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(ctx->file.as<uint8_t>() + len, 0, RIO_DEVICE_PAD, ctx->stream));
     FrameParams P;
-    rc = ctx_frame_params(ctx, ctx->file.as<uint8_t>(), len, P);
+    rc = ctx_frame_params(ctx, ctx->file.as<uint8_t>(), len, P, ctx->fa);
     if (rc) return rc;
     HIP_TRY(launch_phase_a(P, ctx->stream, ctx->next_events()));
     HIP_TRY(hipMemcpyAsync(&ctx->frame_info, P.info, sizeof(rio_file_info), hipMemcpyDeviceToHost, ctx->stream));
@@ -493,10 +567,10 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
     P.rec_off = ctx->rec_off.as<uint64_t>();
     P.flags = ctx->flags.as<uint8_t>();
     P.rec_cap = n;
-    HIP_TRY(ctx->rec_pay.ensure((n + 1) * 8));
-    P.rec_pay = ctx->rec_pay.as<uint64_t>();
-    HIP_TRY(ctx->rec_desc.ensure((n + 1) * 16));
-    P.rec_desc = ctx->rec_desc.as<uint4>();
+    HIP_TRY(ctx->fa.rec_pay.ensure((n + 1) * 8));
+    P.rec_pay = ctx->fa.rec_pay.as<uint64_t>();
+    HIP_TRY(ctx->fa.rec_desc.ensure((n + 1) * 16));
+    P.rec_desc = ctx->fa.rec_desc.as<uint4>();
     HIP_TRY(launch_phase_b(P, ctx->stream, ctx->same_events()));
     rio_file_info fin{};
     HIP_TRY(hipMemcpyAsync(&fin, P.info, sizeof fin, hipMemcpyDeviceToHost, ctx->stream));

@@ -107,6 +107,9 @@ struct FrameParams {
     uint4* rec_desc;
     uint8_t* sink;           // [kSinkBytes] placeholder-store target of the Snappy decode pipeline
     uint64_t* fail_lanes;    // [2 * kFailLanes] record ranges [r0, r1) of lanes that met a corrupt record
+    // Snappy: files whose mean decoded record is at least this many bytes (and files past 32-bit
+    // lane positions) take the wave-per-record decoder k_snappy_coop instead of k_snappy_pipe
+    uint64_t coop_min;
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)
     RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix
@@ -123,6 +126,14 @@ struct FrameParams {
     uint8_t* flags;
     uint64_t rec_cap;
     rio_file_info* info;  // device copy of the public result
+};
+
+// Files of one rio_device_decode_batch call, passed by value to the batched decode kernel (the
+// kernel argument holds them all: no H2D copy, no host sync, graph-capturable).
+constexpr uint32_t kMaxBatch = 16;
+struct FrameBatch {
+    FrameParams f[kMaxBatch];
+    uint32_t n;
 };
 
 // rio_encode.hip: recordio v4 encoding of a batch of records (rio_device_encode)

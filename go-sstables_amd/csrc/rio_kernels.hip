@@ -1589,7 +1589,8 @@ hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 }
 
 // Phase B: placement into the caller's arrays, decode, final result.
-hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s);  // rio_snappy.hip
+hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool coop);  // rio_snappy.hip
+hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s);             // rio_snappy.hip
 hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s);    // rio_gzip.hip
 
 // Phase B: placement into the caller's arrays, decode, final result. Both decoders check the
@@ -1600,10 +1601,31 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[3], s);
     hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);
     hipLaunchKernelGGL(k_snappy_literal, dim3(2048), dim3(256), 0, s, P);
-    launch_snappy_decode(P, s);
+    launch_snappy_decode(P, s, true);
     launch_gzip_decode(P, s);
     if (ev) (void)hipEventRecord(ev[4], s);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, P);
+    return hipGetLastError();
+}
+
+// rio_device_decode_batch: phase B of every file of the batch; the large-record Snappy decoder runs
+// once over all of them (k_snappy_coop_batch), the other decode kernels per file
+hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev) {
+    for (uint32_t f = 0; f < B.n; f++) {
+        hipLaunchKernelGGL(k_place, dim3(blocks_for(B.f[f].n_chunks, 4)), dim3(256), 0, s, B.f[f]);
+        hipLaunchKernelGGL(k_post_scan, dim3(1), dim3(64), 0, s, B.f[f]);
+    }
+    if (ev) (void)hipEventRecord(ev[3], s);
+    launch_snappy_batch(B, s);
+    for (uint32_t f = 0; f < B.n; f++) {
+        const FrameParams& P = B.f[f];
+        hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);
+        hipLaunchKernelGGL(k_snappy_literal, dim3(2048), dim3(256), 0, s, P);
+        launch_snappy_decode(P, s, false);
+        launch_gzip_decode(P, s);
+    }
+    if (ev) (void)hipEventRecord(ev[4], s);
+    for (uint32_t f = 0; f < B.n; f++) hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, B.f[f]);
     return hipGetLastError();
 }
 

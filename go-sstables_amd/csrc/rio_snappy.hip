@@ -358,6 +358,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || snappy_wide(P, st))
         return;
     if (!st->any_mixed) return;  // every record is one literal: k_snappy_literal copies them
+    if (st->n_records && st->total_bytes / st->n_records >= P.coop_min) return;  // large records: k_snappy_coop
     const uint64_t n = st->n_records;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     // lane number: waves are numbered across workgroups first, so that a file with few records
@@ -382,11 +383,64 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     }
 }
 
-// Files beyond the lane-stream kernel's 32-bit positions (>= 4 GiB of input or output, or a
-// stream over 4 GiB): every record decoded by one thread with byte loops straight to HBM.
+// rio_device_decode_batch: one launch for every lane-decoder file of the batch. The lanes of the grid
+// are split over the files by record count (whole waves per file, so the file's parameters stay
+// wave-uniform scalars), which is what fills the chip when each file alone has fewer records than
+// lanes (BASELINE configs[3]: 8 files of 16384 x 64 KiB records).
+__device__ __forceinline__ bool pipe_active(const FrameParams& P) {
+    const ScanState* st = P.state;
+    return st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_SNAPPY && st->any_mixed &&
+           !snappy_wide(P, st) && !(st->n_records && st->total_bytes / st->n_records >= P.coop_min);
+}
+
+__global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
+    uint64_t N = 0;
+    for (uint32_t f = 0; f < B.n; f++)
+        if (pipe_active(B.f[f])) N += B.f[f].state->n_records;
+    if (N == 0) return;
+    // the fewest records per lane whose whole-wave shares (ceil per file) fit the grid: every wave
+    // of the grid is resident at once (2 per SIMD), so a share past it would run as a second round
+    uint64_t rpl = (N + 64 * waves - 1) / (64 * waves);
+    for (;;) {
+        uint64_t need = 0;
+        for (uint32_t f = 0; f < B.n; f++)
+            if (pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
+        if (need <= waves) break;
+        rpl++;
+    }
+    const uint64_t per_wave = 64 * rpl;
+    uint64_t w0 = 0;
+    for (uint32_t f = 0; f < B.n; f++) {
+        const FrameParams& P = B.f[f];
+        if (!pipe_active(P)) continue;
+        const uint64_t n = P.state->n_records, wf = (n + per_wave - 1) / per_wave;
+        if (wg < w0 + wf) {
+            const uint64_t t = ((wg - w0) << 6) | lane;
+            const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
+            uint8_t* sink = P.sink + wg * 64;
+            uint64_t bad_rec = 0;
+            if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
+                const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
+                if (at < kFailLanes) {
+                    P.fail_lanes[2 * at] = r0;
+                    P.fail_lanes[2 * at + 1] = r1;
+                }
+            }
+            return;
+        }
+        w0 += wf;
+    }
+}
+
+// Files with a record stream past 32-bit positions (never produced by an encoder: a record over
+// 4 GiB): every record decoded by one thread with byte loops straight to HBM.
 __global__ void __launch_bounds__(256) k_snappy_global(FrameParams P) {
     ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !snappy_wide(P, st) ||
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->huge_streams ||
         !st->any_mixed)
         return;
     const uint64_t n = st->n_records;
@@ -422,9 +476,372 @@ __global__ void __launch_bounds__(256) k_snappy_verify(FrameParams P) {
         for (uint64_t i = P.fail_lanes[2 * l] + threadIdx.x; i < P.fail_lanes[2 * l + 1]; i += blockDim.x) verify(i);
 }
 
-hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s) {
+// ------------------------------------------------------------------------------------------
+// k_snappy_coop: one wave per record, all 64 lanes on that record (files of large records: C4's
+// 64 KiB values; and files past the lane decoder's 32-bit positions). A record is decoded in
+// rounds of up to 64 elements:
+//   1. parse: the next 256 stream bytes go to LDS; every lane computes, for 4 positions q, where an
+//      element starting at q would end (J0[q] = next element start, >= 256: outside the window);
+//      five pointer-doubling levels J_k = J_{k-1} o J_{k-1} follow, and lane e finds element e of
+//      the chain as J composed along the bits of e. Lane e then decodes its element's header and
+//      applies golang/snappy's checks (decode_other.go: header and literal inside the stream, copy
+//      offset in [1, produced], output room) — produced = an exclusive scan of element lengths.
+//   2. materialise the round's output in 64-byte windows, lane = output byte: the element covering
+//      each byte comes from a prefix-max over "element starts here" marks; a literal byte is read
+//      from the file, a copy byte from position s = dst - off + (x mod off) < dst (the periodic
+//      extension of an overlapping copy): the current window (resolved through the lanes, always
+//      an earlier element: a short dependency chain), a 1 KiB LDS history ring, or the output arena
+//      (older bytes; their stores are drained by the vmcnt bound before every store, and the loads
+//      bypass L1).
+// A record that fails a check is flagged (mark_bad) where the check fails; its bytes are unspecified.
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr uint32_t kCoopWaves = 4;
+constexpr uint32_t kCoopGrid = 2048;  // x 4 waves: 32 waves per CU (latency-bound: LDS + shuffle chains)
+constexpr uint32_t kCoopWin = 256;    // parse window (stream bytes)
+constexpr uint32_t kCoopLevels = 6;   // 2^6 = 64 elements per round
+constexpr uint32_t kCoopRing = 1024;  // history ring per wave
+constexpr uint32_t kInDw = 72;        // window image: 288 bytes from (base & ~3)
+constexpr uint32_t kOut = 0xFFFFu;    // "no next element inside the window"
+// a mapped output window of the pipeline: the byte's source kind and what it needs
+constexpr uint32_t kSlotLds = 0, kSlotGlobal = 1, kSlotRing = 2, kSlotLane = 3, kSlotIdle = 4;
+struct CoopSlot {
+    uint8_t g;      // global load in flight (far history or a literal byte past the LDS window)
+    uint32_t v;     // literal byte from the LDS window
+    uint32_t code;  // kind << 24 | ring position or source lane
+};
+struct CoopLds {
+    uint32_t in[2][kInDw];                // parse window images (double-buffered: the next one lands
+                                          // while the current round's literals are read)
+    uint16_t J[kCoopLevels][kCoopWin];    // next-element tables
+    uint8_t slot[64];                     // element starts in the current output window
+    uint8_t ring[kCoopRing];              // decoded history of the current record
+};
+
+__device__ __forceinline__ bool coop_active(const FrameParams& P, const ScanState* st) {
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->any_mixed ||
+        st->huge_streams)
+        return false;
+    return snappy_wide(P, st) || (st->n_records && st->total_bytes / st->n_records >= P.coop_min);
+}
+
+// element header from its first 8 bytes (lo = bytes 0..3, hi = 4..7): header length, output length
+// (64-bit: a 4-byte literal length may be 2^32), copy offset
+__device__ __forceinline__ void coop_elem(uint32_t lo, uint32_t hi, uint32_t& hl, uint64_t& len, uint32_t& off,
+                                          bool& lit) {
+    const uint32_t tag = lo & 0xFFu, t = tag & 3u, x = tag >> 2;
+    const uint32_t b1 = (lo >> 8) & 0xFFu, b12 = (lo >> 8) & 0xFFFFu;
+    const uint32_t b1234 = (lo >> 8) | (hi << 24);
+    lit = t == 0;
+    if (t == 0) {
+        if (x < 60) {
+            hl = 1;
+            len = x + 1;
+        } else {
+            const uint32_t nb = x - 59;  // 1..4 length bytes
+            hl = 1 + nb;
+            const uint32_t v = nb == 4 ? b1234 : (b1234 & ((1u << (8 * nb)) - 1u));
+            len = (uint64_t)v + 1;
+        }
+        off = 0;
+    } else if (t == 1) {
+        hl = 2;
+        len = 4 + (x & 7u);
+        off = ((tag & 0xE0u) << 3) | b1;
+    } else if (t == 2) {
+        hl = 3;
+        len = 1 + x;
+        off = b12;
+    } else {
+        hl = 5;
+        len = 1 + x;
+        off = b1234;
+    }
+}
+
+// bytes [u, u + 8) of a window image (u relative to its aligned base)
+__device__ __forceinline__ void coop_bytes8(const uint32_t* in, uint32_t u, uint32_t& lo, uint32_t& hi) {
+    const uint32_t k = u >> 2, r = u & 3u;
+    const uint32_t d0 = in[k], d1 = in[k + 1], d2 = in[k + 2];
+    lo = __builtin_amdgcn_alignbyte(d1, d0, r);
+    hi = __builtin_amdgcn_alignbyte(d2, d1, r);
+}
+
+// wave-wide inclusive scans on DPP (row shifts within 16-lane rows, then row broadcasts 15 / 31):
+// VALU latency instead of the LDS round trips of __shfl_up
+template <bool kMax>
+__device__ __forceinline__ uint32_t wave_incl(uint32_t v) {
+    auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : a + b; };
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_excl_u64(uint64_t v, uint32_t lane, uint64_t& total) {
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        x += lane >= (uint32_t)d ? y : 0ull;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+// the 288 window bytes from aligned address a: one dword per lane + 8 (clamped inside the padded file)
+struct WinRegs {
+    uint32_t w0, w1;
+};
+__device__ __forceinline__ WinRegs coop_fetch(const FrameParams& P, uint64_t a, uint32_t lane, uint64_t dw_end) {
+    const uint64_t g0 = a + 4ull * lane, g1 = g0 + 256;
+    WinRegs r;
+    r.w0 = *reinterpret_cast<const uint32_t*>(P.file + (g0 < dw_end ? g0 : dw_end));
+    r.w1 = lane < kInDw - 64 ? *reinterpret_cast<const uint32_t*>(P.file + (g1 < dw_end ? g1 : dw_end)) : 0u;
+    return r;
+}
+__device__ __forceinline__ void coop_land(uint32_t* in, const WinRegs& r, uint32_t lane) {
+    in[lane] = r.w0;
+    if (lane < kInDw - 64) in[64 + lane] = r.w1;
+}
+
+// decode one record: stream [start, start + slen) of the file, dlen bytes to out
+__device__ bool coop_record(const FrameParams& P, CoopLds& S, uint32_t lane, uint64_t start, uint32_t slen,
+                            uint32_t dlen, uint8_t* out, uint8_t* sink) {
+    const uint64_t dw_end = ((P.len + RIO_DEVICE_PAD) & ~3ull) - 4;  // last readable dword
+    const bool small_out = dlen < (1u << 25);  // element lengths of a round fit 32-bit scans
+    uint32_t pos = 0;  // stream position of the next element
+    uint32_t d = 0;    // bytes produced
+    uint32_t buf = 0;
+    coop_land(S.in[0], coop_fetch(P, (start + pos) & ~3ull, lane, dw_end), lane);
+    while (pos < slen) {
+        const uint32_t* in = S.in[buf];
+        const uint64_t base = start + pos;
+        const uint32_t sh = (uint32_t)(base & 3u);
+        const uint32_t lim = slen - pos < 0xFFF0u ? slen - pos : 0xFFF0u;  // stream bytes from the window start
+        __builtin_amdgcn_wave_barrier();
+        // ---- 1. parse: J0 for q = 4 lane + j, then pointer doubling ----
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t q = 4 * lane + j;
+            uint32_t lo, hi, hl, off;
+            uint64_t len;
+            bool lit;
+            coop_bytes8(in, q + sh, lo, hi);
+            coop_elem(lo, hi, hl, len, off, lit);
+            uint32_t nx = kOut;
+            if (q < lim && hl <= lim - q) {
+                const uint64_t e = (uint64_t)q + hl + (lit ? len : 0);
+                if (e <= lim) nx = (uint32_t)(e < kOut - 1 ? e : kOut - 1);
+            }
+            S.J[0][q] = (uint16_t)nx;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t k = 1; k < kCoopLevels; k++) {
+            uint16_t v[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint32_t t = S.J[k - 1][4 * lane + j];
+                v[j] = t < kCoopWin ? S.J[k - 1][t] : (uint16_t)t;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) S.J[k][4 * lane + j] = v[j];
+            __builtin_amdgcn_wave_barrier();
+        }
+        // element e = lane of this round: the chain position next^e(0)
+        uint32_t p = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kCoopLevels; k++)
+            if (((lane >> k) & 1u) && p < kCoopWin) p = S.J[k][p];
+        const bool valid = p < (lim < kCoopWin ? lim : kCoopWin);
+        uint32_t lo = 0, hi = 0, hl = 0, off = 0;
+        uint64_t len = 0;
+        bool lit = false;
+        if (valid) {
+            coop_bytes8(in, p + sh, lo, hi);
+            coop_elem(lo, hi, hl, len, off, lit);
+        }
+        bool bad = valid && (hl > lim - p || (lit && len > lim - p - hl));
+        const uint64_t olen = valid ? (len < (uint64_t)dlen + 1 ? len : (uint64_t)dlen + 1) : 0;
+        uint64_t total, excl;
+        if (small_out) {  // olen <= 2^25: the round's sum fits 32 bits
+            const uint32_t inc = wave_incl<false>((uint32_t)olen);
+            excl = inc - (uint32_t)olen;
+            total = (uint32_t)__shfl(inc, 63, 64);
+        } else {
+            excl = wave_excl_u64(olen, lane, total);
+        }
+        const uint64_t de = d + excl;
+        bad = bad || (valid && (de + olen > dlen || (!lit && (off == 0 || off > de))));
+        if (__any(bad)) return false;
+        const uint32_t m = __builtin_popcountll(__ballot(valid));
+        const uint32_t ext = p + hl + (lit ? (uint32_t)len : 0u);  // stream end of element e (window-relative)
+        const uint32_t next_pos = pos + (uint32_t)__shfl(ext, m - 1, 64);
+        // prefetch the next round's window while this one materialises
+        WinRegs nxt{0, 0};
+        const bool more = next_pos < slen;
+        if (more) nxt = coop_fetch(P, (start + next_pos) & ~3ull, lane, dw_end);
+        const uint32_t e_dst = (uint32_t)de, e_len = (uint32_t)olen;
+        // literal: window position of its bytes; copy: offset
+        const uint32_t e_a = lit ? p + hl : off;
+        // ---- 2. materialise [d, d + total) in 64-byte windows, lane = byte ----
+        // Software-pipelined by kCoopD windows: window j + kCoopD is mapped (covering element, byte
+        // source, its global load issued) while window j is finished (ring / in-window sources
+        // resolved, stored). Every map issues exactly one vector load and every finish one store
+        // (placeholders go to the wave's sink line), so the compiler waits for exactly the load
+        // issued kCoopD windows earlier; that wait also retires every store older than it, which is
+        // what makes far history (> kCoopRing bytes back, at least 12 windows old) safe to load.
+        const uint32_t Wend = d + (uint32_t)total;
+        const uint32_t nwin = ((uint32_t)total + 63) >> 6;
+        const uint32_t in_avail = kInDw * 4 - 8 - sh;  // window bytes a literal may take from LDS
+        uint32_t ei = 0;  // element covering the next window to map
+        auto map = [&](CoopSlot& T, uint32_t j) __attribute__((always_inline)) {
+            const uint32_t W = d + 64 * j;
+            uint32_t type = kSlotIdle, v = 0, sp = 0;
+            const uint8_t* ap = sink + lane;
+            if (W < Wend) {  // wave-uniform
+                S.slot[lane] = 0;
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) S.slot[0] = (uint8_t)(ei + 1);
+                if (valid && e_dst > W && e_dst < W + 64) S.slot[e_dst - W] = (uint8_t)(lane + 1);
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t k = wave_incl<true>(S.slot[lane]) - 1;
+                const uint32_t dk = __shfl(e_dst, k, 64), lk = __shfl(e_len, k, 64), ak = __shfl(e_a, k, 64);
+                const bool litk = __shfl(lit ? 1 : 0, k, 64) != 0;
+                const uint32_t b = W + lane;
+                const uint32_t x = b - dk;
+                if (b >= Wend) {
+                    type = kSlotIdle;
+                } else if (litk) {
+                    const uint32_t u = ak + x;  // window-relative stream position
+                    if (u < in_avail) {
+                        type = kSlotLds;
+                        v = (in[(u + sh) >> 2] >> (8 * ((u + sh) & 3u))) & 0xFFu;
+                    } else {
+                        type = kSlotGlobal;
+                        ap = P.file + base + u;
+                    }
+                } else {
+                    uint32_t q = x;
+                    if (x >= ak) {  // inside the copy's own period: x mod off (x < 64, off < 64 here)
+                        const uint32_t qq = (uint32_t)((float)x * __frcp_rn((float)ak));
+                        int r = (int)x - (int)(qq * ak);
+                        r += r < 0 ? (int)ak : 0;
+                        r -= r >= (int)ak ? (int)ak : 0;
+                        q = (uint32_t)r;
+                    }
+                    sp = dk - ak + q;  // < dk: an earlier element's byte
+                    if (sp >= W) {
+                        type = kSlotLane;
+                        sp -= W;  // the source lane
+                    } else if (W - sp <= kCoopRing) {
+                        type = kSlotRing;
+                    } else {
+                        type = kSlotGlobal;
+                        ap = out + sp;
+                    }
+                }
+                const uint32_t Wn = W + 64;
+                if (Wn < Wend) {
+                    const uint32_t k63 = __shfl(k, 63, 64), end63 = __shfl(dk + lk, 63, 64);
+                    ei = end63 > Wn ? k63 : k63 + 1;
+                }
+            }
+            T.g = __builtin_nontemporal_load(ap);  // L2: bypasses this CU's L1 (far history was written here)
+            T.v = v;
+            T.code = (type << 24) | sp;
+        };
+        auto finish = [&](CoopSlot& T, uint32_t j) __attribute__((always_inline)) {
+            const uint32_t type = T.code >> 24, sp = T.code & 0xFFFFFFu;
+            const uint32_t b = d + 64 * j + lane;
+            uint32_t val = type == kSlotGlobal ? (uint32_t)T.g : T.v;
+            if (type == kSlotRing) val = S.ring[sp & (kCoopRing - 1)];
+            bool pend = type == kSlotLane;
+            const uint32_t srcl = pend ? sp : lane;
+            while (__any(pend)) {
+                const uint32_t sv = __shfl(val, srcl, 64);
+                const bool sp2 = __shfl(pend ? 1 : 0, srcl, 64) != 0;
+                if (pend && !sp2) {
+                    val = sv;
+                    pend = false;
+                }
+            }
+            const bool active = type != kSlotIdle;
+            *(active ? out + b : sink + lane) = (uint8_t)val;
+            if (active) S.ring[b & (kCoopRing - 1)] = (uint8_t)val;
+        };
+        CoopSlot T0, T1, T2, T3;
+        map(T0, 0);
+        map(T1, 1);
+        map(T2, 2);
+        map(T3, 3);
+        for (uint32_t j = 0; j < nwin; j += 4) {
+            finish(T0, j);
+            map(T0, j + 4);
+            finish(T1, j + 1);
+            map(T1, j + 5);
+            finish(T2, j + 2);
+            map(T2, j + 6);
+            finish(T3, j + 3);
+            map(T3, j + 7);
+        }
+        d = Wend;
+        pos = next_pos;
+        buf ^= 1u;
+        if (more) coop_land(S.in[buf], nxt, lane);
+    }
+    return d == dlen;
+}
+
+// every record of one file, records strided over all waves of the grid
+__device__ __forceinline__ void coop_file(const FrameParams& P, CoopLds& S, uint32_t lane, uint64_t wave,
+                                          uint64_t nw) {
+    const ScanState* st = P.state;
+    if (!coop_active(P, st)) return;
+    const uint64_t n = st->n_records;
+    uint8_t* sink = P.sink + (wave % ((uint64_t)kSnappyGrid * (kSnappyBlock / 64))) * 64;  // placeholder line
+    for (uint64_t i = wave; i < n; i += nw) {
+        if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
+        const uint4 dsc = P.rec_desc[i];
+        const uint64_t start = ((uint64_t)dsc.y << 32) | dsc.x;
+        if (!coop_record(P, S, lane, start, dsc.z, dsc.w, P.out + P.out_off[i], sink) && lane == 0) mark_bad(P, i);
+    }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64 * kCoopWaves) k_snappy_coop(FrameParams P) {
+    __shared__ CoopLds lds[kCoopWaves];
+    const uint32_t wv = threadIdx.x >> 6;
+    coop_file(P, lds[wv], threadIdx.x & 63u, (uint64_t)blockIdx.x * kCoopWaves + wv, (uint64_t)gridDim.x * kCoopWaves);
+}
+
+// rio_device_decode_batch: the files one after the other, every wave of the grid on each (a wave
+// that finishes its share of file f goes on to file f + 1 at once: no grid-wide step)
+__global__ void __launch_bounds__(64 * kCoopWaves) k_snappy_coop_batch(FrameBatch B) {
+    __shared__ CoopLds lds[kCoopWaves];
+    const uint32_t wv = threadIdx.x >> 6;
+    for (uint32_t f = 0; f < B.n; f++)
+        coop_file(B.f[f], lds[wv], threadIdx.x & 63u, (uint64_t)blockIdx.x * kCoopWaves + wv,
+                  (uint64_t)gridDim.x * kCoopWaves);
+}
+
+hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
+    hipLaunchKernelGGL(k_snappy_pipe_batch, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, B);
+    hipLaunchKernelGGL(k_snappy_coop_batch, dim3(kCoopGrid), dim3(64 * kCoopWaves), 0, s, B);
+    return hipGetLastError();
+}
+
+// main = false: the caller runs the lane and wave decoders for this file itself (a batch)
+hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main) {
     // 4 waves x 20 KiB = 80 KiB per workgroup: 2 workgroups (8 waves) per CU
-    hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, P);
+    if (main) {
+        hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, P);
+        hipLaunchKernelGGL(k_snappy_coop, dim3(kCoopGrid), dim3(64 * kCoopWaves), 0, s, P);
+    }
     hipLaunchKernelGGL(k_snappy_global, dim3(64), dim3(256), 0, s, P);
     hipLaunchKernelGGL(k_snappy_verify, dim3(256), dim3(256), 0, s, P);
     return hipGetLastError();

@@ -108,6 +108,11 @@ _SIGS = {
         c_int,
         [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p],
     ),
+    "rio_device_decode_batch": (
+        c_int,
+        [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p],
+    ),
     "rio_max_records": (c_uint64, [c_uint64]),
     "rio_ctx_last_stage_ms": (c_int, [c_void_p, POINTER(c_float), c_int]),
     "rio_ctx_set_timing": (c_int, [c_void_p, c_int]),

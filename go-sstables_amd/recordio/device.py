@@ -72,6 +72,34 @@ class DeviceDecoder:
         raw = bytes(b.info.cpu().numpy().tobytes())
         return L.FileInfo.from_buffer_copy(raw).as_dict()
 
+    def launch_batch(self, files: list, bufs: list, stream=None) -> None:
+        """Enqueue rio_device_decode_batch for [(d_file, length)] into the matching DecodeBuffers."""
+        import numpy as np
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        n = len(files)
+        p = lambda xs: np.array(xs, dtype=np.uint64)  # noqa: E731
+        arrs = [p([f.data_ptr() for f, _ in files]), p([ln for _, ln in files]), p([b.out.data_ptr() for b in bufs]),
+                p([b.out.numel() for b in bufs]), p([b.out_off.data_ptr() for b in bufs]),
+                p([b.rec_off.data_ptr() for b in bufs]), p([b.flags.data_ptr() for b in bufs]),
+                p([b.out_off.numel() - 1 for b in bufs]), p([b.info.data_ptr() for b in bufs])]
+        rc = L.lib().rio_device_decode_batch(self.ctx, n, *[a.ctypes.data for a in arrs], ctypes.c_void_p(s.cuda_stream))
+        if rc != L.RIO_OK:
+            raise RuntimeError(f"rio_device_decode_batch: {L.strerror(rc)}")
+
+    def decode_batch(self, files: list, stream=None):
+        """Size every file's outputs with capacity-0 probes (one batch call), then decode the batch.
+        Returns [(buffers, info)] in file order."""
+        probes = [self.alloc(0, 0) for _ in files]
+        self.launch_batch(files, probes, stream)
+        torch.cuda.synchronize(self.device)
+        infos = [self.info(b) for b in probes]
+        bufs = [self.alloc(i["n_records"], i["total_out_bytes"]) if i["status"] == L.RIO_ERR_CAPACITY else b
+                for b, i in zip(probes, infos)]
+        self.launch_batch(files, bufs, stream)
+        torch.cuda.synchronize(self.device)
+        return [(b, self.info(b)) for b in bufs]
+
     def decode(self, d_file: torch.Tensor, length: int, stream=None):
         """Size the outputs with a capacity-0 probe, then decode. Returns (buffers, info)."""
         probe = self.alloc(0, 0)

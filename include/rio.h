@@ -162,6 +162,15 @@ int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, 
 int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                       uint64_t rec_cap, rio_file_info* d_info, void* stream);
+/* Batch form: n_files device-resident files, file k = d_files[k] (lens[k] bytes, 16-byte aligned,
+ * RIO_DEVICE_PAD readable bytes past it) decoded into its own outputs (d_out[k] ... d_info[k], as for
+ * rio_device_decode). The arrays of pointers are host arrays; everything runs on `stream` without
+ * host synchronisation. Replaces a loop of FileReader / MMapReader opens over a directory or shard
+ * (wal/replayer.go:18-77, BASELINE configs[3]): the large-record decoder runs once across the files. */
+int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uint8_t* const* d_files, const uint64_t* lens,
+                            uint8_t* const* d_out, const uint64_t* out_cap, uint64_t* const* d_out_off,
+                            uint64_t* const* d_rec_off, uint8_t* const* d_flags, const uint64_t* rec_cap,
+                            rio_file_info* const* d_info, void* stream);
 /* Upper bound on records in a file of `len` bytes (smallest v3/v4 record is 6/7 bytes). */
 uint64_t rio_max_records(uint64_t len);
 /* Kernel-timing probe for benchmarks: per-stage device milliseconds of the last
