@@ -101,7 +101,7 @@ def reduce_sum(value: float, world: int, device=None) -> float:
     return float(t.item())
 
 
-def job_throughput(dt: float, bytes_in: float, steps: int, world: int, device) -> tuple[float, float, float]:
+def job_throughput(dt: float, bytes_in: float, steps: int, world: int, device=None) -> tuple[float, float, float]:
     """Whole-job rate of a file-sharded run: every rank timed its own `steps` decodes of its own
     file (`bytes_in` per step); the job took the slowest rank's time. Returns (GiB/s, ms per step,
     max time). The two all-reduces are the job's only collectives and sit outside the timed region."""
@@ -809,111 +809,131 @@ def run_readat(args, world, rank, local, device):
         print(json.dumps(line), flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_latest.json"))
-    args = ap.parse_args()
+class DeviceBackend:
+    """The device call of a decode step: rio_device_decode (one file) or rio_device_decode_batch
+    (a file set) on this rank's GPU, files resident in HBM, outputs preallocated."""
 
-    world, rank, local = dist_env()
-    import numpy as np
-    import torch
+    def __init__(self, local: int, device):
+        from recordio.device import DeviceDecoder
 
-    torch.cuda.set_device(local)
-    device = torch.device(f"cuda:{local}")
-    if world > 1:
-        import torch.distributed as dist
+        self.local, self.device = local, device
+        self.dec = DeviceDecoder(local)
 
-        # gloo on the host: the barrier and the max/sum over ranks are the job's only collectives
-        # (the decode path has none: files are sharded, north_star "no RCCL")
-        dist.init_process_group(backend="gloo")
+    def load(self, images, batch: bool):
+        import torch
 
-    if args.config in ("c5", "wal", "idx", "enc", "readat"):
-        {"c5": run_sstable, "wal": run_wal, "idx": run_index, "enc": run_encode, "readat": run_readat}[args.config](
-            args, world, rank, local, device)
-        if world > 1:
-            torch.distributed.destroy_process_group()
-        return
+        from recordio.device import to_device_file
 
+        self.files = [to_device_file(img, self.local) for img in images]
+        self.batch = batch
+        self.stream = torch.cuda.current_stream(self.device)
+        if batch:
+            self.bufs = [b for b, _ in self.dec.decode_batch(self.files)] if self.files else []
+        else:
+            self.bufs = [self.dec.decode(*self.files[0])[0]]
+        return [ln for _, ln in self.files]
+
+    def step(self):
+        if not self.files:
+            return
+        if self.batch:
+            self.dec.launch_batch(self.files, self.bufs, self.stream)
+        else:
+            self.dec.launch(self.files[0][0], self.files[0][1], self.bufs[0], self.stream)
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize(self.device)
+
+    def infos(self):
+        return [self.dec.info(b) for b in self.bufs]
+
+    def set_timing(self, slots: int):
+        from recordio import _lib as L
+
+        L.lib().rio_ctx_set_timing(self.dec.ctx, slots)
+
+    def stage_ms(self):
+        return self.dec.stage_ms() if self.files else []
+
+    def evict(self):
+        """Write 1 GiB of HBM (pushes the decode's working set out of the MALL)."""
+        import torch
+
+        if not hasattr(self, "_evict"):
+            self._evict = torch.empty(1 << 30, dtype=torch.uint8, device=self.device)
+        self._evict.fill_(1)
+
+    def rec_offs(self, n):
+        return self.bufs[0].rec_off[:n].cpu().numpy()
+
+
+def plan_files(config: str, world: int, rank: int) -> list:
+    """Seeds of the files this rank decodes: C4's fixed 8-file set sharded round-robin over the
+    ranks (BASELINE configs[3]), otherwise one rank-seeded file per GPU."""
+    if config in MULTI_FILE:
+        n_files, seed0 = MULTI_FILE[config]
+        return [seed0 + f for f in shard_files(n_files, world, rank)]
+    return [rank_seed(rank)]
+
+
+def run_decode(args, world, rank, backend, sizes=None) -> dict:
+    """One decode config on this rank: plan and generate its files, hand them to the backend (the
+    device), warm up, time exactly args.steps steps between barriers, reduce over ranks (gloo) and
+    build the JSON line. `sizes` = (records, record_bytes) overrides the config's (tests)."""
     from recordio import _lib as L
     from recordio import generate
-    from recordio.device import DeviceDecoder, to_device_file
 
     n_rec, rec_len, comp, kind, desc = CONFIGS[args.config]
+    if sizes:
+        n_rec, rec_len = sizes
     threads = min(16, os.cpu_count() or 1)
-    # C4 (BASELINE configs[3]): a fixed set of 8 files sharded over the ranks, decoded per step by
-    # one rio_device_decode_batch call; the other configs: one rank-seeded file per GPU
-    if args.config in MULTI_FILE:
-        n_files, seed0 = MULTI_FILE[args.config]
-        mine = shard_files(n_files, world, rank)
-        seeds = [seed0 + f for f in mine]
-    else:
-        mine, seeds = [rank], [rank_seed(rank)]
-    images = [generate(n_rec, rec_len, comp, kind=kind, seed=sd, threads=threads) for sd in seeds]
-    files = [to_device_file(img, local) for img in images]
-    dec = DeviceDecoder(local)
-    stream = torch.cuda.current_stream(device)
     batch = args.config in MULTI_FILE
-    if batch:
-        outs = dec.decode_batch(files) if files else []
-        bufs = [b for b, _ in outs]
-
-        def step():
-            if files:
-                dec.launch_batch(files, bufs, stream)
-    else:
-        b0, _ = dec.decode(*files[0])
-        bufs = [b0]
-
-        def step():
-            dec.launch(files[0][0], files[0][1], bufs[0], stream)
-
+    seeds = plan_files(args.config, world, rank)
+    images = [generate(n_rec, rec_len, comp, kind=kind, seed=sd, threads=threads) for sd in seeds]
+    lengths = backend.load(images, batch)
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
-    infos = [dec.info(b) for b in bufs]
+        backend.step()
+    backend.sync()
+    infos = backend.infos()
     for info in infos:
         if info["status"] != L.RIO_EOF or info["n_records"] != n_rec:
             raise RuntimeError(f"decode failed: {info}")
-    length = sum(ln for _, ln in files)  # input bytes of this rank per step
+    length = sum(lengths)  # input bytes of this rank per step
     n = sum(i["n_records"] for i in infos)
     nb = sum(i["total_out_bytes"] for i in infos)
 
-    L.lib().rio_ctx_set_timing(dec.ctx, args.steps)
+    backend.set_timing(args.steps)
     if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(device)
+        import torch.distributed as dist
+
+        dist.barrier()
+    backend.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(device)
+        backend.step()
+    backend.sync()
     dt = time.perf_counter() - t0
     if world > 1:
-        torch.distributed.barrier()
-    stage = dec.stage_ms() if files else []  # per-stage HIP-event means over the timed steps
-    L.lib().rio_ctx_set_timing(dec.ctx, 1)
+        dist.barrier()
+    stage = backend.stage_ms()  # per-stage HIP-event means over the timed steps
+    backend.set_timing(1)
 
-    value, ms_per_step, dt_max = job_throughput(dt, length, args.steps, world, device)
+    value, ms_per_step, dt_max = job_throughput(dt, length, args.steps, world)
 
     # SURVEY §8d: when input + output fit the 256 MB MALL (C1), back-to-back steps re-read a warm
     # cache. A second pass writes 1 GiB between decodes (outside the per-stage HIP events) and
     # reports the cold-cache stage times beside the headline.
     mall_flushed = None
-    if files and length + nb < (512 << 20):
-        evict = torch.empty(1 << 30, dtype=torch.uint8, device=device)
-        L.lib().rio_ctx_set_timing(dec.ctx, args.steps)
+    if lengths and length + nb < (512 << 20):
+        backend.set_timing(args.steps)
         for _ in range(args.steps):
-            evict.fill_(1)
-            step()
-        torch.cuda.synchronize(device)
-        cold = dec.stage_ms()
-        L.lib().rio_ctx_set_timing(dec.ctx, 1)
-        del evict
+            backend.evict()
+            backend.step()
+        backend.sync()
+        cold = backend.stage_ms()
+        backend.set_timing(1)
         if len(cold) == 4:
             cold_ms = sum(cold)
             mall_flushed = {"ms_per_step": round(cold_ms, 4), "value": round(length / (cold_ms * 1e-3) / 2**30, 3),
@@ -923,7 +943,7 @@ def main():
     # roofline of the dominant kernel (Snappy / copy decode): algorithmic bytes per launch =
     # input file bytes (headers + payloads read once) + decoded bytes written once
     # + 8(N+1) out_off + 8N rec_off + N flags read
-    alg_bytes = length + nb + 8 * (n + len(files)) + 8 * n + n
+    alg_bytes = length + nb + 8 * (n + len(lengths)) + 8 * n + n
     decode_ms = stage[3] if len(stage) == 4 else float("nan")
     achieved = alg_bytes / (decode_ms * 1e-3) / 1e9
     traffic = None
@@ -962,7 +982,7 @@ def main():
                  else ", one file per rank"),
         "config": {"workload": desc, "records": n, "record_bytes": rec_len, "file_bytes": length,
                    "decoded_bytes": nb, "compression": {0: "none", 1: "gzip", 2: "snappy"}[comp],
-                   "files_this_rank": len(files),
+                   "files_this_rank": len(lengths),
                    "parallelism": f"file-sharded x{world} ({total_files} files), no data-path collectives"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": kernel,
@@ -977,10 +997,45 @@ def main():
     if mall_flushed:
         line["mall_flushed"] = mall_flushed
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec_offs = None if batch else bufs[0].rec_off[:n].cpu().numpy()
+        rec_offs = None if batch else backend.rec_offs(n)
         line["cpu_baseline"] = cpu_baseline(images, rec_offs, n_rec)
     if rank == 0 and world == 1 and not args.no_e2e and not batch:
         line["e2e"] = e2e_rate(images[0], nb)
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_latest.json"))
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    import numpy as np
+    import torch
+
+    torch.cuda.set_device(local)
+    device = torch.device(f"cuda:{local}")
+    if world > 1:
+        import torch.distributed as dist
+
+        # gloo on the host: the barrier and the max/sum over ranks are the job's only collectives
+        # (the decode path has none: files are sharded, north_star "no RCCL")
+        dist.init_process_group(backend="gloo")
+
+    if args.config in ("c5", "wal", "idx", "enc", "readat"):
+        {"c5": run_sstable, "wal": run_wal, "idx": run_index, "enc": run_encode, "readat": run_readat}[args.config](
+            args, world, rank, local, device)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    line = run_decode(args, world, rank, DeviceBackend(local, device))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

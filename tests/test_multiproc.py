@@ -1,9 +1,11 @@
 """World-size-2 rehearsal of the file-sharded multi-GPU job on CPU (gloo backend).
 
 The decode path shards by file with no data-path collective: every rank
-decodes its own file and the job reports the slowest rank's time and the summed input bytes. This
-test runs bench.py's own sharding / seeding / reduction code in two gloo processes; the per-rank
-decode is the CPU oracle standing in for the device (the device leg is bench.py on the GPU box).
+decodes its own files and the job reports the slowest rank's time and the summed input bytes. These
+tests run bench.py's own per-rank code (bench.run_decode: file plan, generation, warm-up, barriers,
+timed steps, gloo reductions, the JSON line) in two gloo processes. The single substitution is the
+device call itself: a backend with bench.DeviceBackend's interface that decodes with the CPU oracle,
+because this container has no GPU (the device leg is bench.py on the GPU box).
 """
 import hashlib
 import os
@@ -67,3 +69,87 @@ def _worker(rank: int, world: int, port: int):
 
 def test_file_sharded_job_world2():
     mp.spawn(_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+class OracleBackend:
+    """bench.DeviceBackend's interface with the device call replaced by the CPU oracle."""
+
+    def __init__(self):
+        self.steps = 0
+
+    def load(self, images, batch):
+        self.images, self.batch = images, batch
+        self.step()
+        return [int(img.shape[0]) for img in images]
+
+    def step(self):
+        import oracle_py as orc
+
+        self.res = [orc.file_reader_decode_arrays(img) for img in self.images]
+        self.steps += 1
+
+    def sync(self):
+        pass
+
+    def infos(self):
+        return [{k: r[k] for k in ("status", "n_records", "total_out_bytes")} for r in self.res]
+
+    def set_timing(self, slots):
+        pass
+
+    def stage_ms(self):
+        return [0.01, 0.01, 0.01, 0.1] if self.images else []
+
+    def evict(self):
+        pass
+
+    def rec_offs(self, n):
+        return self.res[0]["rec_off"][:n]
+
+
+def _run_decode_worker(rank: int, world: int, port: int, config: str, q):
+    for p in (REPO, os.path.join(REPO, "go-sstables_amd"), os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import argparse
+
+        import bench
+
+        args = argparse.Namespace(config=config, steps=3, warmup=1, no_cpu_baseline=True, no_e2e=True,
+                                  traffic_json="/nonexistent")
+        be = OracleBackend()
+        line = bench.run_decode(args, world, rank, be, sizes=(150, 2048))
+        q.put((rank, bench.plan_files(config, world, rank), be.steps, line))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config,files_per_rank", [("c4", 4), ("c2", 1)])
+def test_bench_run_decode_world2(config, files_per_rank):
+    """bench.run_decode on two gloo ranks: C4's 8 files split 4/4 with no overlap, one file per rank
+    otherwise; both ranks report the same whole-job value (sum of bytes over the max time)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_run_decode_worker, args=(r, 2, port, config, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict((r, (seeds, steps, line)) for r, seeds, steps, line in (q.get(timeout=300) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seeds = [got[r][0] for r in range(2)]
+    assert all(len(s) == files_per_rank for s in seeds) and not set(seeds[0]) & set(seeds[1])
+    if config == "c4":
+        assert sorted(seeds[0] + seeds[1]) == list(range(100, 108))
+    for r in range(2):
+        _, steps, line = got[r]
+        # load + warm-up + exactly args.steps timed + the cold-cache (MALL-flushed) pass of small files
+        assert steps == 1 + 1 + 3 + 3 and "mall_flushed" in line
+        assert line["n_gpus"] == 2 and line["config"]["files_this_rank"] == files_per_rank
+        assert line["config"]["records"] == 150 * files_per_rank
+    assert got[0][2]["value"] == got[1][2]["value"] > 0
