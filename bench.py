@@ -826,11 +826,13 @@ class DeviceBackend:
 
         self.files = [to_device_file(img, self.local) for img in images]
         self.batch = batch
+        # the header's compression type (the host has the image): only that codec's kernels launch
+        self.comp = int(images[0][4]) if images and len(images[0]) >= 8 else None
         self.stream = torch.cuda.current_stream(self.device)
         if batch:
             self.bufs = [b for b, _ in self.dec.decode_batch(self.files)] if self.files else []
         else:
-            self.bufs = [self.dec.decode(*self.files[0])[0]]
+            self.bufs = [self.dec.decode(*self.files[0], comp=self.comp)[0]]
         return [ln for _, ln in self.files]
 
     def step(self):
@@ -839,7 +841,7 @@ class DeviceBackend:
         if self.batch:
             self.dec.launch_batch(self.files, self.bufs, self.stream)
         else:
-            self.dec.launch(self.files[0][0], self.files[0][1], self.bufs[0], self.stream)
+            self.dec.launch(self.files[0][0], self.files[0][1], self.bufs[0], self.stream, self.comp)
 
     def sync(self):
         import torch

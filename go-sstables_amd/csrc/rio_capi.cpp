@@ -32,6 +32,7 @@
 
 namespace rio {
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* key_off,
@@ -214,6 +215,8 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     P.len = len;
     P.chunk_bytes = ctx->chunk_bytes;
     P.coop_min = ctx->coop_min;
+    P.comp_hint = RIO_COMP_UNKNOWN;
+    P.zero_done = 0;
     P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + ctx->chunk_bytes - 1) / ctx->chunk_bytes : 0;
     P.slots = ctx->chunk_bytes / 6 + 1;
     P.n_blocks = (P.n_chunks + 255) / 256;
@@ -328,7 +331,15 @@ extern "C" int rio_ctx_last_stage_ms(rio_ctx* c, float* ms, int n) {
 extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                                  uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                                  uint64_t rec_cap, rio_file_info* d_info, void* stream) {
+    return rio_device_decode_ex(ctx, d_file, len, RIO_COMP_UNKNOWN, d_out, out_cap, d_out_off, d_rec_off, d_flags,
+                                rec_cap, d_info, stream);
+}
+
+extern "C" int rio_device_decode_ex(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint32_t compression,
+                                    uint8_t* d_out, uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off,
+                                    uint8_t* d_flags, uint64_t rec_cap, rio_file_info* d_info, void* stream) {
     if (!ctx || !d_file || !d_out_off || !d_rec_off || !d_flags || !d_info) return RIO_ERR_ARG;
+    if (compression > RIO_COMP_LZW && compression != RIO_COMP_UNKNOWN) return RIO_ERR_ARG;
     if ((reinterpret_cast<uintptr_t>(d_file) & 15) != 0) return RIO_ERR_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     FrameParams P;
@@ -345,9 +356,10 @@ extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t l
     P.rec_pay = ctx->fa.rec_pay.as<uint64_t>();
     HIP_TRY(ctx->fa.rec_desc.ensure((rec_cap + 1) * 16));
     P.rec_desc = ctx->fa.rec_desc.as<uint4>();
+    P.comp_hint = compression;
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     hipEvent_t* ev = ctx->next_events();
-    HIP_TRY(launch_phase_a(P, s, ev));
+    HIP_TRY(launch_frame(P, s, ev));
     HIP_TRY(launch_phase_b(P, s, ev));
     return RIO_OK;
 }
@@ -397,7 +409,7 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
         hipEvent_t* e = (ev && g == 0) ? ev : nullptr;
         hipEvent_t* last = (ev && g + kMaxBatch >= n_files) ? ev : nullptr;
         if (e) HIP_TRY(hipEventRecord(e[0], s));
-        for (uint32_t j = 0; j < B.n; j++) HIP_TRY(launch_phase_a(B.f[j], s, nullptr));
+        for (uint32_t j = 0; j < B.n; j++) HIP_TRY(launch_frame(B.f[j], s, nullptr));
         if (last) {
             HIP_TRY(hipEventRecord(last[1], s));
             HIP_TRY(hipEventRecord(last[2], s));
@@ -561,6 +573,8 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
     HIP_TRY(ctx->rec_off.ensure(n * 8 + 8));
     HIP_TRY(ctx->flags.ensure(n + 8));
     FrameParams P = ctx->last;
+    P.zero_done = 1;               // phase A ran k_zero (rio_frame's status is final)
+    P.comp_hint = fi.compression;  // from the file header rio_frame read
     P.out = ctx->out.as<uint8_t>();
     P.out_cap = nb;
     P.out_off = ctx->out_off.as<uint64_t>();

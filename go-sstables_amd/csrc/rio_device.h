@@ -75,7 +75,9 @@ struct ScanState {
     uint32_t capacity_fail;
     uint32_t huge_streams;  // a record stream exceeds 32-bit positions: k_snappy_global runs
     uint32_t any_mixed;     // snappy: some record is not one literal covering its output (k_place);
-                            // 0 => every record is copied by k_snappy_literal instead of k_snappy_pipe
+                            // 0 => every record is copied by k_copy_records instead of k_snappy_pipe
+    uint32_t scan_ticket;   // k_scan_blocks: the last block to finish runs the top-level scan
+    uint32_t finish_ticket; // k_finish: the last block to finish publishes the result
 };
 
 // Result of the single-record (ReadNextAt) kernel.
@@ -110,6 +112,10 @@ struct FrameParams {
     // Snappy: files whose mean decoded record is at least this many bytes (and files past 32-bit
     // lane positions) take the wave-per-record decoder k_snappy_coop instead of k_snappy_pipe
     uint64_t coop_min;
+    // the file header's compression type as the host knows it (RIO_COMP_UNKNOWN: every decoder is
+    // launched and exits unless the file is its own); k_finish rejects a file that contradicts it
+    uint32_t comp_hint;
+    uint32_t zero_done;  // the zero-tail check already ran (host API phase A): k_place skips it
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)
     RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix

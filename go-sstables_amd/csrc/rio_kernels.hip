@@ -326,10 +326,23 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
 }
 
 // ------------------------------------------------------------------------------------------
-// k_header
+// File header (readFileHeaderFromBuffer, common_reader.go:22-44) and the per-call state reset; run
+// by k_walk: every wave reads the 8 header bytes itself, block 0's first thread resets the state
+// the later kernels accumulate into (no separate launch)
 // ------------------------------------------------------------------------------------------
-__global__ void k_header(FrameParams P) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ __forceinline__ int file_header_status(const FrameParams& P, uint32_t& v, uint32_t& c) {
+    v = c = 0;
+    if (P.len < RIO_FILE_HEADER_BYTES) return RIO_ERR_SHORT_FILE_HEADER;
+    const uint8_t* f = P.file;
+    v = f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+    c = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+    if (v > RIO_VERSION4 || v < RIO_VERSION1) return RIO_ERR_VERSION;
+    if (c > RIO_COMP_LZW) return RIO_ERR_COMPRESSION_TYPE;
+    if (v < RIO_VERSION3 || c == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;  // reference reader keeps these
+    return RIO_OK;
+}
+
+__device__ void init_state(const FrameParams& P) {
     ScanState* st = P.state;
     const uint8_t* f = P.file;
     st->n_records = 0;
@@ -348,6 +361,8 @@ __global__ void k_header(FrameParams P) {
     st->huge_streams = 0;
     st->any_mixed = 0;
     st->slow = 0;
+    st->scan_ticket = 0;
+    st->finish_ticket = 0;
     if (P.len < RIO_FILE_HEADER_BYTES) {
         st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;
         st->version = st->compression = 0;
@@ -550,13 +565,13 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
 #endif
     __shared__ WalkLds W[kWalkWaves];
     __shared__ uint32_t crct[1024];
+    if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
     crc32c_tab_init(crct);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
-    const ScanState* st = P.state;
-    if (c >= P.n_chunks || st->hdr_status != RIO_OK) return;  // wave-uniform
+    uint32_t ver, comp;
+    if (c >= P.n_chunks || file_header_status(P, ver, comp) != RIO_OK) return;  // wave-uniform
     WalkLds& L = W[wv];
-    const uint32_t ver = st->version, comp = st->compression;
     const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
     const uint8_t* f = P.file;
     uint64_t* so = P.scratch_off + c * P.slots;
@@ -736,12 +751,16 @@ __device__ __forceinline__ RunSum chunk_run(const FrameParams& P, uint64_t c) {
 
 constexpr int kScanBlock = 256;
 
-// Level 1: inclusive scan of 256 chunk runs per block in LDS (Hillis-Steele, 8 steps).
+__device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]);
+
+// Level 1: inclusive scan of 256 chunk runs per block in LDS (Hillis-Steele, 8 steps). The last
+// block to finish (arrival ticket) runs level 2 over the block runs: one launch for the scan.
 __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
     __shared__ RunSum buf[2][kScanBlock];
+    __shared__ uint32_t last;
     const int t = threadIdx.x;
     const uint64_t c = (uint64_t)blockIdx.x * kScanBlock + t;
-    if (P.state->hdr_status != RIO_OK) return;
+    if (P.state->hdr_status != RIO_OK) return;  // block-uniform
     RunSum v = c < P.n_chunks ? chunk_run(P, c) : run_identity();
     int cur = 0;
     buf[cur][t] = v;
@@ -755,6 +774,16 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
     }
     if (c < P.n_chunks) P.chunk_excl[c] = t > 0 ? buf[cur][t - 1] : run_identity();
     if (t == kScanBlock - 1) P.block_runs[blockIdx.x] = buf[cur][t];
+    // release this block's run, take a ticket; the last arriver acquires every block's run
+    __syncthreads();
+    if (t == 0) {
+        __threadfence();
+        last = atomicAdd(&P.state->scan_ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    scan_top(P, buf);
 }
 
 // Sequential repair (slow path): walks the true chain chunk by chunk, re-walking any chunk whose
@@ -800,13 +829,11 @@ __device__ void slow_path(const FrameParams& P, uint32_t ver, uint32_t comp) {
     }
 }
 
-// Level 2: one workgroup scans the block runs (tiles of 1024 with a carry), decides fast/slow
-// path and the terminal status.
-__global__ void __launch_bounds__(1024) k_scan_top(FrameParams P) {
-    __shared__ RunSum buf[2][1024];
+// Level 2 (k_scan_blocks' last block): scans the block runs in tiles of kScanBlock with a carry,
+// decides fast/slow path and the terminal status.
+__device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
     __shared__ RunSum carry_s;
     ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK) return;
     const uint32_t ver = st->version, comp = st->compression;
     const int t = threadIdx.x;
     if (P.n_chunks == 0) {
@@ -818,13 +845,13 @@ __global__ void __launch_bounds__(1024) k_scan_top(FrameParams P) {
     }
     if (t == 0) carry_s = run_identity();
     __syncthreads();
-    for (uint64_t base = 0; base < P.n_blocks; base += 1024) {
+    for (uint64_t base = 0; base < P.n_blocks; base += kScanBlock) {
         const uint64_t b = base + t;
         RunSum v = b < P.n_blocks ? P.block_runs[b] : run_identity();
         int cur = 0;
         buf[cur][t] = v;
         __syncthreads();
-        for (int d = 1; d < 1024; d <<= 1) {
+        for (int d = 1; d < kScanBlock; d <<= 1) {
             RunSum x = buf[cur][t];
             if (t >= d) x = combine(buf[cur][t - d], x);
             buf[cur ^ 1][t] = x;
@@ -835,7 +862,7 @@ __global__ void __launch_bounds__(1024) k_scan_top(FrameParams P) {
         RunSum excl = combine(carry, t > 0 ? buf[cur][t - 1] : run_identity());
         if (b < P.n_blocks) P.block_excl[b] = excl;
         __syncthreads();
-        if (t == 1023) carry_s = combine(carry, buf[cur][t]);
+        if (t == kScanBlock - 1) carry_s = combine(carry, buf[cur][t]);
         __syncthreads();
     }
     const RunSum total = carry_s;
@@ -894,11 +921,27 @@ __device__ __forceinline__ bool snappy_single_literal(const uint8_t* p, uint64_t
 // Placement: one wave per chunk copies its owned scratch records to their global index (64
 // records per step, out_off by a wave prefix sum: coalesced stores instead of one thread's serial
 // record loop).
+// Its prologue also does what used to be two launches: the capacity check + sentinel out_off[n]
+// (block 0) and, on the device-resident path, the zero-tail test of a magic mismatch (grid-stride).
 __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const ScanState* st = P.state;
-    if (c >= P.n_chunks || st->hdr_status != RIO_OK) return;  // wave-uniform
+    ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (st->n_records > P.rec_cap || st->total_bytes > P.out_cap)
+            st->capacity_fail = 1;
+        else
+            P.out_off[st->n_records] = st->total_bytes;
+    }
+    if (!P.zero_done && st->zero_from != kNone) {
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        uint32_t nz = 0;
+        for (uint64_t q = st->zero_from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < P.len; q += stride)
+            nz |= P.file[q];
+        if (__any(nz != 0) && lane == 0) atomicOr(&st->zero_nonzero, 1u);
+    }
+    if (c >= P.n_chunks) return;  // wave-uniform
     ChunkPlace pl;
     if (st->slow) {
         pl = P.place[c];
@@ -961,18 +1004,6 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     if (snappy && __any(mixed) && lane == 0) P.state->any_mixed = 1u;
 }
 
-// Capacity check + sentinel out_off[n] + zero-tail range.
-__global__ void k_post_scan(FrameParams P) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK) return;
-    if (st->n_records > P.rec_cap || st->total_bytes > P.out_cap) {
-        st->capacity_fail = 1;
-        return;
-    }
-    P.out_off[st->n_records] = st->total_bytes;
-}
-
 __global__ void __launch_bounds__(256) k_zero(FrameParams P) {
     ScanState* st = P.state;
     const uint64_t from = st->zero_from;
@@ -999,37 +1030,15 @@ __device__ __forceinline__ void copy_fwd(uint8_t* dst, uint64_t d, const uint8_t
     }
 }
 
-// Uncompressed files: 16-lane groups, one record per group; each lane moves 16 bytes per step
-// (unaligned load and store; the record's last piece is stored exactly).
-__global__ void __launch_bounds__(256) k_decode_copy(FrameParams P) {
+// Uncompressed files, and Snappy files whose every record is one literal (incompressible values:
+// the reference benchmark's random records; k_snappy_pipe exits at once for those): 16-lane groups,
+// one record per group; each lane moves 16 bytes per step (unaligned load and store; the record's
+// last piece is stored exactly).
+__global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
     const ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_NONE) return;
-    const uint64_t n = st->n_records;
-    const uint32_t lane = threadIdx.x & 15;
-    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
-    for (uint64_t i = grp; i < n; i += ngrp) {
-        const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
-        if (o1 == o0) continue;
-        const uint8_t* src = P.file + P.rec_off[i] + (P.rec_pay[i] & 0xFF);
-        uint8_t* dst = P.out + o0;
-        const uint64_t len = o1 - o0;
-        for (uint64_t k = 16 * lane; k < len; k += 256) {
-            const uint4 v = ldu16(src + k);
-            if (k + 16 <= len)
-                stu16(dst + k, v);
-            else
-                st_partial(dst + k, v, (uint32_t)(len - k));
-        }
-    }
-}
-
-// Snappy files whose every record is one literal (incompressible values: the reference benchmark's
-// random records) skip the lane-per-record decoder: 16-lane groups copy each literal's bytes like
-// k_decode_copy. k_snappy_pipe exits at once for such files (rio_snappy.hip).
-__global__ void __launch_bounds__(256) k_snappy_literal(FrameParams P) {
-    const ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || st->any_mixed) return;
+    if (st->hdr_status != RIO_OK || st->capacity_fail) return;
+    const bool none = st->compression == RIO_COMP_NONE;
+    if (!none && !(st->compression == RIO_COMP_SNAPPY && !st->any_mixed)) return;
     const uint64_t n = st->n_records;
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
@@ -1039,7 +1048,7 @@ __global__ void __launch_bounds__(256) k_snappy_literal(FrameParams P) {
         if (len == 0) continue;
         const uint64_t pay = P.rec_pay[i];  // 64-bit stream position and length (any file size)
         const uint8_t* s0 = P.file + P.rec_off[i] + (pay & 0xFF);
-        const uint8_t* src = s0 + snappy_literal_hdr(s0, pay >> 8, len);
+        const uint8_t* src = none ? s0 : s0 + snappy_literal_hdr(s0, pay >> 8, len);
         uint8_t* dst = P.out + o0;
         for (uint64_t k = 16 * lane; k < len; k += 256) {
             const uint4 v = ldu16(src + k);
@@ -1051,8 +1060,7 @@ __global__ void __launch_bounds__(256) k_snappy_literal(FrameParams P) {
     }
 }
 
-__global__ void k_finalize(FrameParams P) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void finalize_info(const FrameParams& P) {
     ScanState* st = P.state;
     rio_file_info info;
     info.version = st->version;
@@ -1102,7 +1110,52 @@ __global__ void k_finalize(FrameParams P) {
             info.n_bad = st->n_bad;  // (records past a hand-back point never reach this kernel's view)
         }
     }
+    if (P.comp_hint != RIO_COMP_UNKNOWN && st->hdr_status == RIO_OK && st->compression != P.comp_hint) {
+        info.status = RIO_ERR_ARG;  // the caller's hint launched another codec's kernels: nothing decoded
+        info.n_records = 0;
+        info.total_out_bytes = 0;
+    }
     *P.info = info;
+}
+
+// The framing result (host API phase A: the sizes the caller allocates for)
+__global__ void k_finalize(FrameParams P) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) finalize_info(P);
+}
+
+// Last decode step: records of Snappy lanes that met a corrupt record are decoded again one thread
+// each (k_snappy_pipe lists the lanes; every record when more than kFailLanes did) in place (a record
+// that decoded is rewritten with the same bytes) and flagged where golang/snappy's Decode returns
+// ErrCorrupt; then the last block to finish publishes the result (k_finalize's work). One launch.
+__global__ void __launch_bounds__(256) k_finish(FrameParams P) {
+    __shared__ uint32_t last;
+    ScanState* st = P.state;
+    if (st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_SNAPPY && st->n_fail_lanes) {
+        auto verify = [&](uint64_t i) {
+            if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) return;
+            const uint64_t pay = P.rec_pay[i], o0 = P.out_off[i], o1 = P.out_off[i + 1];
+            if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), pay >> 8, P.out + o0, o1 - o0))
+                mark_bad(P, i);
+        };
+        if (st->n_fail_lanes > kFailLanes) {  // the list overflowed: every record
+            const uint64_t n = st->n_records, stride = (uint64_t)gridDim.x * blockDim.x;
+            for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) verify(i);
+        } else {
+            for (uint64_t l = blockIdx.x; l < st->n_fail_lanes; l += gridDim.x)
+                for (uint64_t i = P.fail_lanes[2 * l] + threadIdx.x; i < P.fail_lanes[2 * l + 1]; i += blockDim.x)
+                    verify(i);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&st->finish_ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        finalize_info(P);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1574,58 +1627,59 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
     return (unsigned)(b == 0 ? 1 : b);
 }
 
-// Phase A: framing + scan + zero-tail check; k_finalize publishes the framing result (sizes).
-hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
+// Framing: k_walk (file header, state reset, chunk walk), k_scan_blocks (both scan levels).
+hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], s);
-    hipLaunchKernelGGL(k_header, dim3(1), dim3(64), 0, s, P);
     hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, P);
-    hipLaunchKernelGGL(k_zero, dim3(256), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, P);
     if (ev) (void)hipEventRecord(ev[2], s);
     return hipGetLastError();
 }
 
-// Phase B: placement into the caller's arrays, decode, final result.
-hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool coop);  // rio_snappy.hip
-hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s);             // rio_snappy.hip
-hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s);    // rio_gzip.hip
-
-// Phase B: placement into the caller's arrays, decode, final result. Both decoders check the
-// file's compression type on the device and exit at once when it is not theirs.
-hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
-    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_post_scan, dim3(1), dim3(64), 0, s, P);
-    if (ev) (void)hipEventRecord(ev[3], s);
-    hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_snappy_literal, dim3(2048), dim3(256), 0, s, P);
-    launch_snappy_decode(P, s, true);
-    launch_gzip_decode(P, s);
-    if (ev) (void)hipEventRecord(ev[4], s);
+// Host API phase A: framing, then the zero-tail test and the sizes (k_finalize) for the caller.
+hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
+    launch_frame(P, s, ev);
+    hipLaunchKernelGGL(k_zero, dim3(256), dim3(256), 0, s, P);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, P);
     return hipGetLastError();
 }
 
-// rio_device_decode_batch: phase B of every file of the batch; the large-record Snappy decoder runs
-// once over all of them (k_snappy_coop_batch), the other decode kernels per file
+hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main);  // rio_snappy.hip
+hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s);             // rio_snappy.hip
+hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s);              // rio_gzip.hip
+
+// the decoders of one file: by the compression hint, or all of them (each exits unless the file is
+// its own)
+static void launch_decoders(const FrameParams& P, hipStream_t s, bool snappy_main) {
+    const uint32_t c = P.comp_hint;
+    const bool any = c == RIO_COMP_UNKNOWN;
+    if (any || c == RIO_COMP_NONE || c == RIO_COMP_SNAPPY)
+        hipLaunchKernelGGL(k_copy_records, dim3(2048), dim3(256), 0, s, P);
+    if ((any || c == RIO_COMP_SNAPPY) && snappy_main) launch_snappy_decode(P, s, true);
+    if (any || c == RIO_COMP_GZIP) launch_gzip_decode(P, s);
+}
+
+// Decode: placement (+ capacity check, zero tail), the decoders, k_finish (verify + result).
+hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
+    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+    if (ev) (void)hipEventRecord(ev[3], s);
+    launch_decoders(P, s, true);
+    if (ev) (void)hipEventRecord(ev[4], s);
+    hipLaunchKernelGGL(k_finish, dim3(64), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+// rio_device_decode_batch: phase B of every file of the batch; the Snappy decoders run once over all
+// of them (k_snappy_pipe_batch / k_snappy_coop_batch), the other decode kernels per file
 hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev) {
-    for (uint32_t f = 0; f < B.n; f++) {
+    for (uint32_t f = 0; f < B.n; f++)
         hipLaunchKernelGGL(k_place, dim3(blocks_for(B.f[f].n_chunks, 4)), dim3(256), 0, s, B.f[f]);
-        hipLaunchKernelGGL(k_post_scan, dim3(1), dim3(64), 0, s, B.f[f]);
-    }
     if (ev) (void)hipEventRecord(ev[3], s);
     launch_snappy_batch(B, s);
-    for (uint32_t f = 0; f < B.n; f++) {
-        const FrameParams& P = B.f[f];
-        hipLaunchKernelGGL(k_decode_copy, dim3(2048), dim3(256), 0, s, P);
-        hipLaunchKernelGGL(k_snappy_literal, dim3(2048), dim3(256), 0, s, P);
-        launch_snappy_decode(P, s, false);
-        launch_gzip_decode(P, s);
-    }
+    for (uint32_t f = 0; f < B.n; f++) launch_decoders(B.f[f], s, false);
     if (ev) (void)hipEventRecord(ev[4], s);
-    for (uint32_t f = 0; f < B.n; f++) hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, B.f[f]);
+    for (uint32_t f = 0; f < B.n; f++) hipLaunchKernelGGL(k_finish, dim3(64), dim3(256), 0, s, B.f[f]);
     return hipGetLastError();
 }
 

@@ -352,130 +352,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     return !bad;
 }
 
-__global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || snappy_wide(P, st))
-        return;
-    if (!st->any_mixed) return;  // every record is one literal: k_snappy_literal copies them
-    if (st->n_records && st->total_bytes / st->n_records >= P.coop_min) return;  // large records: k_snappy_coop
-    const uint64_t n = st->n_records;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    // lane number: waves are numbered across workgroups first, so that a file with few records
-    // (fewer than lanes) spreads its active waves over every CU
-    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t t = (((uint64_t)wave * gridDim.x + blockIdx.x) << 6) | lane;
-    // contiguous record ranges of ceil(n / T) records: lanes of a wave cover consecutive ranges,
-    // and a file with fewer records than lanes fills whole waves (the rest exit at once)
-    const uint64_t rpl = (n + T - 1) / T;
-    const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
-    if ((t & ~63ull) * rpl >= n) return;  // the whole wave is idle (wave-uniform exit)
-    uint8_t* sink = P.sink + (t >> 6) * 64;  // the wave's placeholder line
-    uint64_t bad_rec = 0;
-    if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
-        // a record of this lane did not decode: k_snappy_verify re-decodes the lane's records one
-        // thread each and flags the failing ones
-        const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
-        if (at < kFailLanes) {
-            P.fail_lanes[2 * at] = r0;
-            P.fail_lanes[2 * at + 1] = r1;
-        }
-    }
-}
-
-// rio_device_decode_batch: one launch for every lane-decoder file of the batch. The lanes of the grid
-// are split over the files by record count (whole waves per file, so the file's parameters stay
-// wave-uniform scalars), which is what fills the chip when each file alone has fewer records than
-// lanes (BASELINE configs[3]: 8 files of 16384 x 64 KiB records).
-__device__ __forceinline__ bool pipe_active(const FrameParams& P) {
-    const ScanState* st = P.state;
-    return st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_SNAPPY && st->any_mixed &&
-           !snappy_wide(P, st) && !(st->n_records && st->total_bytes / st->n_records >= P.coop_min);
-}
-
-__global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
-    uint64_t N = 0;
-    for (uint32_t f = 0; f < B.n; f++)
-        if (pipe_active(B.f[f])) N += B.f[f].state->n_records;
-    if (N == 0) return;
-    // the fewest records per lane whose whole-wave shares (ceil per file) fit the grid: every wave
-    // of the grid is resident at once (2 per SIMD), so a share past it would run as a second round
-    uint64_t rpl = (N + 64 * waves - 1) / (64 * waves);
-    for (;;) {
-        uint64_t need = 0;
-        for (uint32_t f = 0; f < B.n; f++)
-            if (pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
-        if (need <= waves) break;
-        rpl++;
-    }
-    const uint64_t per_wave = 64 * rpl;
-    uint64_t w0 = 0;
-    for (uint32_t f = 0; f < B.n; f++) {
-        const FrameParams& P = B.f[f];
-        if (!pipe_active(P)) continue;
-        const uint64_t n = P.state->n_records, wf = (n + per_wave - 1) / per_wave;
-        if (wg < w0 + wf) {
-            const uint64_t t = ((wg - w0) << 6) | lane;
-            const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
-            uint8_t* sink = P.sink + wg * 64;
-            uint64_t bad_rec = 0;
-            if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
-                const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
-                if (at < kFailLanes) {
-                    P.fail_lanes[2 * at] = r0;
-                    P.fail_lanes[2 * at + 1] = r1;
-                }
-            }
-            return;
-        }
-        w0 += wf;
-    }
-}
-
-// Files with a record stream past 32-bit positions (never produced by an encoder: a record over
-// 4 GiB): every record decoded by one thread with byte loops straight to HBM.
-__global__ void __launch_bounds__(256) k_snappy_global(FrameParams P) {
-    ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->huge_streams ||
-        !st->any_mixed)
-        return;
-    const uint64_t n = st->n_records;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
-        const uint64_t pay = P.rec_pay[i], slen = pay >> 8;
-        const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
-        if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), slen, P.out + o0, o1 - o0))
-            mark_bad(P, i);
-    }
-}
-
-// Records of lanes that met a corrupt record (or of every lane when more than kFailLanes did): one
-// thread per record decodes it again in place (a record that decoded is rewritten with the same
-// bytes) and flags the ones that fail, exactly where golang/snappy's Decode returns ErrCorrupt.
-__global__ void __launch_bounds__(256) k_snappy_verify(FrameParams P) {
-    ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || st->n_fail_lanes == 0)
-        return;
-    auto verify = [&](uint64_t i) {
-        if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) return;
-        const uint64_t pay = P.rec_pay[i], o0 = P.out_off[i], o1 = P.out_off[i + 1];
-        if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), pay >> 8, P.out + o0, o1 - o0))
-            mark_bad(P, i);
-    };
-    if (st->n_fail_lanes > kFailLanes) {  // the list overflowed: every record
-        const uint64_t n = st->n_records, stride = (uint64_t)gridDim.x * blockDim.x;
-        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) verify(i);
-        return;
-    }
-    for (uint64_t l = blockIdx.x; l < st->n_fail_lanes; l += gridDim.x)
-        for (uint64_t i = P.fail_lanes[2 * l] + threadIdx.x; i < P.fail_lanes[2 * l + 1]; i += blockDim.x) verify(i);
-}
-
 // ------------------------------------------------------------------------------------------
 // k_snappy_coop: one wave per record, all 64 lanes on that record (files of large records: C4's
 // 64 KiB values; and files past the lane decoder's 32-bit positions). A record is decoded in
@@ -519,10 +395,9 @@ struct CoopLds {
 };
 
 __device__ __forceinline__ bool coop_active(const FrameParams& P, const ScanState* st) {
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->any_mixed ||
-        st->huge_streams)
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->any_mixed)
         return false;
-    return snappy_wide(P, st) || (st->n_records && st->total_bytes / st->n_records >= P.coop_min);
+    return st->huge_streams || snappy_wide(P, st) || (st->n_records && st->total_bytes / st->n_records >= P.coop_min);
 }
 
 // element header from its first 8 bytes (lo = bytes 0..3, hi = 4..7): header length, output length
@@ -803,6 +678,18 @@ __device__ __forceinline__ void coop_file(const FrameParams& P, CoopLds& S, uint
     const ScanState* st = P.state;
     if (!coop_active(P, st)) return;
     const uint64_t n = st->n_records;
+    if (st->huge_streams) {
+        // a record stream past 32-bit positions (never produced by an encoder: a record over 4 GiB):
+        // every record by one thread, byte loops straight to HBM
+        for (uint64_t i = wave * 64 + lane; i < n; i += nw * 64) {
+            if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
+            const uint64_t pay = P.rec_pay[i];
+            const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
+            if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), pay >> 8, P.out + o0, o1 - o0))
+                mark_bad(P, i);
+        }
+        return;
+    }
     uint8_t* sink = P.sink + (wave % ((uint64_t)kSnappyGrid * (kSnappyBlock / 64))) * 64;  // placeholder line
     for (uint64_t i = wave; i < n; i += nw) {
         if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
@@ -812,12 +699,6 @@ __device__ __forceinline__ void coop_file(const FrameParams& P, CoopLds& S, uint
     }
 }
 }  // namespace
-
-__global__ void __launch_bounds__(64 * kCoopWaves) k_snappy_coop(FrameParams P) {
-    __shared__ CoopLds lds[kCoopWaves];
-    const uint32_t wv = threadIdx.x >> 6;
-    coop_file(P, lds[wv], threadIdx.x & 63u, (uint64_t)blockIdx.x * kCoopWaves + wv, (uint64_t)gridDim.x * kCoopWaves);
-}
 
 // rio_device_decode_batch: the files one after the other, every wave of the grid on each (a wave
 // that finishes its share of file f goes on to file f + 1 at once: no grid-wide step)
@@ -829,6 +710,93 @@ __global__ void __launch_bounds__(64 * kCoopWaves) k_snappy_coop_batch(FrameBatc
                   (uint64_t)gridDim.x * kCoopWaves);
 }
 
+__global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
+    if (!st->any_mixed) return;  // every record is one literal: k_copy_records copies them
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (coop_active(P, st)) {  // large records / past 32-bit positions: the wave-per-record decoder
+        coop_file(P, reinterpret_cast<CoopLds*>(lds)[wave], lane, (uint64_t)blockIdx.x * (kSnappyBlock / 64) + wave,
+                  (uint64_t)gridDim.x * (kSnappyBlock / 64));
+        return;
+    }
+    const uint64_t n = st->n_records;
+    // lane number: waves are numbered across workgroups first, so that a file with few records
+    // (fewer than lanes) spreads its active waves over every CU
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (((uint64_t)wave * gridDim.x + blockIdx.x) << 6) | lane;
+    // contiguous record ranges of ceil(n / T) records: lanes of a wave cover consecutive ranges,
+    // and a file with fewer records than lanes fills whole waves (the rest exit at once)
+    const uint64_t rpl = (n + T - 1) / T;
+    const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
+    if ((t & ~63ull) * rpl >= n) return;  // the whole wave is idle (wave-uniform exit)
+    uint8_t* sink = P.sink + (t >> 6) * 64;  // the wave's placeholder line
+    uint64_t bad_rec = 0;
+    if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
+        // a record of this lane did not decode: k_snappy_verify re-decodes the lane's records one
+        // thread each and flags the failing ones
+        const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
+        if (at < kFailLanes) {
+            P.fail_lanes[2 * at] = r0;
+            P.fail_lanes[2 * at + 1] = r1;
+        }
+    }
+}
+
+// rio_device_decode_batch: one launch for every lane-decoder file of the batch. The lanes of the grid
+// are split over the files by record count (whole waves per file, so the file's parameters stay
+// wave-uniform scalars), which is what fills the chip when each file alone has fewer records than
+// lanes (BASELINE configs[3]: 8 files of 16384 x 64 KiB records).
+__device__ __forceinline__ bool pipe_active(const FrameParams& P) {
+    const ScanState* st = P.state;
+    return st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_SNAPPY && st->any_mixed &&
+           !snappy_wide(P, st) && !(st->n_records && st->total_bytes / st->n_records >= P.coop_min);
+}
+
+__global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
+    uint64_t N = 0;
+    for (uint32_t f = 0; f < B.n; f++)
+        if (pipe_active(B.f[f])) N += B.f[f].state->n_records;
+    if (N == 0) return;
+    // the fewest records per lane whose whole-wave shares (ceil per file) fit the grid: every wave
+    // of the grid is resident at once (2 per SIMD), so a share past it would run as a second round
+    uint64_t rpl = (N + 64 * waves - 1) / (64 * waves);
+    for (;;) {
+        uint64_t need = 0;
+        for (uint32_t f = 0; f < B.n; f++)
+            if (pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
+        if (need <= waves) break;
+        rpl++;
+    }
+    const uint64_t per_wave = 64 * rpl;
+    uint64_t w0 = 0;
+    for (uint32_t f = 0; f < B.n; f++) {
+        const FrameParams& P = B.f[f];
+        if (!pipe_active(P)) continue;
+        const uint64_t n = P.state->n_records, wf = (n + per_wave - 1) / per_wave;
+        if (wg < w0 + wf) {
+            const uint64_t t = ((wg - w0) << 6) | lane;
+            const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
+            uint8_t* sink = P.sink + wg * 64;
+            uint64_t bad_rec = 0;
+            if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
+                const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
+                if (at < kFailLanes) {
+                    P.fail_lanes[2 * at] = r0;
+                    P.fail_lanes[2 * at + 1] = r1;
+                }
+            }
+            return;
+        }
+        w0 += wf;
+    }
+}
+
 hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
     hipLaunchKernelGGL(k_snappy_pipe_batch, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, B);
     hipLaunchKernelGGL(k_snappy_coop_batch, dim3(kCoopGrid), dim3(64 * kCoopWaves), 0, s, B);
@@ -838,12 +806,8 @@ hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
 // main = false: the caller runs the lane and wave decoders for this file itself (a batch)
 hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main) {
     // 4 waves x 20 KiB = 80 KiB per workgroup: 2 workgroups (8 waves) per CU
-    if (main) {
+    if (main)
         hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, P);
-        hipLaunchKernelGGL(k_snappy_coop, dim3(kCoopGrid), dim3(64 * kCoopWaves), 0, s, P);
-    }
-    hipLaunchKernelGGL(k_snappy_global, dim3(64), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_snappy_verify, dim3(256), dim3(256), 0, s, P);
     return hipGetLastError();
 }
 

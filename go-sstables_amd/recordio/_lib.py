@@ -45,6 +45,7 @@ RIO_FLAG_NIL = 1
 RIO_FLAG_CORRUPT = 2
 RIO_FLAG_EOF = 4
 RIO_DEVICE_PAD = 64
+RIO_COMP_UNKNOWN = 0xFFFFFFFF
 COMP_NONE, COMP_GZIP, COMP_SNAPPY, COMP_LZW = 0, 1, 2, 3
 
 
@@ -107,6 +108,11 @@ _SIGS = {
     "rio_device_decode": (
         c_int,
         [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p],
+    ),
+    "rio_device_decode_ex": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+         c_void_p],
     ),
     "rio_device_decode_batch": (
         c_int,

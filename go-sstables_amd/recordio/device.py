@@ -57,13 +57,15 @@ class DeviceDecoder:
             info=torch.zeros(INFO_BYTES, dtype=torch.uint8, device=dev),
         )
 
-    def launch(self, d_file: torch.Tensor, length: int, b: DecodeBuffers, stream=None) -> None:
-        """Enqueue the whole decode on `stream` (default: torch's current stream); no host sync."""
+    def launch(self, d_file: torch.Tensor, length: int, b: DecodeBuffers, stream=None, comp=None) -> None:
+        """Enqueue the whole decode on `stream` (default: torch's current stream); no host sync.
+        `comp`: the file header's compression type when the caller knows it (only that codec's
+        kernels are launched: rio_device_decode_ex)."""
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        rc = L.lib().rio_device_decode(
-            self.ctx, d_file.data_ptr(), length, b.out.data_ptr(), b.out.numel(), b.out_off.data_ptr(),
-            b.rec_off.data_ptr(), b.flags.data_ptr(), b.out_off.numel() - 1, b.info.data_ptr(),
-            ctypes.c_void_p(s.cuda_stream))
+        rc = L.lib().rio_device_decode_ex(
+            self.ctx, d_file.data_ptr(), length, L.RIO_COMP_UNKNOWN if comp is None else comp, b.out.data_ptr(),
+            b.out.numel(), b.out_off.data_ptr(), b.rec_off.data_ptr(), b.flags.data_ptr(), b.out_off.numel() - 1,
+            b.info.data_ptr(), ctypes.c_void_p(s.cuda_stream))
         if rc != L.RIO_OK:
             raise RuntimeError(f"rio_device_decode: {L.strerror(rc)}")
 
@@ -100,16 +102,16 @@ class DeviceDecoder:
         torch.cuda.synchronize(self.device)
         return [(b, self.info(b)) for b in bufs]
 
-    def decode(self, d_file: torch.Tensor, length: int, stream=None):
+    def decode(self, d_file: torch.Tensor, length: int, stream=None, comp=None):
         """Size the outputs with a capacity-0 probe, then decode. Returns (buffers, info)."""
         probe = self.alloc(0, 0)
-        self.launch(d_file, length, probe, stream)
+        self.launch(d_file, length, probe, stream, comp)
         torch.cuda.synchronize(self.device)
         pi = self.info(probe)
         if pi["status"] != L.RIO_ERR_CAPACITY:
             return probe, pi
         b = self.alloc(pi["n_records"], pi["total_out_bytes"])
-        self.launch(d_file, length, b, stream)
+        self.launch(d_file, length, b, stream, comp)
         torch.cuda.synchronize(self.device)
         return b, self.info(b)
 

@@ -162,6 +162,14 @@ int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, 
 int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                       uint64_t rec_cap, rio_file_info* d_info, void* stream);
+/* Same as rio_device_decode for a file whose 8-byte header the caller has already read (an mmap'd or
+ * uploaded file): `compression` is its compression type, so only that codec's decode kernels are
+ * launched (a Snappy file: 6 launches). RIO_COMP_UNKNOWN launches every decoder, as
+ * rio_device_decode does. A file whose header contradicts the hint comes back as RIO_ERR_ARG. */
+#define RIO_COMP_UNKNOWN 0xFFFFFFFFu
+int rio_device_decode_ex(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint32_t compression, uint8_t* d_out,
+                         uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags, uint64_t rec_cap,
+                         rio_file_info* d_info, void* stream);
 /* Batch form: n_files device-resident files, file k = d_files[k] (lens[k] bytes, 16-byte aligned,
  * RIO_DEVICE_PAD readable bytes past it) decoded into its own outputs (d_out[k] ... d_info[k], as for
  * rio_device_decode). The arrays of pointers are host arrays; everything runs on `stream` without

@@ -213,3 +213,25 @@ def test_full_size_c3_10m_64b_records_exact():
     assert np.all(np.diff(g["rec_off"]) > 0) and np.all(np.diff(g["out_off"]) == 64)
     o = orc.file_reader_decode_arrays(img)
     assert_same_as_oracle(g, o, "C3-10M")
+
+
+@pytest.mark.parametrize("name", ["mixed_c0", "mixed_c2", "nil_snappy", "mixed_c2_zero_tail", "v3_mixed_snappy"])
+def test_compression_hint_launches_only_that_codec(name):
+    """rio_device_decode_ex with the header's compression type decodes exactly as the unhinted call;
+    a hint the header contradicts comes back RIO_ERR_ARG with nothing decoded."""
+    from gpu_util import decoder
+    from recordio import _lib as L
+    from recordio.device import to_device_file
+
+    img = dict(CASES)[name]
+    comp = img[4]
+    d, n = to_device_file(img)
+    b, info = decoder().decode(d, n, comp=comp)
+    o = orc.file_reader_decode_arrays(img)
+    k, nb = info["n_records"], info["total_out_bytes"]
+    g = dict(info, out=b.out[:nb].cpu().numpy(), out_off=b.out_off[:k + 1].cpu().numpy(),
+             rec_off=b.rec_off[:k].cpu().numpy(), flags=b.flags[:k].cpu().numpy())
+    assert_same_as_oracle(g, o, name)
+    wrong = 1 if comp != 1 else 2
+    _, bad = decoder().decode(d, n, comp=wrong)
+    assert bad["status"] == L.RIO_ERR_ARG and bad["n_records"] == 0
