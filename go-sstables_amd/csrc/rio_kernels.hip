@@ -1,19 +1,23 @@
 // rio_kernels.hip — CDNA4 (gfx950) kernels of the recordio v3/v4 decode path.
 //
-// Pipeline for one file already in HBM:
-//   k_header        file header (readFileHeaderFromBuffer, common_reader.go:22-44)
-//   k_walk          one thread per 4 KiB chunk: speculative entry (first CRC-validated header in
-//                   the chunk) then header-to-header hops (readRecordHeaderV4/V3,
-//                   common_reader.go:83-151; payload sizing common_reader.go:162-169; snappy
-//                   preamble = decoded size). Records go to per-chunk scratch slots.
+// Pipeline for one file already in HBM: six launches for a Snappy file when the
+// host passes the codec (rio_device_decode_ex), follow-up steps run by the last block to arrive.
+//   k_walk          one wave per 32 KiB chunk: speculative entries at every 91 8d 4c candidate,
+//                   framed in parallel (readRecordHeaderV4/V3, common_reader.go:83-151; payload
+//                   sizing common_reader.go:162-169; snappy preamble = decoded size), chain picked
+//                   by a lane vote; records to per-chunk scratch. Block 0 also reads the file
+//                   header (readFileHeaderFromBuffer, common_reader.go:22-44) and resets ScanState.
 //   k_scan_blocks   256-chunk blocks: inclusive scan of key-point chunk summaries (stitches each
-//   k_scan_top      chunk's speculative entry to its predecessor's exit; a mismatch => sequential
-//                   repair walk), record/byte prefix sums, terminal status (FileReader.ReadNext
-//                   loop, file_reader.go:61-131).
-//   k_place         scratch -> rec_off / out_off / flags at their global record index.
-//   k_zero          zero-tail check behind a magic mismatch (file_reader.go:76-91).
-//   k_decode_*      payload -> record bytes (copy, or golang/snappy v1.0.0 block decode).
-//   k_finalize      public rio_file_info.
+//                   chunk's speculative entry to its predecessor's exit; a mismatch => sequential
+//                   repair walk); the last block runs the top level: record/byte prefix sums,
+//                   terminal status (FileReader.ReadNext loop, file_reader.go:61-131).
+//   k_place         prologue: arena capacity, zero-tail check behind a magic mismatch
+//                   (file_reader.go:76-91); scratch -> rec_off / out_off / flags at their global index.
+//   k_copy_records  uncompressed payloads and single-literal Snappy records (16-lane copies).
+//   k_snappy_pipe   golang/snappy v1.0.0 block decode (rio_snappy.hip); k_gzip_* (rio_gzip.hip).
+//   k_finish        re-check of records handed over by decoder lanes; last block: rio_file_info.
+// Host-API phase A (rio_frame) adds k_zero + k_finalize after the scan. Seek map (k_count91 ..
+// k_seek_jump) and single-record k_read_at / k_seek_next serve the ReadAtI handle.
 // Byte/integer work only: no MFMA. All offsets 64-bit.
 #include <hip/hip_runtime.h>
 

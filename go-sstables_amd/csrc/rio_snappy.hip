@@ -23,10 +23,10 @@
 //   * Input: aligned 16-byte chunks loaded kD iterations ahead land in a 64-byte LDS ring.
 //   * LDS image per wave is chunk-interleaved ([chunk][lane][16 B]): every 16-byte access by a
 //     wave touches each bank once, whatever positions the lanes are at.
-// k_snappy_global: records whose compressed stream exceeds 32-bit positions (never produced by a
-// real encoder) decode with byte loops straight to HBM.
+// Wave-per-record decoder (coop_*, k_snappy_coop_batch): files or arenas past 32-bit positions and
+// streams >= 4 GiB; 64-bit addressing, one 64-byte output window per round with lane = byte.
 // Files whose every record is a single literal (k_place sets ScanState::any_mixed otherwise) are
-// copied by k_snappy_literal (rio_kernels.hip) and both kernels here exit at once.
+// copied by k_copy_records (rio_kernels.hip) and the kernels here exit at once.
 #include <hip/hip_runtime.h>
 
 #include "rio_device.h"
@@ -137,7 +137,7 @@ __device__ __forceinline__ Slot empty_slot() {
 }
 }  // namespace
 
-// Files the 32-bit lane-stream positions cannot cover take k_snappy_global.
+// Files the 32-bit lane-stream positions cannot cover take the wave-per-record decoder.
 __device__ __forceinline__ bool snappy_wide(const FrameParams& P, const ScanState* st) {
     return st->huge_streams || P.len >= 0xFFFFFF00ull || st->total_bytes >= 0xFFFFFF00ull;
 }

@@ -344,9 +344,9 @@ int rio_device_read_at(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint64
 
 /* ------------------------------------------------------------------------------------------ */
 /* Reader handles mirroring recordio.ReaderI / recordio.ReadAtI on top of the device path.     */
-/* Returned data pointers stay valid until the next call on the same reader (ReadNextAt,       */
-/* SeekNext) or until Close (ReadNext; windowed file readers: until the next ReadNext); the Go   */
-/* adapter slices/copies them into Go memory.                                                   */
+/* Returned data pointers: ReadNext until Close (windowed file readers: until the next        */
+/* ReadNext); ReadNextAt / SeekNext as documented at their declarations. The Go adapter        */
+/* slices/copies them into Go memory.                                                           */
 /* ------------------------------------------------------------------------------------------ */
 typedef struct rio_reader rio_reader;
 
@@ -363,7 +363,12 @@ void rio_reader_last_detail(rio_reader* r, uint64_t* detail0, uint64_t* detail1,
  * for gzip's empty payload) and the next call returns the record after it; skip_next passes over it. */
 int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil);
 int rio_reader_skip_next(rio_reader* r);
-/* ReadAtI (thread-safe in the reference; here serialised per handle) */
+/* ReadAtI (recordio.go:91-105), thread-safe: any number of threads may call these on one handle.
+ * The first call decodes the whole file once; after that ReadNextAt at a record start, and SeekNext
+ * (seek_len >= 3) whose scan lands on a decoded record, are a binary search on the calling thread
+ * (no kernel, no lock) and *data points into the reader's decoded arena, valid until rio_reader_free.
+ * Other offsets run the single-record kernels on a per-call stream; *data is then valid until the
+ * calling thread's next ReadNextAt / SeekNext. Detail values are per thread (rio_reader_last_detail). */
 int rio_reader_read_next_at(rio_reader* r, uint64_t offset, const uint8_t** data, uint64_t* len,
                             int* is_nil);
 int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, const uint8_t** data,
