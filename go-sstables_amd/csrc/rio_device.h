@@ -78,6 +78,7 @@ struct ScanState {
                             // 0 => every record is copied by k_copy_records instead of k_snappy_pipe
     uint32_t scan_ticket;   // k_scan_blocks: the last block to finish runs the top-level scan
     uint32_t finish_ticket; // k_finish: the last block to finish publishes the result
+    uint32_t pipe_next;     // k_snappy_pipe: next record chunk handed to a wave that finished its own
 };
 
 // Result of the single-record (ReadNextAt) kernel.

@@ -367,6 +367,7 @@ __device__ void init_state(const FrameParams& P) {
     st->slow = 0;
     st->scan_ticket = 0;
     st->finish_ticket = 0;
+    st->pipe_next = 0;
     if (P.len < RIO_FILE_HEADER_BYTES) {
         st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;
         st->version = st->compression = 0;

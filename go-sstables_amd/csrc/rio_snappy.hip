@@ -38,10 +38,19 @@ namespace {
 constexpr uint32_t kOutCh = 16;                  // history ring: 16 chunks = 256 bytes per lane
 constexpr uint32_t kInCh = 4;                    // input ring: 4 chunks = 64 bytes per lane
 constexpr uint32_t kWaveLds = (kOutCh + kInCh) * 64 * 16;  // 20 KiB per wave
-constexpr uint32_t kFarOff = kOutCh * 16 - 48;   // copies reaching further back read HBM
+// emitter generation: 9 = every piece through one destination-aligned funnel (below), 8 = the
+// source funnel + placement shifts of round 1 (kept for A/B builds: make variant VDEFS=-DRIO_PIPE=8)
+#ifndef RIO_PIPE
+#define RIO_PIPE 9
+#endif
 constexpr uint32_t kD = 4;                       // pipeline depth in iterations
+// copies reaching further back than kFarOff read the output arena (flushed: see snappy_lane)
+constexpr uint32_t kFarOff = RIO_PIPE >= 9 ? 16 * (kD - 1) + 16 + 128 : kOutCh * 16 - 48;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
 static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128, "far history must be flushed before the parser reads it");
+// v9: a ring copy's source window starts >= 16 * (chunk(d) - kFarOff / 16), and ring chunk chunk(d) + 2
+// (= chunk(d) - 14 mod 16) serves as the staging chunk of literal / far bytes: it must be dead
+static_assert(RIO_PIPE < 9 || (kOutCh == 16 && kFarOff <= 16 * 13), "staging chunk must hold no live history");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
 
 // bytes [r, r + 16) of the 32-byte little-endian concatenation (a, b), r in [0, 16): dword
@@ -74,6 +83,35 @@ __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
     return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
+// bytes [f, f + 16) and [f + 16, f + 32) of the 48-byte little-endian concatenation (A, B, C),
+// f in [0, 16): one dword-select network shared by both halves, then v_alignbyte_b32
+__device__ __forceinline__ void funnel32(uint4 A, uint4 B, uint4 C, uint32_t f, uint4& L, uint4& H) {
+    const uint32_t sh = f & 3u;
+    const bool h1 = (f & 4u) != 0, h2 = (f & 8u) != 0;
+    // written out (no arrays): an indexed form is lowered to a private-memory table lookup
+    uint32_t p0 = h1 ? A.y : A.x, p1 = h1 ? A.z : A.y, p2 = h1 ? A.w : A.z, p3 = h1 ? B.x : A.w,
+             p4 = h1 ? B.y : B.x, p5 = h1 ? B.z : B.y, p6 = h1 ? B.w : B.z, p7 = h1 ? C.x : B.w,
+             p8 = h1 ? C.y : C.x, p9 = h1 ? C.z : C.y, p10 = h1 ? C.w : C.z;
+    pin_v(p0), pin_v(p1), pin_v(p2), pin_v(p3), pin_v(p4), pin_v(p5), pin_v(p6), pin_v(p7), pin_v(p8), pin_v(p9),
+        pin_v(p10);
+    const uint32_t e0 = h2 ? p2 : p0, e1 = h2 ? p3 : p1, e2 = h2 ? p4 : p2, e3 = h2 ? p5 : p3, e4 = h2 ? p6 : p4,
+                   e5 = h2 ? p7 : p5, e6 = h2 ? p8 : p6, e7 = h2 ? p9 : p7, e8 = h2 ? p10 : p8;
+    L = make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
+                   __builtin_amdgcn_alignbyte(e3, e2, sh), __builtin_amdgcn_alignbyte(e4, e3, sh));
+    H = make_uint4(__builtin_amdgcn_alignbyte(e5, e4, sh), __builtin_amdgcn_alignbyte(e6, e5, sh),
+                   __builtin_amdgcn_alignbyte(e7, e6, sh), __builtin_amdgcn_alignbyte(e8, e7, sh));
+}
+
+// bytes [0, r) from `st`, [r, 16) from `v` (r in [0, 16)): two 64-bit masks, then bit selects
+__device__ __forceinline__ uint4 merge_at(uint4 st, uint4 v, uint32_t r) {
+    const uint32_t s8 = 8u * r;
+    const uint64_t all = ~0ull;
+    const uint64_t mlo = s8 >= 64 ? 0ull : (all << s8), mhi = s8 >= 64 ? (all << ((s8 - 64) & 63)) : all;
+    const uint32_t m0 = (uint32_t)mlo, m1 = (uint32_t)(mlo >> 32), m2 = (uint32_t)mhi, m3 = (uint32_t)(mhi >> 32);
+    return make_uint4((v.x & m0) | (st.x & ~m0), (v.y & m1) | (st.y & ~m1), (v.z & m2) | (st.z & ~m2),
+                      (v.w & m3) | (st.w & ~m3));
+}
+
 // place v at byte offset r of a 32-byte window: lo = v << 8r (bytes of the chunk holding the
 // position), hi = v >> 8(16 - r) (bytes spilling into the next chunk)
 __device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& hi) {
@@ -88,7 +126,8 @@ __device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& h
 #define RIO_NT 0
 #endif
 // timing-only experiment knobs (wrong output): 1 = no out16 funnel, 2 = no place16, 4 = no in16 funnel,
-// 8 = no flush bpermutes of the owner base, 16 = far-history loads to the sink (traffic attribution)
+// 8 = no flush bpermutes of the owner base, 16 = far-history loads to the sink (traffic attribution),
+// 32 = flush stores to the sink
 #ifndef RIO_EXP
 #define RIO_EXP 0
 #endif
@@ -97,11 +136,14 @@ __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
 }
 __device__ __forceinline__ uint4 ld_far(const uint8_t* p) { return (RIO_NT & 2) ? ldu16_nt(p) : ldu16(p); }
 
-// per-lane view of the wave's chunk-interleaved LDS image
+// per-lane view of the wave's chunk-interleaved LDS images. History and input ring are separate
+// __shared__ objects, so the compiler knows they never alias and may issue the parser's input-ring
+// reads while the emitter's history writes are still queued.
 struct LaneLds {
-    uint8_t* p;  // wave image + lane * 16
-    __device__ uint4* out(uint32_t pos) const { return reinterpret_cast<uint4*>(p + ((pos >> 4) & (kOutCh - 1)) * 1024); }
-    __device__ uint4* in(uint32_t c) const { return reinterpret_cast<uint4*>(p + (kOutCh + (c & (kInCh - 1))) * 1024); }
+    uint8_t* h;  // wave history image + lane * 16
+    uint8_t* i;  // wave input-ring image + lane * 16
+    __device__ uint4* out(uint32_t pos) const { return reinterpret_cast<uint4*>(h + ((pos >> 4) & (kOutCh - 1)) * 1024); }
+    __device__ uint4* in(uint32_t c) const { return reinterpret_cast<uint4*>(i + (c & (kInCh - 1)) * 1024); }
     // 16 bytes of history at output position q
     __device__ uint4 out16(uint32_t q) const {
         return (RIO_EXP & 1) ? *out(q) : funnel16(*out(q), *out(q + 16), q & 15u);
@@ -152,9 +194,10 @@ __device__ __forceinline__ bool snappy_wide(const FrameParams& P, const ScanStat
 // lanes writes one owner's next complete 64-byte block (16 B per lane, 64 contiguous bytes of one
 // stream): a wave store touches 16 streams instead of 64, which the L2 absorbs ~3x faster.
 // Returns false with *bad_rec = the failing record if a record does not decode.
-__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint32_t lane,
+__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint8_t* wi,
+                                            uint32_t lane,
                             uint8_t* sink, uint64_t* bad_rec) {
-    const LaneLds L{wl + lane * 16};
+    const LaneLds L{wl + lane * 16, wi + lane * 16};
     const bool live = r0 < r1;
     uint8_t* const out = P.out;
     const uint4 d0 = live ? P.rec_desc[r0] : zero4();
@@ -195,19 +238,42 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     }
 
     Slot S0 = empty_slot(), S1 = empty_slot(), S2 = empty_slot(), S3 = empty_slot();
-    uint32_t drain = 0;
+    uint32_t drain = 0, qsrc = 0;
+    // the parser's input window [s, s + 16), read one step ahead (end of the previous step) so that
+    // its LDS latency hides behind the emit and flush
+    // (the two raw chunks travel; the funnel runs where the parser needs the bytes)
+    uint4 Wa = *L.in(s >> 4), Wb = *L.in((s >> 4) + 1);
 
-    auto step = [&](Slot& S, const uint32_t j) __attribute__((always_inline)) {
+    auto step = [&](Slot& S, const Slot& N, const uint32_t j) __attribute__((always_inline)) {
         drain += pdone ? 1u : 0u;
-        // 1. land the input chunk loaded kD iterations ago
-        const bool landed = S.in_c != kNoChunk;
-        if (landed) *L.in(S.in_c) = S.in;
-        whi = landed ? S.in_c + 1 : whi;
-        // ... and the next record's descriptor, if this slot fetched it
+        // 1. the next record's descriptor, if this slot fetched it
         nd = sel4(S.desc != 0, S.aux, nd);
         nds = S.desc ? 2u : nds;
+        const uint32_t pos = s;
 
         // 2. emit the piece parsed kD iterations ago (a bubble appends nothing)
+#if RIO_PIPE >= 9
+        // Destination-aligned: a literal's or far copy's 16 bytes are first stored to the dead ring
+        // chunk chunk(d) + 2, so every piece is "bytes [w, w + 32) of the ring, w = source - r" with
+        // r = d & 15: one funnel over three ring chunks yields the destination chunk and its
+        // successor already aligned; bytes below r come from the staged head, bytes past the piece
+        // are garbage that later pieces overwrite (never flushed: flushes take complete blocks < d).
+        {
+            const uint32_t r = d & 15u, cd = d >> 4;
+            const uint32_t w = (S.kind == 1 ? S.q : ((cd + 2u) << 4) + S.q) - r;
+            uint4 lo, hi;
+            funnel32(*L.out(w), *L.out(w + 16u), *L.out(w + 32u), w & 15u, lo, hi);
+            lo = merge_at(stage, lo, r);
+            *L.out(d) = lo;
+            *L.out(d + 16) = hi;
+            stage = sel4(r + S.n >= 16, hi, lo);
+            d += S.n;
+            // stage the NEXT slot's literal / far bytes now: an LDS read right after a write to the
+            // same address waits for the write (~2000 cycles on gfx950, scripts/lds_probe.hip RAW);
+            // d does not move before that slot's emit, so its staging chunk is already known
+            *L.out(((d >> 4) + 2u) << 4) = sel4(N.kind == 0, N.lit, N.aux);
+        }
+#else
         {
             const uint4 h = L.out16(S.q);
             const uint4 v = keep_bytes(sel4(S.kind == 0, S.lit, sel4(S.kind == 2, S.aux, h)), S.n);
@@ -220,6 +286,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             stage = sel4(r + S.n >= 16, hi, lo);
             d += S.n;
         }
+#endif
 
         // 3. cooperative flush: lane writes 16 bytes of owner o's next 64-byte block if complete
         {
@@ -228,14 +295,13 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
             const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
             const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
-            st_out((ofb >> 31) ? obase[j & 3u] + pos : sink, fv);
+            st_out(((ofb >> 31) && !(RIO_EXP & 32)) ? obase[j & 3u] + pos : sink, fv);
             fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
         }
 
         // 4. parse the next piece into this slot (selects only: lanes diverge in data, not flow)
         {
-            const uint32_t pos = s;
-            const uint4 W = L.in16(pos);  // input bytes [s, s + 16)
+            const uint4 W = (RIO_EXP & 4) ? Wa : funnel16(Wa, Wb, pos & 15u);  // input bytes [s, s + 16)
             const bool avail = min((pos + 15) >> 4, lastc) < whi;
             // element header at s (golang/snappy decode_other.go tag forms): every form is computed
             // and combined with selects, so divergent tags cost no exec-mask branches
@@ -278,9 +344,17 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
             const uint32_t n = go ? min(rem1, lit1 ? 16u - sh : min(16u, eff1)) : 0u;
             S.n = n;
-            S.q = pd - eff1;
             S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
+            qsrc = pd - eff1;
+#if RIO_PIPE >= 9
+            // the literal starts sh bytes into W; the emitter's funnel absorbs that shift (S.q = sh),
+            // a far copy's bytes sit at the start of the staging chunk (S.q = 0)
+            S.q = S.kind == 1 ? qsrc : (S.kind == 0 ? sh : 0u);
+            S.lit = W;
+#else
+            S.q = qsrc;
             S.lit = shift_small(W, sh);
+#endif
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
@@ -292,30 +366,34 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             s = badn ? s_end : s;
             // record boundary: stream consumed -> the record must be complete; switch to the next
             // (its descriptor landed) or finish the range
+            // (a real branch: a lane ends a record every ~130 steps, so most steps of a wave skip it;
+            // it holds no memory operation, so the wave's memory schedule stays uniform)
             const bool at_end = !pdone && rem == 0 && s == s_end;
-            const bool bad_len = at_end && pd != rd_end;  // snappy: d != len(dst) => ErrCorrupt
-            const bool more = k + 1 < r1;
-            const bool sw = at_end && !bad_len && more && nds == 2;
-            bad = bad || bad_len;
-            const bool fill = bad_len;  // (rd_end > pd: output room is checked per element)
-            rem = fill ? rd_end - pd : rem;
-            eff = fill ? 16u : eff;
-            islit = islit && !fill;
-            pdone = pdone || (at_end && !bad_len && !more);
-            k += sw ? 1u : 0u;
-            const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
-            s = sw ? (uint32_t)(nstart - base) : s;
-            s_end = sw ? s + nd.z : s_end;
-            rd_start = sw ? pd : rd_start;
-            rd_end = sw ? pd + nd.w : rd_end;
-            nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
+            if (at_end) {
+                const bool bad_len = pd != rd_end;  // snappy: d != len(dst) => ErrCorrupt
+                const bool more = k + 1 < r1;
+                const bool sw = !bad_len && more && nds == 2;
+                bad = bad || bad_len;
+                // fill (rd_end > pd: output room is checked per element)
+                rem = bad_len ? rd_end - pd : rem;
+                eff = bad_len ? 16u : eff;
+                islit = islit && !bad_len;
+                pdone = pdone || (!bad_len && !more);
+                k += sw ? 1u : 0u;
+                const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
+                s = sw ? (uint32_t)(nstart - base) : s;
+                s_end = sw ? s + nd.z : s_end;
+                rd_start = sw ? pd : rd_start;
+                rd_end = sw ? pd + nd.w : rd_end;
+                nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
+            }
         }
         // far history (flushed: see header), or the next record's descriptor, or a placeholder load
         {
             const bool want_desc = S.kind != 2 && nds == 0;
             S.desc = want_desc ? 1u : 0u;
             nds = want_desc ? 1u : nds;
-            const uint8_t* ap = S.kind == 2 ? ((RIO_EXP & 16) ? sink : gout + S.q)
+            const uint8_t* ap = S.kind == 2 ? ((RIO_EXP & 16) ? sink : gout + qsrc)
                                             : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
             S.aux = ld_far(ap);
         }
@@ -328,16 +406,26 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.in_c = take ? cn : kNoChunk;
             cn += take ? 1u : 0u;
         }
+
+        // 6. land the next slot's input chunk (loaded kD - 1 iterations ago), then read the next
+        // step's parser window
+        {
+            const bool landed = N.in_c != kNoChunk;
+            if (landed) *L.in(N.in_c) = N.in;
+            whi = landed ? N.in_c + 1 : whi;
+            Wa = *L.in(s >> 4);
+            Wb = *L.in((s >> 4) + 1);
+        }
     };
 
     // one exit per kD steps, taken by the whole wave: every path around the loop issues the same
     // memory operations, so the compiler's wait counts stay exact
     static_assert(kD == 4, "unrolled for four slots");
     do {
-        step(S0, 0);
-        step(S1, 1);
-        step(S2, 2);
-        step(S3, 3);
+        step(S0, S1, 0);
+        step(S1, S2, 1);
+        step(S2, S3, 2);
+        step(S3, S0, 3);
     } while (__any(drain < kD));
     // the stream's tail (< 128 bytes), lane by lane; written even after a failure: the bytes of
     // the records before the failing one must be complete
@@ -393,6 +481,8 @@ struct CoopLds {
     uint8_t slot[64];                     // element starts in the current output window
     uint8_t ring[kCoopRing];              // decoded history of the current record
 };
+// k_snappy_pipe runs the wave decoder in the wave's history image
+static_assert(sizeof(CoopLds) <= kOutCh * 1024, "wave decoder LDS must fit a history image");
 
 __device__ __forceinline__ bool coop_active(const FrameParams& P, const ScanState* st) {
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->any_mixed)
@@ -711,36 +801,43 @@ __global__ void __launch_bounds__(64 * kCoopWaves) k_snappy_coop_batch(FrameBatc
 }
 
 __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ __attribute__((aligned(16))) uint8_t hist[kSnappyBlock / 64][kOutCh * 1024];
+    __shared__ __attribute__((aligned(16))) uint8_t inring[kSnappyBlock / 64][kInCh * 1024];
     ScanState* st = P.state;
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
     if (!st->any_mixed) return;  // every record is one literal: k_copy_records copies them
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     if (coop_active(P, st)) {  // large records / past 32-bit positions: the wave-per-record decoder
-        coop_file(P, reinterpret_cast<CoopLds*>(lds)[wave], lane, (uint64_t)blockIdx.x * (kSnappyBlock / 64) + wave,
+        coop_file(P, *reinterpret_cast<CoopLds*>(hist[wave]), lane, (uint64_t)blockIdx.x * (kSnappyBlock / 64) + wave,
                   (uint64_t)gridDim.x * (kSnappyBlock / 64));
         return;
     }
     const uint64_t n = st->n_records;
-    // lane number: waves are numbered across workgroups first, so that a file with few records
-    // (fewer than lanes) spreads its active waves over every CU
-    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t t = (((uint64_t)wave * gridDim.x + blockIdx.x) << 6) | lane;
-    // contiguous record ranges of ceil(n / T) records: lanes of a wave cover consecutive ranges,
-    // and a file with fewer records than lanes fills whole waves (the rest exit at once)
-    const uint64_t rpl = (n + T - 1) / T;
-    const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
-    if ((t & ~63ull) * rpl >= n) return;  // the whole wave is idle (wave-uniform exit)
-    uint8_t* sink = P.sink + (t >> 6) * 64;  // the wave's placeholder line
-    uint64_t bad_rec = 0;
-    if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
-        // a record of this lane did not decode: k_snappy_verify re-decodes the lane's records one
-        // thread each and flags the failing ones
-        const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
-        if (at < kFailLanes) {
-            P.fail_lanes[2 * at] = r0;
-            P.fail_lanes[2 * at + 1] = r1;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t g = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
+    uint8_t* sink = P.sink + g * 64;                               // the wave's placeholder line
+    // Records go to waves in chunks of 64 lanes x rpc consecutive records (each lane one contiguous
+    // range: one stream, no drain between its records). Chunk g is wave g's; a wave that finishes
+    // takes the next unclaimed chunk, so waves whose records decode slower, or that start later, do
+    // not hold the kernel's tail. About four chunks per wave.
+    const uint64_t rpc = n >= 4 * 64 * waves ? n / (4 * 64 * waves) : 1;
+    const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
+    uint64_t chunk = g;
+    while (chunk < nchunks) {
+        const uint64_t r0 = min(chunk * per + lane * rpc, n), r1 = min(r0 + rpc, n);
+        uint64_t bad_rec = 0;
+        if (!snappy_lane(P, r0, r1, hist[wave], inring[wave], lane, sink, &bad_rec)) {
+            // a record of this lane did not decode: k_finish re-decodes the lane's records one
+            // thread each and flags the failing ones
+            const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
+            if (at < kFailLanes) {
+                P.fail_lanes[2 * at] = r0;
+                P.fail_lanes[2 * at + 1] = r1;
+            }
         }
+        uint32_t next = 0;
+        if (lane == 0) next = atomicAdd(&st->pipe_next, 1u);
+        chunk = waves + __shfl(next, 0);
     }
 }
 
@@ -755,7 +852,8 @@ __device__ __forceinline__ bool pipe_active(const FrameParams& P) {
 }
 
 __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ __attribute__((aligned(16))) uint8_t hist[kSnappyBlock / 64][kOutCh * 1024];
+    __shared__ __attribute__((aligned(16))) uint8_t inring[kSnappyBlock / 64][kInCh * 1024];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
@@ -784,7 +882,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
             const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
             uint8_t* sink = P.sink + wg * 64;
             uint64_t bad_rec = 0;
-            if (!snappy_lane(P, r0, r1, lds + wave * kWaveLds, lane, sink, &bad_rec)) {
+            if (!snappy_lane(P, r0, r1, hist[wave], inring[wave], lane, sink, &bad_rec)) {
                 const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
                 if (at < kFailLanes) {
                     P.fail_lanes[2 * at] = r0;
@@ -798,7 +896,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
 }
 
 hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
-    hipLaunchKernelGGL(k_snappy_pipe_batch, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, B);
+    hipLaunchKernelGGL(k_snappy_pipe_batch, dim3(kSnappyGrid), dim3(kSnappyBlock), 0, s, B);
     hipLaunchKernelGGL(k_snappy_coop_batch, dim3(kCoopGrid), dim3(64 * kCoopWaves), 0, s, B);
     return hipGetLastError();
 }
@@ -807,7 +905,7 @@ hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
 hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main) {
     // 4 waves x 20 KiB = 80 KiB per workgroup: 2 workgroups (8 waves) per CU
     if (main)
-        hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), (kSnappyBlock / 64) * kWaveLds, s, P);
+        hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), 0, s, P);
     return hipGetLastError();
 }
 

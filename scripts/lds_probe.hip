@@ -98,6 +98,9 @@ __global__ void k_probe(int mode, unsigned long long* cycles, unsigned* bad) {
 // waiting after each (counted in bulk), to price the LDS array / store path rather than latency.
 // mode 0: aligned read, 1: unaligned read, 2: aligned write, 3: unaligned write,
 //      4: read 4-aligned, 5: read 8-aligned, 6: write 4-aligned, 7: write 8-aligned (all b128)
+//      8: b32 read byte-unaligned, 9: b32 write byte-unaligned, 10: b32 read aligned, 11: b32 write aligned,
+//      12: u8 read, 13: b8 write, 14: b64 read byte-unaligned, 15: b64 write byte-unaligned,
+//      16: u16 read byte-unaligned, 17: b16 write byte-unaligned
 __global__ void k_tput(int mode, unsigned long long* cycles, unsigned* sink) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t t = threadIdx.x;
@@ -113,7 +116,33 @@ __global__ void k_tput(int mode, unsigned long long* cycles, unsigned* sink) {
         if (mode == 4 || mode == 6) off &= ~3u;
         if (mode == 5 || mode == 7) off &= ~7u;
         const uint32_t addr = (base + off) % (kLds * 4 - 32);
-        if (mode <= 1 || mode == 4 || mode == 5) {
+        if (mode == 10 || mode == 11) off &= ~3u;
+        const uint32_t a2 = (base + off) % (kLds * 4 - 32);
+        if (mode >= 8) {
+            uint32_t v = acc.x + x;
+            if (mode == 8 || mode == 10) {
+                asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a2) : "memory");
+            } else if (mode == 9 || mode == 11) {
+                asm volatile("ds_write_b32 %0, %1" ::"v"(a2), "v"(v) : "memory");
+            } else if (mode == 12) {
+                asm volatile("ds_read_u8 %0, %1" : "=v"(v) : "v"(a2) : "memory");
+            } else if (mode == 13) {
+                asm volatile("ds_write_b8 %0, %1" ::"v"(a2), "v"(v) : "memory");
+            } else if (mode == 14) {
+                uint64_t w;
+                asm volatile("ds_read_b64 %0, %1" : "=v"(w) : "v"(a2) : "memory");
+                v = (uint32_t)w ^ (uint32_t)(w >> 32);
+            } else if (mode == 15) {
+                uint64_t w = ((uint64_t)v << 32) | x;
+                asm volatile("ds_write_b64 %0, %1" ::"v"(a2), "v"(w) : "memory");
+            } else if (mode == 16) {
+                asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(a2) : "memory");
+            } else {
+                asm volatile("ds_write_b16 %0, %1" ::"v"(a2), "v"(v) : "memory");
+            }
+            if ((it & 15) == 15) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            acc.x += v;
+        } else if (mode <= 1 || mode == 4 || mode == 5) {
             typedef v4u __attribute__((aligned(1))) v4b;
             acc += *reinterpret_cast<const v4b*>(lds + addr);
         } else {
@@ -150,8 +179,11 @@ int main() {
     }
     const char* tnames[] = {"tput read_b128 aligned", "tput read_b128 unaligned", "tput write_b128 aligned",
                             "tput write_b128 unaligned", "tput read_b128 4-aligned", "tput read_b128 8-aligned",
-                            "tput write_b128 4-aligned", "tput write_b128 8-aligned"};
-    for (int mode = 0; mode < 8; mode++) {
+                            "tput write_b128 4-aligned", "tput write_b128 8-aligned",
+                            "tput read_b32 unaligned", "tput write_b32 unaligned", "tput read_b32 aligned",
+                            "tput write_b32 aligned", "tput read_u8", "tput write_b8", "tput read_b64 unaligned",
+                            "tput write_b64 unaligned", "tput read_u16 unaligned", "tput write_b16 unaligned"};
+    for (int mode = 0; mode < 18; mode++) {
         (void)hipMemset(cyc, 0, 8);
         // 1024 threads = 16 waves on one CU (4 per SIMD), 128 KiB LDS
         hipLaunchKernelGGL(k_tput, dim3(1), dim3(1024), kLds * 4, 0, mode, cyc, bad);
