@@ -239,6 +239,9 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 
     Slot S0 = empty_slot(), S1 = empty_slot(), S2 = empty_slot(), S3 = empty_slot();
     uint32_t drain = 0, qsrc = 0;
+    // v9: the next emit's source window (three ring chunks) and its funnel shift
+    uint4 wA = zero4(), wB = zero4(), wC = zero4();
+    uint32_t wF = 0;
     // the parser's input window [s, s + 16), read one step ahead (end of the previous step) so that
     // its LDS latency hides behind the emit and flush
     // (the two raw chunks travel; the funnel runs where the parser needs the bytes)
@@ -259,19 +262,24 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         // successor already aligned; bytes below r come from the staged head, bytes past the piece
         // are garbage that later pieces overwrite (never flushed: flushes take complete blocks < d).
         {
-            const uint32_t r = d & 15u, cd = d >> 4;
-            const uint32_t w = (S.kind == 1 ? S.q : ((cd + 2u) << 4) + S.q) - r;
+            const uint32_t r = d & 15u;
             uint4 lo, hi;
-            funnel32(*L.out(w), *L.out(w + 16u), *L.out(w + 32u), w & 15u, lo, hi);
+            funnel32(wA, wB, wC, wF, lo, hi);  // this piece's window, read during the previous step
             lo = merge_at(stage, lo, r);
             *L.out(d) = lo;
             *L.out(d + 16) = hi;
             stage = sel4(r + S.n >= 16, hi, lo);
             d += S.n;
-            // stage the NEXT slot's literal / far bytes now: an LDS read right after a write to the
-            // same address waits for the write (~2000 cycles on gfx950, scripts/lds_probe.hip RAW);
-            // d does not move before that slot's emit, so its staging chunk is already known
-            *L.out(((d >> 4) + 2u) << 4) = sel4(N.kind == 0, N.lit, N.aux);
+            // The NEXT slot: d does not move before its emit, so its staging chunk and source window
+            // are known now. Stage its literal / far bytes, then read its window: the reads' latency
+            // hides behind this step's flush and parse instead of sitting on the emit chain.
+            const uint32_t r2 = d & 15u, cs = (d >> 4) + 2u;
+            *L.out(cs << 4) = sel4(N.kind == 0, N.lit, N.aux);
+            const uint32_t w = (N.kind == 1 ? N.q : (cs << 4) + N.q) - r2;
+            wA = *L.out(w);
+            wB = *L.out(w + 16u);
+            wC = *L.out(w + 32u);
+            wF = w & 15u;
         }
 #else
         {
