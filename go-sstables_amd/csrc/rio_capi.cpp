@@ -205,6 +205,7 @@ struct rio_ctx {
     // last host-API framing (rio_frame -> rio_decode)
     FrameParams last{};
     bool framed = false;
+    bool predecoded = false;  // gzip: rio_frame decoded the file already (ctx arenas hold the result)
     uint64_t file_len = 0;
     rio_file_info frame_info{};
 };
@@ -536,6 +537,48 @@ static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const u
     HIP_TRY(launch_phase_a(P, ctx->stream, ctx->next_events()));
     HIP_TRY(hipMemcpyAsync(&ctx->frame_info, P.info, sizeof(rio_file_info), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->predecoded = false;
+    const rio_file_info& fi = ctx->frame_info;
+    if (fi.compression == RIO_COMP_GZIP && fi.status != RIO_ERR_VERSION && fi.status != RIO_ERR_COMPRESSION_TYPE &&
+        fi.status != RIO_ERR_UNSUPPORTED && fi.status != RIO_ERR_SHORT_FILE_HEADER) {
+        // gzip: decode now. The framing sizes a record from its last member's ISIZE; a record of
+        // several members (Go's multistream reader) is larger, which only the decode finds out, and
+        // the caller allocates from the sizes returned here. A decode that needs more room than the
+        // framing's sizes reports RIO_ERR_CAPACITY with the sizes it needs: frame and decode again
+        // into arenas of that size (the whole pipeline: framing resets the device state).
+        uint64_t n = fi.n_records, nb = fi.total_out_bytes;
+        rio_file_info fin{};
+        for (int attempt = 0; attempt < 3; attempt++) {
+            HIP_TRY(ctx->out.ensure(nb + 16));
+            HIP_TRY(ctx->out_off.ensure((n + 1) * 8));
+            HIP_TRY(ctx->rec_off.ensure(n * 8 + 8));
+            HIP_TRY(ctx->flags.ensure(n + 8));
+            HIP_TRY(ctx->fa.rec_pay.ensure((n + 1) * 8));
+            HIP_TRY(ctx->fa.rec_desc.ensure((n + 1) * 16));
+            if (attempt) HIP_TRY(launch_phase_a(P, ctx->stream, nullptr));
+            FrameParams D = P;
+            D.zero_done = 1;  // phase A ran k_zero
+            D.comp_hint = RIO_COMP_GZIP;
+            D.out = ctx->out.as<uint8_t>();
+            D.out_cap = nb;
+            D.out_off = ctx->out_off.as<uint64_t>();
+            D.rec_off = ctx->rec_off.as<uint64_t>();
+            D.flags = ctx->flags.as<uint8_t>();
+            D.rec_cap = n;
+            D.rec_pay = ctx->fa.rec_pay.as<uint64_t>();
+            D.rec_desc = ctx->fa.rec_desc.as<uint4>();
+            HIP_TRY(launch_phase_b(D, ctx->stream, attempt ? nullptr : ctx->same_events()));
+            HIP_TRY(hipMemcpyAsync(&fin, D.info, sizeof fin, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            P = D;
+            if (fin.status != RIO_ERR_CAPACITY) break;
+            n = fin.n_records;
+            nb = fin.total_out_bytes;
+        }
+        if (fin.status == RIO_ERR_CAPACITY) return RIO_ERR_CAPACITY;
+        ctx->frame_info = fin;
+        ctx->predecoded = true;
+    }
     *info = ctx->frame_info;
     ctx->last = P;
     ctx->framed = true;
@@ -568,6 +611,18 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
     }
     const uint64_t n = fi.n_records, nb = fi.total_out_bytes;
     if (rec_cap < n || out_cap < nb || (n && (!out_off || !rec_off || !flags)) || (nb && !out)) return RIO_ERR_CAPACITY;
+    if (ctx->predecoded) {  // gzip: rio_frame decoded the file (its sizes are the decoded ones)
+        const FrameParams& P = ctx->last;
+        int rc;
+        if (nb && (rc = d2h_staged(ctx, out, P.out, nb))) return rc;
+        if (out_off && (rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(out_off), P.out_off, (n + 1) * 8))) return rc;
+        if (n) {
+            if ((rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(rec_off), P.rec_off, n * 8))) return rc;
+            if ((rc = d2h_staged(ctx, flags, P.flags, n))) return rc;
+        }
+        *info = fi;
+        return RIO_OK;
+    }
     HIP_TRY(ctx->out.ensure(nb + 16));
     HIP_TRY(ctx->out_off.ensure((n + 1) * 8));
     HIP_TRY(ctx->rec_off.ensure(n * 8 + 8));

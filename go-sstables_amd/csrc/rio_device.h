@@ -70,7 +70,7 @@ struct ScanState {
     uint64_t n_repairs;
     uint64_t first_bad;        // first record flagged RIO_FLAG_CORRUPT / RIO_FLAG_EOF (kNone = none)
     uint64_t n_bad;            // records so flagged
-    uint64_t unsupported_rec;  // first record the device path hands back (gzip: several members)
+    uint64_t unsupported_rec;  // first record the device path hands back (absurd gzip sizes)
     uint32_t n_fail_lanes;     // Snappy lane-decoder lanes listed in fail_lanes (> kFailLanes: all)
     uint32_t capacity_fail;
     uint32_t huge_streams;  // a record stream exceeds 32-bit positions: k_snappy_global runs
@@ -79,6 +79,9 @@ struct ScanState {
     uint32_t scan_ticket;   // k_scan_blocks: the last block to finish runs the top-level scan
     uint32_t finish_ticket; // k_finish: the last block to finish publishes the result
     uint32_t pipe_next;     // k_snappy_pipe: next record chunk handed to a wave that finished its own
+    uint32_t gz_resize;     // gzip: some record holds several members whose output the framing's
+                            // size (its last member's ISIZE) does not cover: k_gz_resize sizes them
+    uint32_t gz_redo;       // k_gz_resize ran: the scan, placement and gzip decoders run again
 };
 
 // Result of the single-record (ReadNextAt) kernel.
@@ -117,6 +120,7 @@ struct FrameParams {
     // launched and exits unless the file is its own); k_finish rejects a file that contradicts it
     uint32_t comp_hint;
     uint32_t zero_done;  // the zero-tail check already ran (host API phase A): k_place skips it
+    uint32_t redo;       // gzip redo round (k_gz_resize onwards): the kernel exits unless gz_resize
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)
     RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix

@@ -10,14 +10,18 @@
 //     HLIT <= 286, HDIST <= 30, every code complete except a single 1-bit code, empty distance
 //     codes allowed until used; symbols 286/287 and distance codes 30/31 are corrupt; a distance
 //     beyond the member's output so far is corrupt.
-// Every failure is the codec-error class (RIO_ERR_DECOMPRESS). Where this path cannot follow the
-// reader it hands the file back: a record holding more than one gzip member (Go's multistream
-// reader would go on reading), or a record announced as <= 1 / 2 KiB that decodes past its class's
-// window, ends the sequence with RIO_ERR_UNSUPPORTED and the adapter keeps the reference reader.
-// Bytes decoded past the announced size are never stored; the member then fails its ISIZE check
-// exactly like Go's (gzip.ErrChecksum).
+//   * Several members per record (Go's Reader is multistream): after a member's trailer the next
+//     header follows; nothing after a trailer ends the record; anything else that is not a whole
+//     header is an error. Each member's CRC-32 and ISIZE cover its own output, and DEFLATE distances
+//     never reach into an earlier member (the decompressor is reset per member).
+// Every failure is the codec-error class (RIO_ERR_DECOMPRESS).
 //
-// The framing sized each record from the last four payload bytes (ISIZE of its only member).
+// Sizes: the framing sized each record from its last four payload bytes (the last member's ISIZE),
+// which is the record's size when it holds one member. A record whose output does not fit that size
+// (several members, or a corrupt single member) is not stored: it is marked for k_gz_resize, which
+// counts the output of every member without storing it (and classifies the record as corrupt where
+// Go would fail). Then the scan, the placement and these decoders run once more with the counted
+// sizes (launch_gzip_redo); every kernel of that round exits at once when no record needed it.
 //
 // k_gzip_inflate<kWin>: one wavefront per record (grid-stride over records). Huffman decoding is
 // inherently serial, so the whole wave runs the decoder in lock step on wave-uniform state (bit
@@ -44,7 +48,10 @@ constexpr uint32_t kGzSmallWin = 2048;    // records with decoded size <= this: 
 constexpr uint32_t kGzLargeWin = 32768;   // DEFLATE window (maximum distance)
 constexpr uint32_t kFastBits = 9;         // decode-table bits
 constexpr uint32_t kFastSize = 1u << kFastBits;
-constexpr uint64_t kPayFail = 1ull << 63;  // rec_pay marker: inflate failed, no CRC check
+constexpr uint64_t kPayFail = 1ull << 63;    // rec_pay marker: no CRC check by k_gzip_crc (inflate failed,
+                                              // or several members, whose CRCs the inflate checked)
+constexpr uint64_t kPayResize = 1ull << 62;  // rec_pay marker: output larger than the framing's size
+constexpr uint64_t kPayLen = ~(kPayFail | kPayResize);
 // RFC 1951 3.2.7 code-length code order; in constant memory so the uniform index is a scalar load
 // (a local array indexed at run time lived in scratch)
 __constant__ uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -231,20 +238,71 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t s, uint32_t& eb) {  // s 
     return ((2u + (s & 1u)) << eb) + 1u;
 }
 
-enum : int { kGzOk = 0, kGzCorrupt = 1, kGzUnsupported = 2 };
+enum : int { kGzOk = 0, kGzCorrupt = 1, kGzUnsupported = 2, kGzResize = 3, kGzOkChecked = 4 };
 
-// Inflate one record's single gzip member into `out` (exactly dlen bytes announced by ISIZE).
-// kWhole: the window holds the whole record (flushed once at the end; decoding past it hands the file
-// back, see the header).
-template <uint32_t kWin, uint32_t kIn>
+// CRC-32/IEEE table for the per-member checks of records of several members (k_gzip_crc checks a
+// record against its one trailer; these records are rare, so one lane runs the table loop)
+struct CrcTab {
+    uint32_t t[256];
+    constexpr CrcTab() : t() {
+        for (uint32_t k = 0; k < 256; k++) {
+            uint32_t c = k;
+            for (int j = 0; j < 8; j++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+            t[k] = c;
+        }
+    }
+};
+__constant__ CrcTab kCrc = CrcTab();
+
+// running CRC-32 register (pre/post-inverted by the caller) over n bytes of the LDS window from w0
+// (`win`) or of global memory (`g`); lane 0 computes, every lane gets the result
+template <uint32_t kWin>
+__device__ uint32_t gz_crc_run(uint32_t c, const uint8_t* win, uint32_t w0, const uint8_t* g, uint32_t n,
+                               uint32_t lane) {
+    if (lane == 0)
+        for (uint32_t k = 0; k < n; k++) c = kCrc.t[(c ^ (win ? win[(w0 + k) & (kWin - 1)] : g[k])) & 0xFFu] ^ (c >> 8);
+    __builtin_amdgcn_wave_barrier();
+    return uni(c);
+}
+
+// Inflate one record's gzip members into `out` (dlen bytes, the size the framing or k_gz_resize gave
+// it). kWhole: the window holds the whole record (flushed once at the end). kCount (k_gz_resize):
+// the record is decoded through the window but nothing is stored, every member's CRC-32 and ISIZE
+// are checked, *total = the output of every member; a record Go's reader fails on is kGzCorrupt.
+// Output past dlen is never stored: kGzResize (k_gz_resize decides).
+template <uint32_t kWin, uint32_t kIn, bool kCount = false>
 __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen, uint8_t* out, uint32_t dlen,
-                         uint32_t lane) {
-    constexpr bool kWhole = kWin < kGzLargeWin;
+                         uint32_t lane, uint64_t* total = nullptr) {
+    constexpr bool kWhole = kWin < kGzLargeWin && !kCount;
+    constexpr uint32_t kMaxOut = 0xFFFFFFF0u;  // counted sizes past this are handed back
+    const uint32_t cap = kCount ? kMaxOut : dlen;
     GzTables& T = S.t;
     BitIn<kIn> B{src, S.in, slen, 0, 0, 0ull, 0};
+    uint32_t d = 0, flushed = 0, dm = 0;  // dm: output position where the current member starts
+    uint32_t mcrc = 0xFFFFFFFFu;          // kCount: CRC-32 register of the member's flushed bytes
+    bool multi = false;
+    auto flush = [&](uint32_t upto) {  // window bytes [flushed, upto) -> HBM, 16 per lane
+        if (kCount) {  // nothing stored: the bytes leaving the window go into the member's CRC
+            mcrc = gz_crc_run<kWin>(mcrc, S.win, flushed, nullptr, upto - flushed, lane);
+            flushed = upto;
+            return;
+        }
+        while (flushed < upto) {
+            const uint32_t q = flushed + lane * 16;
+            if (q < upto) {
+                const uint4 v = *reinterpret_cast<const uint4*>(S.win + (q & (kWin - 1)));
+                if (q + 16 <= upto)
+                    stu16(out + q, v);
+                else
+                    st_partial(out + q, v, upto - q);
+            }
+            flushed = min(upto, flushed + 1024);
+        }
+    };
+  for (;;) {  // members
     B.refill(lane);
-    // ---- member header (gzip reader.go readHeader) ----
-    if (slen < 10) return kGzCorrupt;
+    // ---- member header (gzip reader.go readHeader: io.ReadFull of 10 bytes) ----
+    if (slen - min(slen, (uint32_t)(B.consumed() >> 3)) < 10) return kGzCorrupt;
     const uint32_t id = B.bits(16), cm = B.bits(8), flg = B.bits(8);
     if (id != 0x8B1Fu || cm != 8u) return kGzCorrupt;
     B.refill(lane);
@@ -290,21 +348,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
     if (B.overrun()) return kGzCorrupt;
 
     // ---- DEFLATE blocks (flate inflate.go) ----
-    uint32_t d = 0, flushed = 0;
     bool fin = false;
-    auto flush = [&](uint32_t upto) {  // window bytes [flushed, upto) -> HBM, 16 per lane
-        while (flushed < upto) {
-            const uint32_t q = flushed + lane * 16;
-            if (q < upto) {
-                const uint4 v = *reinterpret_cast<const uint4*>(S.win + (q & (kWin - 1)));
-                if (q + 16 <= upto)
-                    stu16(out + q, v);
-                else
-                    st_partial(out + q, v, upto - q);
-            }
-            flushed = min(upto, flushed + 1024);
-        }
-    };
     while (!fin) {
         B.refill(lane);
         fin = B.bits(1) != 0;
@@ -320,14 +364,14 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             if (B.overrun() || (ln ^ 0xFFFFu) != nl) return kGzCorrupt;
             const uint32_t p0 = p + 4;
             if (ln > slen - min(slen, p0)) return kGzCorrupt;
-            if (kWhole && d + ln > kWin) return kGzUnsupported;
+            if (ln > cap - d) return kCount ? kGzUnsupported : kGzResize;
             // 1 KiB at a time, flushing in between: the window never overruns unflushed bytes
             for (uint32_t k0 = 0; k0 < ln; k0 += 1024) {
                 const uint32_t m = min(1024u, ln - k0);
                 for (uint32_t k = lane; k < m; k += 64) S.win[(d + k) & (kWin - 1)] = src[p0 + k0 + k];
                 __builtin_amdgcn_wave_barrier();
                 d += m;
-                if (!kWhole && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
+                if (!kWhole && d - flushed >= 1024) flush(d & ~1023u);
             }
             B.pos = p0 + ln;
             B.nb = 0;
@@ -399,7 +443,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             const int s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
             if (s < 0 || B.overrun()) return kGzCorrupt;
             if (s < 256) {
-                if (kWhole && d >= kWin) return kGzUnsupported;
+                if (d >= cap) return kCount ? kGzUnsupported : kGzResize;
                 if (lane == 0) S.win[d & (kWin - 1)] = (uint8_t)s;
                 d++;
             } else if (s == 256) {
@@ -413,8 +457,8 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                 if (ds < 0 || ds >= 30) return kGzCorrupt;
                 uint32_t deb;
                 const uint32_t dist = dist_base((uint32_t)ds, deb) + B.bits(deb);
-                if (B.overrun() || dist > d) return kGzCorrupt;
-                if (kWhole && d + len > kWin) return kGzUnsupported;
+                if (B.overrun() || dist > d - dm) return kGzCorrupt;  // not into an earlier member
+                if (len > cap - d) return kCount ? kGzUnsupported : kGzResize;
                 // source bytes all precede d: k mod dist repeats the last `dist` bytes
                 const float rc = 1.0f / (float)dist;
                 for (uint32_t k0 = 0; k0 < len; k0 += 64) {
@@ -432,17 +476,54 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                 d += len;
             }
             __builtin_amdgcn_wave_barrier();
-            if (!kWhole && d - flushed >= 1024) flush(min(d & ~1023u, dlen));
+            if (!kWhole && d - flushed >= 1024) flush(d & ~1023u);
         }
     }
-    // ---- trailer: byte-aligned CRC-32 + ISIZE ending the payload (one member per record) ----
+    // ---- trailer: byte-aligned CRC-32 + ISIZE of this member ----
     const uint32_t tp = (uint32_t)((B.consumed() + 7) >> 3);
-    if (tp + 8 > slen) return kGzCorrupt;           // truncated trailer (io.ErrUnexpectedEOF)
-    if (tp + 8 < slen) return kGzUnsupported;        // another member follows (multistream)
-    if (d != dlen) return kGzCorrupt;                // ISIZE mismatch (gzip.ErrChecksum)
+    if (tp + 8 > slen) return kGzCorrupt;  // truncated trailer (io.ErrUnexpectedEOF)
+    B.pos = tp;
+    B.nb = 0;
+    B.bb = 0;
+    B.refill(lane);
+    const uint32_t want_crc = B.bits(32), isize = B.bits(32);
+    if (isize != d - dm) return kGzCorrupt;  // gzip.ErrChecksum (size)
+    multi = multi || tp + 8 < slen;
+    if (kCount || multi) {
+        // this member's CRC-32 here (k_gzip_crc sees the record's last trailer only)
+        __builtin_amdgcn_wave_barrier();
+        uint32_t got;
+        if (kCount) {
+            flush(d);
+            got = mcrc ^ 0xFFFFFFFFu;
+            mcrc = 0xFFFFFFFFu;
+        } else if (kWhole) {
+            got = gz_crc_run<kWin>(0xFFFFFFFFu, S.win, dm, nullptr, d - dm, lane) ^ 0xFFFFFFFFu;
+        } else {
+            // bytes already flushed from the arena, the rest from the window (no extra flush: the
+            // flush position stays 1 KiB aligned, so no 16-byte read straddles the window's end)
+            const uint32_t g_end = max(dm, flushed);
+            uint32_t c = 0xFFFFFFFFu;
+            if (g_end > dm) {
+                __threadfence_block();  // the member's stores complete before lane 0 reads them back
+                c = gz_crc_run<kWin>(c, nullptr, 0, out + dm, g_end - dm, lane);
+            }
+            got = gz_crc_run<kWin>(c, S.win, g_end, nullptr, d - g_end, lane) ^ 0xFFFFFFFFu;
+        }
+        if (got != want_crc) return kGzCorrupt;  // gzip.ErrChecksum
+    }
+    if (tp + 8 == slen) break;  // nothing after the trailer: the reader's clean io.EOF
+    // the next member's header follows (Go's multistream Reader)
+    dm = d;
+  }
+    if (kCount) {
+        *total = d;
+        return kGzOk;
+    }
+    if (d != dlen) return kGzResize;  // several members, or a shorter output than the size claimed
     __builtin_amdgcn_wave_barrier();
     flush(d);
-    return kGzOk;  // CRC-32: k_gzip_crc
+    return multi ? kGzOkChecked : kGzOk;  // one member: CRC-32 by k_gzip_crc
 }
 
 __device__ __forceinline__ bool gzip_active(const FrameParams& P, const ScanState* st) {
@@ -472,8 +553,8 @@ constexpr uint32_t gz_in() { return kWin == kGzTinyWin ? kGzTinyIn : kGzIn; }
 template <uint32_t kWin>
 __global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(FrameParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const ScanState* st = P.state;
-    if (!gzip_active(P, st)) return;
+    ScanState* st = P.state;
+    if (!gzip_active(P, st) || (P.redo && !st->gz_redo)) return;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     using Lds = GzLds<kWin, gz_in<kWin>()>;
     Lds& S = *reinterpret_cast<Lds*>(lds + wv * sizeof(Lds));
@@ -486,14 +567,23 @@ __global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(
         const uint32_t cls = dlen <= kGzTinyWin ? kGzTinyWin : dlen <= kGzSmallWin ? kGzSmallWin : kGzLargeWin;
         if (cls != kWin) continue;
         const uint64_t pay = P.rec_pay[i];
-        const uint64_t slen = pay >> 8;
+        const uint64_t slen = (pay & kPayLen) >> 8;
         if (slen >= 0xFFFFFFF0ull || dlen >= 0xFFFFFFF0ull) {
             if (lane == 0) gz_fail(P, i, kGzUnsupported);
             continue;
         }
         const int rc = gz_record<kWin, gz_in<kWin>()>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen, P.out + o0,
                                        (uint32_t)dlen, lane);
-        if (rc != kGzOk && lane == 0) gz_fail(P, i, rc);
+        if (lane == 0) {
+            if (rc == kGzOkChecked) {
+                P.rec_pay[i] = pay | kPayFail;  // every member's CRC checked here
+            } else if (rc == kGzResize && !P.redo) {
+                P.rec_pay[i] = pay | kPayFail | kPayResize;  // sized by k_gz_resize, decoded in the redo round
+                st->gz_resize = 1u;
+            } else if (rc != kGzOk) {
+                gz_fail(P, i, rc == kGzResize ? kGzCorrupt : rc);  // (redo round: the counted size is final)
+            }
+        }
     }
 }
 
@@ -507,14 +597,14 @@ __global__ void __launch_bounds__(256) k_gzip_crc(FrameParams P) {
     }
     __syncthreads();
     const ScanState* st = P.state;
-    if (!gzip_active(P, st)) return;
+    if (!gzip_active(P, st) || (P.redo && !st->gz_redo)) return;
     const uint64_t n = st->n_records;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
         const uint64_t pay = P.rec_pay[i];
         if (pay & kPayFail) continue;
-        const uint64_t slen = (pay & ~kPayFail) >> 8;
+        const uint64_t slen = (pay & kPayLen) >> 8;
         const uint8_t* t = P.file + P.rec_off[i] + (pay & 0xFF) + slen - 8;
         const uint32_t want = t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
         const uint8_t* o = P.out + P.out_off[i];
@@ -531,6 +621,61 @@ __global__ void __launch_bounds__(256) k_gzip_crc(FrameParams P) {
         for (; k < len; k++) c = tab[(c ^ o[k]) & 0xFFu] ^ (c >> 8);
         if ((c ^ 0xFFFFFFFFu) != want) mark_bad(P, i);  // gzip.ErrChecksum
     }
+}
+
+// Sizes of the records the decoders marked kPayResize: every member's output counted (nothing stored),
+// one wave per record, the chunk's scratch length and byte sum corrected for the redo scan; a record
+// Go's reader fails on is flagged corrupt (its size stays the framing's). One wave per chunk (its
+// records are slots [0, owned) of ChunkPlace, as in k_place). A file whose placement came from the
+// sequential repair (rare) is handed back at the first such record instead.
+__global__ void __launch_bounds__(64 * kGzWaves) k_gz_resize(FrameParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    ScanState* st = P.state;
+    if (!st->gz_resize || !gzip_active(P, st)) return;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    if (!st->slow && blockIdx.x == 0 && threadIdx.x == 0) {  // read by the redo round's kernels only
+        st->gz_redo = 1u;
+        st->scan_ticket = 0;
+        st->first_bad = kNone;  // recounted by the redo placement and decoders
+        st->n_bad = 0;
+    }
+    using Lds = GzLds<kGzLargeWin, kGzIn>;  // the DEFLATE window: the CRCs need the bytes
+    Lds& S = *reinterpret_cast<Lds*>(lds + wv * sizeof(Lds));
+    for (uint64_t c = (uint64_t)blockIdx.x * kGzWaves + wv; c < P.n_chunks; c += (uint64_t)gridDim.x * kGzWaves) {
+    const ChunkPlace pl = P.place[c];
+    uint64_t* sl = P.scratch_len + c * P.slots;
+    for (uint64_t k = 0; k < pl.owned; k++) {
+        const uint64_t i = pl.base_idx + k;
+        const uint64_t pay = P.rec_pay[i];
+        if (!(pay & kPayResize)) continue;
+        if (st->slow) {
+            if (lane == 0) atomicMin((unsigned long long*)&st->unsupported_rec, (unsigned long long)i);
+            continue;
+        }
+        uint64_t total = 0;
+        const int rc = gz_record<kGzLargeWin, kGzIn, true>(S, P.file + P.rec_off[i] + (pay & 0xFF),
+                                                              (uint32_t)((pay & kPayLen) >> 8), nullptr, 0, lane, &total);
+        if (lane == 0) {
+            if (rc == kGzOk) {
+                const uint64_t old = sl[k] & kLenMask;
+                sl[k] = (sl[k] & ~kLenMask) | total;
+                P.chunks[c].bytes += total - old;  // (this wave is the chunk's only writer)
+            } else if (rc == kGzCorrupt) {
+                sl[k] |= kBadBit;
+            } else {
+                atomicMin((unsigned long long*)&st->unsupported_rec, (unsigned long long)i);
+            }
+        }
+    }
+    }
+}
+
+hipError_t launch_gzip_resize(const FrameParams& P, hipStream_t s) {
+    // one workgroup per CU (the DEFLATE windows fill the LDS), chunks grid-stride: a file with no
+    // such record costs one short launch
+    hipLaunchKernelGGL(k_gz_resize, dim3(256), dim3(64 * kGzWaves), kGzWaves * sizeof(GzLds<kGzLargeWin, kGzIn>),
+                       s, P);
+    return hipGetLastError();
 }
 
 hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s) {

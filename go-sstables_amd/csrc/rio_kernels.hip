@@ -368,6 +368,8 @@ __device__ void init_state(const FrameParams& P) {
     st->scan_ticket = 0;
     st->finish_ticket = 0;
     st->pipe_next = 0;
+    st->gz_resize = 0;
+    st->gz_redo = 0;
     if (P.len < RIO_FILE_HEADER_BYTES) {
         st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;
         st->version = st->compression = 0;
@@ -766,6 +768,7 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
     const int t = threadIdx.x;
     const uint64_t c = (uint64_t)blockIdx.x * kScanBlock + t;
     if (P.state->hdr_status != RIO_OK) return;  // block-uniform
+    if (P.redo && !P.state->gz_redo) return;
     RunSum v = c < P.n_chunks ? chunk_run(P, c) : run_identity();
     int cur = 0;
     buf[cur][t] = v;
@@ -933,6 +936,7 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     ScanState* st = P.state;
     if (st->hdr_status != RIO_OK) return;
+    if (P.redo && !st->gz_redo) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (st->n_records > P.rec_cap || st->total_bytes > P.out_cap)
             st->capacity_fail = 1;
@@ -1653,6 +1657,19 @@ hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main);  // rio_snappy.hip
 hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s);             // rio_snappy.hip
 hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s);              // rio_gzip.hip
+hipError_t launch_gzip_resize(const FrameParams& P, hipStream_t s);              // rio_gzip.hip
+
+// gzip redo round: records holding several members (Go's multistream reader) are sized by
+// k_gz_resize; then the scan, placement and gzip decoders run again with the corrected sizes. Every
+// kernel of the round exits at once unless a record needed it.
+static void launch_gzip_redo(const FrameParams& P0, hipStream_t s) {
+    FrameParams P = P0;
+    P.redo = 1;
+    launch_gzip_resize(P, s);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
+    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+    launch_gzip_decode(P, s);
+}
 
 // the decoders of one file: by the compression hint, or all of them (each exits unless the file is
 // its own)
@@ -1662,7 +1679,10 @@ static void launch_decoders(const FrameParams& P, hipStream_t s, bool snappy_mai
     if (any || c == RIO_COMP_NONE || c == RIO_COMP_SNAPPY)
         hipLaunchKernelGGL(k_copy_records, dim3(2048), dim3(256), 0, s, P);
     if ((any || c == RIO_COMP_SNAPPY) && snappy_main) launch_snappy_decode(P, s, true);
-    if (any || c == RIO_COMP_GZIP) launch_gzip_decode(P, s);
+    if (any || c == RIO_COMP_GZIP) {
+        launch_gzip_decode(P, s);
+        launch_gzip_redo(P, s);
+    }
 }
 
 // Decode: placement (+ capacity check, zero tail), the decoders, k_finish (verify + result).

@@ -92,28 +92,30 @@ class DeviceDecoder:
     def decode_batch(self, files: list, stream=None):
         """Size every file's outputs with capacity-0 probes (one batch call), then decode the batch.
         Returns [(buffers, info)] in file order."""
-        probes = [self.alloc(0, 0) for _ in files]
-        self.launch_batch(files, probes, stream)
-        torch.cuda.synchronize(self.device)
-        infos = [self.info(b) for b in probes]
-        bufs = [self.alloc(i["n_records"], i["total_out_bytes"]) if i["status"] == L.RIO_ERR_CAPACITY else b
-                for b, i in zip(probes, infos)]
-        self.launch_batch(files, bufs, stream)
-        torch.cuda.synchronize(self.device)
+        bufs = [self.alloc(0, 0) for _ in files]
+        # a gzip record of several members is larger than the framing's size: its decode asks again
+        for _ in range(3):
+            self.launch_batch(files, bufs, stream)
+            torch.cuda.synchronize(self.device)
+            infos = [self.info(b) for b in bufs]
+            if all(i["status"] != L.RIO_ERR_CAPACITY for i in infos):
+                break
+            bufs = [self.alloc(i["n_records"], i["total_out_bytes"]) if i["status"] == L.RIO_ERR_CAPACITY else b
+                    for b, i in zip(bufs, infos)]
         return [(b, self.info(b)) for b in bufs]
 
     def decode(self, d_file: torch.Tensor, length: int, stream=None, comp=None):
         """Size the outputs with a capacity-0 probe, then decode. Returns (buffers, info)."""
-        probe = self.alloc(0, 0)
-        self.launch(d_file, length, probe, stream, comp)
-        torch.cuda.synchronize(self.device)
-        pi = self.info(probe)
-        if pi["status"] != L.RIO_ERR_CAPACITY:
-            return probe, pi
-        b = self.alloc(pi["n_records"], pi["total_out_bytes"])
-        self.launch(d_file, length, b, stream, comp)
-        torch.cuda.synchronize(self.device)
-        return b, self.info(b)
+        b = self.alloc(0, 0)
+        # (a gzip record of several members is larger than the framing's size: the decode asks again)
+        for _ in range(3):
+            self.launch(d_file, length, b, stream, comp)
+            torch.cuda.synchronize(self.device)
+            info = self.info(b)
+            if info["status"] != L.RIO_ERR_CAPACITY:
+                break
+            b = self.alloc(info["n_records"], info["total_out_bytes"])
+        return b, info
 
     def stage_ms(self):
         ms = (ctypes.c_float * 4)()

@@ -198,16 +198,25 @@ def cases():
 # ---------------------------------------------------------------------------------------------
 # gzip-compressed files (compType 1, GzipCompressor: one gzip member per record)
 # ---------------------------------------------------------------------------------------------
-def gzip_member(data: bytes, level: int = 6, strategy: int = 0, header: bytes = None) -> bytes:
-    """One gzip member. header=None: zlib's own 10-byte header; else `header` + raw DEFLATE + trailer."""
+def gzip_member(data: bytes, level: int = 6, strategy: int = 0, header: bytes = None, zdict: bytes = None) -> bytes:
+    """One gzip member. header=None: zlib's own 10-byte header; else `header` + raw DEFLATE + trailer.
+    zdict: DEFLATE with a preset dictionary, so the body refers back past its own start."""
     import zlib
 
-    if header is None:
+    if header is None and zdict is None:
         co = zlib.compressobj(level, zlib.DEFLATED, 31, 9, strategy)
         return co.compress(data) + co.flush()
-    co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+    co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy, **({"zdict": zdict} if zdict else {}))
     body = co.compress(data) + co.flush()
-    return header + body + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data) & 0xFFFFFFFF)
+    return ((header or gzip_header()) + body +
+            struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data) & 0xFFFFFFFF))
+
+
+def gzip_members(data: bytes, cuts, **kw) -> bytes:
+    """`data` as consecutive gzip members split at the offsets `cuts` (Go's multistream reader
+    concatenates their outputs). The record header's uncompressed size is len(data)."""
+    pts = [0] + list(cuts) + [len(data)]
+    return b"".join(gzip_member(data[a:b], **kw) for a, b in zip(pts, pts[1:]))
 
 
 def gzip_header(flg=0, extra=b"", name=b"", comment=b"", hcrc=None) -> bytes:
@@ -255,8 +264,8 @@ def text_records(n, seed, lo=1, hi=1500):
 
 def gzip_cases():
     """(name, image, may_fall_back) gzip files. may_fall_back marks inputs the device path may hand
-    back to the reference reader (RIO_ERR_UNSUPPORTED: a record with more than one member, or one
-    decoding past the small window)."""
+    back to the reference reader (RIO_ERR_UNSUPPORTED); none of these does any more: records of
+    several members decode on the device."""
     import zlib
 
     rng = random.Random(11)
@@ -292,20 +301,45 @@ def gzip_cases():
     corrupt("gz_bad_cm", 7, p[:2] + b"\x07" + p[3:])
     corrupt("gz_bad_crc", 7, p[:-8] + bytes([p[-8] ^ 1]) + p[-7:])
     corrupt("gz_isize_plus1", 7, p[:-4] + struct.pack("<I", good[7][0] + 1))
-    corrupt("gz_isize_minus1", 7, p[:-4] + struct.pack("<I", good[7][0] - 1), may=True)
+    corrupt("gz_isize_minus1", 7, p[:-4] + struct.pack("<I", good[7][0] - 1))
     corrupt("gz_isize_huge", 7, p[:-4] + struct.pack("<I", 0xFFFFFFF0))
-    corrupt("gz_truncated_trailer", 7, p[:-3], may=True)
-    corrupt("gz_truncated_body", 7, p[:len(p) // 2], may=True)
-    corrupt("gz_tiny", 7, p[:5], may=True)
+    corrupt("gz_truncated_trailer", 7, p[:-3])
+    corrupt("gz_truncated_body", 7, p[:len(p) // 2])
+    corrupt("gz_tiny", 7, p[:5])
     corrupt("gz_empty_payload", 7, b"")
     corrupt("gz_btype3", 7, p[:10] + bytes([p[10] | 6]) + p[11:])
-    corrupt("gz_two_members", 7, gzip_member(text[7][:100]) + gzip_member(text[7][100:]), may=True)
-    corrupt("gz_trailing_garbage", 7, p + b"\x00\x01", may=True)
+    corrupt("gz_two_members", 7, gzip_member(text[7][:100]) + gzip_member(text[7][100:]))
+    corrupt("gz_trailing_garbage", 7, p + b"\x00\x01")
+    corrupt("gz_trailing_header_part", 7, p + gzip_member(b"xyz")[:7])
+    corrupt("gz_second_member_bad_crc", 7, gzip_member(text[7][:50]) +
+            (lambda q: q[:-8] + bytes([q[-8] ^ 4]) + q[-7:])(gzip_member(text[7][50:])))
+    corrupt("gz_second_member_bad_magic", 7, gzip_member(text[7][:50]) + b"\x1f\x8c" + gzip_member(text[7][50:])[2:])
+    corrupt("gz_second_member_refers_back", 7, gzip_member(text[7][:80]) +
+            gzip_member(text[7][80:], zdict=text[7][:80]))
+    corrupt("gz_first_member_bad_isize", 7, (lambda q: q[:-4] + struct.pack("<I", 51))(gzip_member(text[7][:50])) +
+            gzip_member(text[7][50:]))
     # bit flips inside the DEFLATE body (header and trailer intact)
     for j in range(12):
         q = bytearray(p)
         pos = 10 + rng.randrange(len(p) - 18)
         q[pos] ^= 1 << rng.randrange(8)
-        corrupt(f"gz_flip{j}", 7, bytes(q), may=True)
+        corrupt(f"gz_flip{j}", 7, bytes(q))
+    # records of several members (gzip.Reader is multistream: the outputs concatenate)
+    multi = [(len(r), gzip_members(r, sorted({len(r) // 3, 2 * len(r) // 3} - {0}))) for r in text[:40]]
+    cases.append(("gz_multi_three", gz_file(multi), False))
+    cases.append(("gz_multi_mixed", gz_file([multi[i] if i % 3 == 0 else good[i % 20] for i in range(40)] +
+                                            [None, (0, gzip_member(b"") + gzip_member(b"")), (0, b"")]), False))
+    cases.append(("gz_multi_empty_members", gz_file([(len(r), gzip_member(b"") + gzip_member(r) + gzip_member(b""))
+                                                    for r in text[40:60]]), False))
+    cases.append(("gz_multi_header_fields", gz_file([(len(text[i]), gzip_member(text[i][:30], header=hdrs[i % 5]) +
+                                                      gzip_member(text[i][30:], header=hdrs[(i + 2) % 5]))
+                                                     for i in range(10)]), False))
+    # sizes across the device's window classes: a small last member on a large record
+    cases.append(("gz_multi_large", gz_file([(len(r), gzip_members(r, [len(r) - 500])) for r in large] +
+                                            [(len(r), gzip_members(r, [100, 20000])) for r in large[4:6]]), False))
+    cases.append(("gz_multi_many", gz_file([(len(r), gzip_members(r, list(range(7, len(r), 37)))) for r in text[60:70]]),
+                  False))
+    cases.append(("gz_multi_stored", gz_file([(len(r), gzip_members(r, [len(r) // 2], level=0)) for r in large[:3]]),
+                  False))
     cases.append(("gz_v3", gz_file([(len(r), gzip_member(r)) for r in text[:30]], version=3), False))
     return cases
