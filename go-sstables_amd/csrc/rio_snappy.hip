@@ -121,9 +121,12 @@ __device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& h
     hi = sel4(r != 0, b, a);
 }
 
-// cache policy experiment knob (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads
+// cache policy (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads. Default 1: the
+// arena stores no longer push the lanes' input lines out of L2 between their 16-byte reads (C2
+// decode: HBM reads 4.1 -> 3.4 GB and writes 1.12 -> 1.03 GB per launch, 0.9 % slower, because far
+// copies then miss L2 more often; C4: 3 % faster). 2 and 3 were slower (+5 %, +8 %).
 #ifndef RIO_NT
-#define RIO_NT 0
+#define RIO_NT 1
 #endif
 // timing-only experiment knobs (wrong output): 1 = no out16 funnel, 2 = no place16, 4 = no in16 funnel,
 // 8 = no flush bpermutes of the owner base, 16 = far-history loads to the sink (traffic attribution),
