@@ -143,7 +143,9 @@ int rio_device_count(int* out);
 
 /* ---- host-memory two-phase API (the cgo binding: one call pair per file) --------------------
  * rio_frame: H2D copy of the file through pinned staging, device framing (record boundaries,
- * header CRC, decoded sizes) and the scan; fills `info` (sizes the caller must allocate).
+ * header CRC, decoded sizes) and the scan; fills `info` (sizes the caller must allocate). For a
+ * gzip file rio_frame also decodes it (a record of several gzip members is larger than its last
+ * member's ISIZE, the framing's size, which only the decode finds out), so the sizes are exact.
  * rio_decode: device decode of every framed record + D2H of the results into caller buffers:
  *   out      [>= info->total_out_bytes]  concatenated record bytes
  *   out_off  [n_records + 1]             record i = out[out_off[i] .. out_off[i+1])
@@ -158,7 +160,10 @@ int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, 
  * synchronisation (graph-capturable). Outputs are device pointers with the layout above; the
  * result struct is written to device memory `d_info`. `d_file` must have RIO_DEVICE_PAD readable
  * bytes past `len`. If the decoded size exceeds out_cap or rec_cap, d_info->status is
- * RIO_ERR_CAPACITY and nothing is decoded. `stream` is a hipStream_t (NULL = the ctx stream). */
+ * RIO_ERR_CAPACITY with the sizes needed in d_info and nothing usable is decoded (call again with
+ * outputs of that size). A gzip file whose records of several members outgrow the framing's sizes
+ * reports this only after its decode: a capacity-0 probe can undersize it, so loop on CAPACITY.
+ * `stream` is a hipStream_t (NULL = the ctx stream). */
 int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                       uint64_t rec_cap, rio_file_info* d_info, void* stream);
@@ -215,7 +220,7 @@ int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_
  * of every value on the device (the two calls above), D2H of what the iterator needs. The handle owns
  * host copies; pointers from rio_sst_entry stay valid until rio_sst_free.
  * Returns RIO_ERR_UNSUPPORTED (no handle, `info` filled) when either file is one the device path hands
- * back (recordio v1/v2, lzw, multi-member gzip): the adapter keeps the reference reader. Otherwise the
+ * back (recordio v1/v2, lzw): the adapter keeps the reference reader. Otherwise the
  * handle is returned and `info` says which of the reference's load errors applies: index/data status
  * outside the EOF family (reading error), first_bad_proto (proto.Unmarshal error, slice_key_index.go:
  * 107-110), first_unplaced (not the writer's layout: keep the reference reader), first_bad_crc
