@@ -830,8 +830,14 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     // Records go to waves in chunks of 64 lanes x rpc consecutive records (each lane one contiguous
     // range: one stream, no drain between its records). Chunk g is wave g's; a wave that finishes
     // takes the next unclaimed chunk, so waves whose records decode slower, or that start later, do
-    // not hold the kernel's tail. About four chunks per wave.
-    const uint64_t rpc = n >= 4 * 64 * waves ? n / (4 * 64 * waves) : 1;
+    // not hold the kernel's tail. About eight chunks per wave.
+// chunks per wave: the balance against the per-chunk drain and setup (A/B on MI355X, records per lane
+// per chunk: C3 64-B records 19 -> 9: decode 0.906 -> 0.870 ms; 4: 0.922, 1: 1.92; C2 stays at 1)
+#ifndef RIO_CHUNKS_PER_WAVE
+#define RIO_CHUNKS_PER_WAVE 8
+#endif
+    constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
+    const uint64_t rpc = n >= kCpw * 64 * waves ? n / (kCpw * 64 * waves) : 1;
     const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
     uint64_t chunk = g;
     while (chunk < nchunks) {
