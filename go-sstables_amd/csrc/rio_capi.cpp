@@ -202,6 +202,11 @@ struct rio_ctx {
     DevBuf q_pfx, q_pfx_out, q_idx, q_perm, q_tmp;
     uint8_t* pinned[2] = {nullptr, nullptr};
     hipEvent_t pin_ev[2] = {};
+    // device-API calls share the ctx's scratch: a call on another stream than the previous one waits
+    // for it (order_ev, recorded after every device-API call)
+    hipEvent_t order_ev = nullptr;
+    hipStream_t order_stream = nullptr;
+    bool order_valid = false;
     // last host-API framing (rio_frame -> rio_decode)
     FrameParams last{};
     bool framed = false;
@@ -281,6 +286,10 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
+    if (c->order_ev) {  // the last device-API call may have run on a caller's stream
+        hipEventSynchronize(c->order_ev);
+        hipEventDestroy(c->order_ev);
+    }
     c->fa.release();
     for (auto& a : c->batch) a->release();
     for (DevBuf* b : {&c->sink, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
@@ -329,6 +338,37 @@ extern "C" int rio_ctx_last_stage_ms(rio_ctx* c, float* ms, int n) {
 // ------------------------------------------------------------------------------------------
 // device-resident single call
 // ------------------------------------------------------------------------------------------
+// The device-API calls of one ctx use the same scratch arenas: a call on a stream other than the
+// previous call's waits for that call first (stream-ordered, no host synchronisation).
+static int order_before(rio_ctx* ctx, hipStream_t s) {
+    if (ctx->order_valid && ctx->order_stream != s) HIP_TRY(hipStreamWaitEvent(s, ctx->order_ev, 0));
+    return RIO_OK;
+}
+static int order_after(rio_ctx* ctx, hipStream_t s) {
+    if (!ctx->order_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ctx->order_ev, s));
+    ctx->order_stream = s;
+    ctx->order_valid = true;
+    return RIO_OK;
+}
+
+extern "C" int rio_ctx_reserve(rio_ctx* ctx, uint64_t max_file_len, uint64_t max_records, uint32_t max_batch) {
+    if (!ctx || max_batch > kMaxBatch) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    FrameParams P;
+    if (int rc = ctx_frame_params(ctx, nullptr, max_file_len, P, ctx->fa)) return rc;
+    HIP_TRY(ctx->fa.rec_pay.ensure((max_records + 1) * 8));
+    HIP_TRY(ctx->fa.rec_desc.ensure((max_records + 1) * 16));
+    while (ctx->batch.size() < max_batch) ctx->batch.emplace_back(new FileArenas());
+    for (uint32_t j = 0; j < max_batch; j++) {
+        FileArenas& A = *ctx->batch[j];
+        if (int rc = ctx_frame_params(ctx, nullptr, max_file_len, P, A)) return rc;
+        HIP_TRY(A.rec_pay.ensure((max_records + 1) * 8));
+        HIP_TRY(A.rec_desc.ensure((max_records + 1) * 16));
+    }
+    if (!ctx->order_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
+    return RIO_OK;
+}
 extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                                  uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                                  uint64_t rec_cap, rio_file_info* d_info, void* stream) {
@@ -359,10 +399,11 @@ extern "C" int rio_device_decode_ex(rio_ctx* ctx, const uint8_t* d_file, uint64_
     P.rec_desc = ctx->fa.rec_desc.as<uint4>();
     P.comp_hint = compression;
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    if (int rc2 = order_before(ctx, s)) return rc2;
     hipEvent_t* ev = ctx->next_events();
     HIP_TRY(launch_frame(P, s, ev));
     HIP_TRY(launch_phase_b(P, s, ev));
-    return RIO_OK;
+    return order_after(ctx, s);
 }
 
 // Batch of device-resident files (BASELINE configs[3]: the 8 files of a GPU's shard in one step):
@@ -382,6 +423,7 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
             return RIO_ERR_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    if (int rc = order_before(ctx, s)) return rc;
     while (ctx->batch.size() < std::min<uint32_t>(n_files, kMaxBatch)) ctx->batch.emplace_back(new FileArenas());
     hipEvent_t* ev = ctx->next_events();
     for (uint32_t g = 0; g < n_files; g += kMaxBatch) {
@@ -417,7 +459,7 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
         }
         HIP_TRY(launch_phase_b_batch(B, s, last));
     }
-    return RIO_OK;
+    return order_after(ctx, s);
 }
 
 // ------------------------------------------------------------------------------------------

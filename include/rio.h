@@ -164,6 +164,12 @@ int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, 
  * outputs of that size). A gzip file whose records of several members outgrow the framing's sizes
  * reports this only after its decode: a capacity-0 probe can undersize it, so loop on CAPACITY.
  * `stream` is a hipStream_t (NULL = the ctx stream). */
+/* Calls of one ctx share its device scratch: a device-API call on a stream other than the previous
+ * call's waits (stream-ordered) for that call. Arenas grow on demand (hipMalloc); before capturing
+ * calls into a hipGraph, size them with rio_ctx_reserve (largest file length, record count and batch
+ * size to come) so that nothing is allocated during capture, and capture on the stream of the
+ * previous call. */
+int rio_ctx_reserve(rio_ctx* ctx, uint64_t max_file_len, uint64_t max_records, uint32_t max_batch);
 int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                       uint64_t rec_cap, rio_file_info* d_info, void* stream);

@@ -67,3 +67,31 @@ def test_threads_with_own_contexts_on_one_device(threads):
     assert not errors, errors
     for t in range(threads):
         assert_same_as_oracle(results[t], expect[t], f"thread {t}")
+
+
+def test_device_calls_alternating_streams_after_reserve():
+    """Device-API calls of one ctx on two streams in turn, with no host synchronisation between them:
+    each call waits for the previous one (they share the ctx's scratch), so every result is the
+    oracle's. rio_ctx_reserve first sizes the arenas (nothing is allocated between the calls)."""
+    import torch
+
+    from recordio.device import DecodeBuffers, DeviceDecoder, to_device_file  # noqa: F401
+
+    imgs = [generate(4000, 1024, 2, kind=1, seed=71).tobytes(), generate(9000, 300, 2, kind=1, seed=72).tobytes(),
+            generate(2000, 900, 0, kind=0, seed=73).tobytes()]
+    dec = DeviceDecoder(0)
+    assert L.lib().rio_ctx_reserve(dec.ctx, max(len(i) for i in imgs), 20000, 2) == 0
+    files = [to_device_file(i) for i in imgs]
+    sized = [dec.decode(d, n)[1] for d, n in files]  # sizes (and a warm ctx)
+    bufs = [dec.alloc(i["n_records"], i["total_out_bytes"]) for i in sized]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(3):
+        for k, ((d, n), b) in enumerate(zip(files, bufs)):
+            dec.launch(d, n, b, streams[(k + rep) % 2])
+    torch.cuda.synchronize()
+    for k, (img, b) in enumerate(zip(imgs, bufs)):
+        info = dec.info(b)
+        n, nb = info["n_records"], info["total_out_bytes"]
+        g = dict(info, out=b.out[:nb].cpu().numpy(), out_off=b.out_off[:n + 1].cpu().numpy(),
+                 rec_off=b.rec_off[:n].cpu().numpy(), flags=b.flags[:n].cpu().numpy())
+        assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), f"stream file {k}")
