@@ -235,3 +235,16 @@ def test_compression_hint_launches_only_that_codec(name):
     wrong = 1 if comp != 1 else 2
     _, bad = decoder().decode(d, n, comp=wrong)
     assert bad["status"] == L.RIO_ERR_ARG and bad["n_records"] == 0
+
+
+@pytest.mark.parametrize("n,ln", [(1, 300), (2, 40), (63, 200), (64, 200), (65, 200), (127, 100), (4097, 64),
+                                  (131071, 16), (131073, 16), (1_048_577, 24), (2_100_001, 12)])
+def test_record_counts_around_decoder_chunks(n, ln):
+    """Snappy files whose record counts sit on and around the lane decoder's chunk boundaries (64
+    lanes x records per lane per chunk; one record per lane up to 8 x 64 x waves records, two past
+    2 M), so partial chunks, idle lanes and the chunk counter's last claims are all exercised."""
+    img = corpus.generate(n, ln, 2, kind=1, seed=n)
+    g = gpu_decode_arrays(img)
+    o = orc.file_reader_decode_arrays(img)
+    assert o["n_records"] == n
+    assert_same_as_oracle(g, o, f"{n} x {ln}")
