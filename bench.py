@@ -60,7 +60,7 @@ WAL_METRIC = "wal replay GiB/s (host WAL files -> ordered host records, PCIe-inc
 IDX_METRIC = "DiskKeyIndex lookups/s (device-resident index.rio, batched Get)"
 ENC_METRIC = "recordio v4 encode GiB/s of records (device-resident, golang/snappy block format)"
 PCIE_PEAK_GBPS = 128.0  # PCIe Gen5 x16, both directions (64 GB/s each)
-DECODE_KERNEL = {0: "k_decode_copy", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
+DECODE_KERNEL = {0: "k_copy_records", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
 # configs decoded as a fixed file set sharded over the ranks: name -> (files, first seed)
 MULTI_FILE = {"c4": (8, 100)}
 SST_TABLES = 8  # C5: 10M keys in 8 tables of 1.25M
@@ -959,7 +959,7 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
             traffic = None
     pipe_ms = sum(stage) if stage else float("nan")
     if comp == 2 and kind == 0:
-        kernel = "k_snappy_literal"  # ref-random records are each one literal: the copy path decodes them
+        kernel = "k_copy_records"  # ref-random records are each one literal: the copy path decodes them
     elif comp == 2 and rec_len >= int(os.environ.get("RIO_COOP_MIN", str(1 << 56)), 0):
         kernel = "k_snappy_coop_batch" if batch else "k_snappy_coop"  # wave-per-record decoder (opt-in)
     elif comp == 2 and batch:
