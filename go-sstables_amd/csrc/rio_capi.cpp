@@ -581,10 +581,12 @@ static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const u
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->predecoded = false;
     const rio_file_info& fi = ctx->frame_info;
-    if (fi.compression == RIO_COMP_GZIP && fi.status != RIO_ERR_VERSION && fi.status != RIO_ERR_COMPRESSION_TYPE &&
+    const bool expand = fi.compression == RIO_COMP_GZIP || fi.compression == RIO_COMP_LZW;
+    if (expand && fi.status != RIO_ERR_VERSION && fi.status != RIO_ERR_COMPRESSION_TYPE &&
         fi.status != RIO_ERR_UNSUPPORTED && fi.status != RIO_ERR_SHORT_FILE_HEADER) {
-        // gzip: decode now. The framing sizes a record from its last member's ISIZE; a record of
-        // several members (Go's multistream reader) is larger, which only the decode finds out, and
+        // gzip / lzw: decode now. The framing sizes a gzip record from its last member's ISIZE, an lzw
+        // record from its header's u; a record of several gzip members (Go's multistream reader) is
+        // larger, an lzw record under a header that lies differs, which only the decode finds out, and
         // the caller allocates from the sizes returned here. A decode that needs more room than the
         // framing's sizes reports RIO_ERR_CAPACITY with the sizes it needs: frame and decode again
         // into arenas of that size (the whole pipeline: framing resets the device state).
@@ -600,7 +602,7 @@ static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const u
             if (attempt) HIP_TRY(launch_phase_a(P, ctx->stream, nullptr));
             FrameParams D = P;
             D.zero_done = 1;  // phase A ran k_zero
-            D.comp_hint = RIO_COMP_GZIP;
+            D.comp_hint = fi.compression;
             D.out = ctx->out.as<uint8_t>();
             D.out_cap = nb;
             D.out_off = ctx->out_off.as<uint64_t>();
@@ -1140,7 +1142,7 @@ static int readat_check(rio_reader* r, const uint8_t** data, uint64_t* len, int*
     if (len) *len = 0;
     if (is_nil) *is_nil = 0;
     if (!r->open || r->closed) return RIO_ERR_STATE;
-    if (r->version < RIO_VERSION3 || r->compression == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;
+    if (r->version < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
     return RIO_OK;
 }
 
@@ -1179,9 +1181,10 @@ extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* re
         const int rc = readat_kernel(r, s, true, seek_len, &ro, data, len, is_nil);
         if (rec_offset) *rec_offset = ro;
         tl_det.off = rc == RIO_ERR_INVALID_OFFSET ? offset : ro;
-        // gzip: the kernel stops at a trial whose payload needs inflating; a record start is served
+        // gzip / lzw: the kernel stops at a trial whose payload needs expanding; a record start is served
         // from the decoded index (an io.EOF-class one continues the scan), anything else is handed back
-        const uint64_t i = rc == RIO_ERR_UNSUPPORTED && r->compression == RIO_COMP_GZIP ? x->find(ro) : x->n;
+        const bool expand = r->compression == RIO_COMP_GZIP || r->compression == RIO_COMP_LZW;
+        const uint64_t i = rc == RIO_ERR_UNSUPPORTED && expand ? x->find(ro) : x->n;
         if (i == x->n) return rc;
         if (x->flags[i] & RIO_FLAG_EOF) {
             s = ro + 3;

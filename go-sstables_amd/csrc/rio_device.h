@@ -19,7 +19,11 @@ constexpr uint32_t kFailLanes = 1024;
 // Snappy decode launch shape (k_snappy_pipe): every wave owns one 64-byte sink line that absorbs
 // the pipeline's placeholder loads and stores.
 constexpr unsigned kSnappyBlock = 256;
-constexpr unsigned kSnappyGrid = 512;
+// RIO_SNAPPY_GRID: experiment builds only (make variant VDEFS=-DRIO_SNAPPY_GRID=256); the sink is sized for 512
+#ifndef RIO_SNAPPY_GRID
+#define RIO_SNAPPY_GRID 512
+#endif
+constexpr unsigned kSnappyGrid = RIO_SNAPPY_GRID;
 constexpr uint64_t kSinkBytes = (uint64_t)kSnappyBlock / 64 * kSnappyGrid * 64;
 
 // Framing chunk: a byte range [cs, ce) of the file; a chunk OWNS the records whose header starts
@@ -80,8 +84,9 @@ struct ScanState {
     uint32_t finish_ticket; // k_finish: the last block to finish publishes the result
     uint32_t pipe_next;     // k_snappy_pipe: next record chunk handed to a wave that finished its own
     uint32_t gz_resize;     // gzip: some record holds several members whose output the framing's
-                            // size (its last member's ISIZE) does not cover: k_gz_resize sizes them
-    uint32_t gz_redo;       // k_gz_resize ran: the scan, placement and gzip decoders run again
+                            // size (its last member's ISIZE) does not cover: k_gz_resize sizes them;
+                            // lzw: some record's output is not its header's u (k_lzw_resize)
+    uint32_t gz_redo;       // k_gz_resize / k_lzw_resize ran: the scan, placement and decoders run again
 };
 
 // Result of the single-record (ReadNextAt) kernel.
@@ -120,7 +125,9 @@ struct FrameParams {
     // launched and exits unless the file is its own); k_finish rejects a file that contradicts it
     uint32_t comp_hint;
     uint32_t zero_done;  // the zero-tail check already ran (host API phase A): k_place skips it
-    uint32_t redo;       // gzip redo round (k_gz_resize onwards): the kernel exits unless gz_resize
+    uint32_t redo;       // redo round of this codec (RIO_COMP_GZIP: k_gz_resize onwards, RIO_COMP_LZW:
+                         // k_lzw_resize onwards; 0: first round): the kernel exits unless the file is
+                         // that codec's and its resize kernel ran
     ChunkSum* chunks;
     RunSum* block_runs;      // [n_blocks] (scan level 1 output)
     RunSum* chunk_excl;      // [n_chunks] exclusive within-block prefix

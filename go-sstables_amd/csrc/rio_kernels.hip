@@ -206,6 +206,11 @@ __device__ void crc32c_tab_init(uint32_t* T) {
     __syncthreads();
 }
 
+// lzw records are sized by the header's u (the reference's buffer size, the decoded length for every
+// file its writer produces) while an lzw stream of `plen` bytes can reach it: a 9-bit code expands to
+// at most 4096 bytes (oracle ORC_LZW_MAX_RATIO). k_lzw_decode counts and re-places any other size.
+__device__ __forceinline__ uint64_t lzw_size(uint64_t u, uint64_t plen) { return u <= 4096ull * plen ? u : 0; }
+
 // FileReader sequential semantics at record start p: header + payload availability + decoded
 // size. next = start of the following record; pay = rec_pay descriptor (rio_device.h).
 // Common records (canonical magic, header + preamble inside 32 bytes, valid) are parsed from two
@@ -251,6 +256,8 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
                 if (!nil && comp == RIO_COMP_SNAPPY && hl <= 24) {
                     k = varint8(win8(w, hl), dl);
                     ok = k && k <= plen && dl <= 0xFFFFFFFFull && dl <= 22ull * (plen - k) + 64;
+                } else if (!nil && comp == RIO_COMP_LZW) {
+                    dl = lzw_size(u, plen);
                 } else if (!nil && comp != RIO_COMP_NONE) {
                     ok = false;  // snappy preamble outside the window; gzip: sized by its trailer
                 }
@@ -322,6 +329,8 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
             return RIO_OK;
         }
         out_len = isz;
+    } else if (comp == RIO_COMP_LZW) {
+        out_len = lzw_size(h.u, plen);
     } else {
         out_len = plen;
     }
@@ -342,7 +351,7 @@ __device__ __forceinline__ int file_header_status(const FrameParams& P, uint32_t
     c = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
     if (v > RIO_VERSION4 || v < RIO_VERSION1) return RIO_ERR_VERSION;
     if (c > RIO_COMP_LZW) return RIO_ERR_COMPRESSION_TYPE;
-    if (v < RIO_VERSION3 || c == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;  // reference reader keeps these
+    if (v < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;  // reference reader keeps these
     return RIO_OK;
 }
 
@@ -386,7 +395,7 @@ __device__ void init_state(const FrameParams& P) {
     } else if (c > RIO_COMP_LZW) {
         hs = RIO_ERR_COMPRESSION_TYPE;
         st->det0 = c;
-    } else if (v < RIO_VERSION3 || c == RIO_COMP_LZW) {
+    } else if (v < RIO_VERSION3) {
         hs = RIO_ERR_UNSUPPORTED;  // reference reader keeps these
     }
     st->hdr_status = hs;
@@ -768,7 +777,7 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
     const int t = threadIdx.x;
     const uint64_t c = (uint64_t)blockIdx.x * kScanBlock + t;
     if (P.state->hdr_status != RIO_OK) return;  // block-uniform
-    if (P.redo && !P.state->gz_redo) return;
+    if (P.redo && (!P.state->gz_redo || P.state->compression != P.redo)) return;  // another codec's redo round
     RunSum v = c < P.n_chunks ? chunk_run(P, c) : run_identity();
     int cur = 0;
     buf[cur][t] = v;
@@ -936,7 +945,7 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     ScanState* st = P.state;
     if (st->hdr_status != RIO_OK) return;
-    if (P.redo && !st->gz_redo) return;
+    if (P.redo && (!st->gz_redo || st->compression != P.redo)) return;  // another codec's redo round
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (st->n_records > P.rec_cap || st->total_bytes > P.out_cap)
             st->capacity_fail = 1;
@@ -1215,11 +1224,13 @@ __device__ int read_at_dev(const uint8_t* f, uint64_t len, uint32_t ver, uint32_
         for (uint64_t k = 0; k < plen; k++) out[k] = pay[k];
         return RIO_OK;
     }
-    if (comp == RIO_COMP_GZIP) {
-        // gzip.NewReader on an empty payload: io.EOF (mmap_reader.go:189-191 wraps it). A payload to
-        // inflate is the host's: it serves record starts from the reader's decoded index and hands
-        // anything else back (r.payload_off / r.len locate it)
-        return plen == 0 ? RIO_EOF_CODEC : RIO_ERR_UNSUPPORTED;
+    if (comp == RIO_COMP_GZIP || comp == RIO_COMP_LZW) {
+        // gzip.NewReader on an empty payload: io.EOF (mmap_reader.go:189-191 wraps it); lzw: an empty
+        // payload is io.ErrUnexpectedEOF. A payload to inflate / expand is the host's: it serves record
+        // starts from the reader's decoded index and hands anything else back (r.payload_off / r.len
+        // locate it)
+        if (plen == 0) return comp == RIO_COMP_GZIP ? RIO_EOF_CODEC : RIO_ERR_DECOMPRESS;
+        return RIO_ERR_UNSUPPORTED;
     }
     uint64_t dl = 0;
     const int k = uvarint_buf(pay, plen, dl);
@@ -1243,7 +1254,7 @@ __global__ void k_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t*
         comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
         if (ver > RIO_VERSION4 || ver < RIO_VERSION1) e = RIO_ERR_VERSION;
         else if (comp > RIO_COMP_LZW) e = RIO_ERR_COMPRESSION_TYPE;
-        else if (ver < RIO_VERSION3 || comp == RIO_COMP_LZW) e = RIO_ERR_UNSUPPORTED;
+        else if (ver < RIO_VERSION3) e = RIO_ERR_UNSUPPORTED;
     }
     if (e == RIO_OK) e = read_at_dev(f, len, ver, comp, off, out, out_cap, r, true);
     r.status = e;
@@ -1309,7 +1320,7 @@ __device__ __forceinline__ int file_header_dev(const uint8_t* f, uint64_t len, u
     comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
     if (ver > RIO_VERSION4 || ver < RIO_VERSION1) return RIO_ERR_VERSION;
     if (comp > RIO_COMP_LZW) return RIO_ERR_COMPRESSION_TYPE;
-    if (ver < RIO_VERSION3 || comp == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;
+    if (ver < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
     return RIO_OK;
 }
 
@@ -1658,17 +1669,29 @@ hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main);
 hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s);             // rio_snappy.hip
 hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s);              // rio_gzip.hip
 hipError_t launch_gzip_resize(const FrameParams& P, hipStream_t s);              // rio_gzip.hip
+hipError_t launch_lzw_decode(const FrameParams& P, hipStream_t s);               // rio_lzw.hip
+hipError_t launch_lzw_resize(const FrameParams& P, hipStream_t s);               // rio_lzw.hip
 
 // gzip redo round: records holding several members (Go's multistream reader) are sized by
 // k_gz_resize; then the scan, placement and gzip decoders run again with the corrected sizes. Every
 // kernel of the round exits at once unless a record needed it.
 static void launch_gzip_redo(const FrameParams& P0, hipStream_t s) {
     FrameParams P = P0;
-    P.redo = 1;
+    P.redo = RIO_COMP_GZIP;
     launch_gzip_resize(P, s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
     hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
     launch_gzip_decode(P, s);
+}
+
+// the same round for lzw records whose decoded size is not the header's u
+static void launch_lzw_redo(const FrameParams& P0, hipStream_t s) {
+    FrameParams P = P0;
+    P.redo = RIO_COMP_LZW;
+    launch_lzw_resize(P, s);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
+    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+    launch_lzw_decode(P, s);
 }
 
 // the decoders of one file: by the compression hint, or all of them (each exits unless the file is
@@ -1682,6 +1705,10 @@ static void launch_decoders(const FrameParams& P, hipStream_t s, bool snappy_mai
     if (any || c == RIO_COMP_GZIP) {
         launch_gzip_decode(P, s);
         launch_gzip_redo(P, s);
+    }
+    if (any || c == RIO_COMP_LZW) {
+        launch_lzw_decode(P, s);
+        launch_lzw_redo(P, s);
     }
 }
 

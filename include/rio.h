@@ -77,7 +77,7 @@ typedef enum rio_status {
     RIO_ERR_COMPRESSION_TYPE = 12,/* "unknown compression type [N]" */
     RIO_ERR_SHORT_FILE_HEADER = 13,/* fewer than 8 bytes in the file */
     RIO_ERR_INVALID_OFFSET = 14,  /* "mmap: invalid ReadAt offset N" (offset > size) */
-    RIO_ERR_UNSUPPORTED = 15,     /* valid file the GPU path does not decode (v1/v2, gzip, lzw):
+    RIO_ERR_UNSUPPORTED = 15,     /* valid file the GPU path does not decode (v1/v2):      
                                      the adapter keeps the reference reader for it */
     RIO_ERR_CAPACITY = 16,        /* caller-provided output arrays too small */
     RIO_ERR_ARG = 17,             /* bad argument */
@@ -226,7 +226,7 @@ int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_
  * of every value on the device (the two calls above), D2H of what the iterator needs. The handle owns
  * host copies; pointers from rio_sst_entry stay valid until rio_sst_free.
  * Returns RIO_ERR_UNSUPPORTED (no handle, `info` filled) when either file is one the device path hands
- * back (recordio v1/v2, lzw): the adapter keeps the reference reader. Otherwise the
+ * back (recordio v1/v2): the adapter keeps the reference reader. Otherwise the
  * handle is returned and `info` says which of the reference's load errors applies: index/data status
  * outside the EOF family (reading error), first_bad_proto (proto.Unmarshal error, slice_key_index.go:
  * 107-110), first_unplaced (not the writer's layout: keep the reference reader), first_bad_crc

@@ -11,6 +11,7 @@
  *   - github.com/golang/snappy v1.0.0 (go.mod:6) block decoder (decode.go, decode_other.go).
  *   - golang.org/x/exp/mmap ReaderAt.ReadAt bounds semantics (go.mod:10).
  *   - Go stdlib compress/gzip reader via zlib (multistream, CRC-32 + ISIZE verified).
+ *   - Go stdlib compress/lzw reader and writer (LSB, litWidth 8), restated in full.
  */
 #include "rio_oracle.h"
 
@@ -315,11 +316,171 @@ static int gzip_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* 
     return RIO_OK;
 }
 
+
+/* ---------------------------------------------------------------------------------------- */
+/* LzwCompressor (lzw_compressor.go:9-63): Go stdlib compress/lzw, LSB bit order, litWidth 8.  */
+/* Restated from Go's compress/lzw reader.go / writer.go (stdlib of go 1.25, go.mod:27; not   */
+/* vendored under /root/reference). Pinned by lzw_compessor_test.go:9-16 ("some data" -> 13   */
+/* bytes: the writer's leading clear code) and, for the decoder, by an independent decoder of */
+/* the same code stream: GIF's variable-length LZW with 8-bit literals (Pillow, tests/).       */
+/* ---------------------------------------------------------------------------------------- */
+enum { LZW_CLEAR = 256, LZW_EOF = 257, LZW_MAXW = 12, LZW_MAXCODE = 4095, LZW_INV = 0xFFFF };
+
+/* lzw.NewReader(src, LSB, 8) drained by bytes.Buffer.ReadFrom (lzw_compressor.go:52-63): reader.go
+ * decode(). A stream that ends before the eof code is io.ErrUnexpectedEOF, a code above hi is "lzw:
+ * invalid code"; both are codec errors (RIO_ERR_DECOMPRESS). Bytes after the eof code are ignored. */
+int orc_lzw_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len) {
+    static __thread uint16_t prefix[1 << LZW_MAXW];
+    static __thread uint8_t suffix[1 << LZW_MAXW];
+    uint8_t tmp[(1 << LZW_MAXW) + 2];
+    uint64_t cap = 4 * n + 64, used = 0, ip = 0;
+    uint8_t* dst = (uint8_t*)malloc(cap);
+    uint32_t bits = 0, nbits = 0, width = 9, hi = LZW_EOF, overflow = 1u << 9, last = LZW_INV;
+    *out = NULL;
+    *out_len = 0;
+    for (;;) {
+        while (nbits < width) { /* readLSB */
+            if (ip >= n) goto bad; /* io.EOF from ReadByte => io.ErrUnexpectedEOF */
+            bits |= (uint32_t)src[ip++] << nbits;
+            nbits += 8;
+        }
+        const uint32_t code = bits & ((1u << width) - 1u);
+        bits >>= width;
+        nbits -= width;
+        uint64_t sl;
+        const uint8_t* sp;
+        if (code < LZW_CLEAR) {
+            tmp[0] = (uint8_t)code;
+            sp = tmp;
+            sl = 1;
+            if (last != LZW_INV) { suffix[hi] = (uint8_t)code; prefix[hi] = (uint16_t)last; }
+        } else if (code == LZW_CLEAR) {
+            width = 9;
+            hi = LZW_EOF;
+            overflow = 1u << 9;
+            last = LZW_INV;
+            continue;
+        } else if (code == LZW_EOF) {
+            break;
+        } else if (code <= hi) {
+            uint32_t c = code, i = sizeof tmp - 1;
+            if (code == hi && last != LZW_INV) { /* KwKwK: last's expansion + its first byte */
+                c = last;
+                while (c >= LZW_CLEAR) c = prefix[c];
+                tmp[i--] = (uint8_t)c;
+                c = last;
+            }
+            while (c >= LZW_CLEAR) {
+                tmp[i--] = suffix[c];
+                c = prefix[c];
+            }
+            tmp[i] = (uint8_t)c;
+            sp = tmp + i;
+            sl = sizeof tmp - i;
+            if (last != LZW_INV) { suffix[hi] = (uint8_t)c; prefix[hi] = (uint16_t)last; }
+        } else {
+            goto bad; /* "lzw: invalid code" */
+        }
+        if (used + sl > cap) {
+            while (used + sl > cap) cap *= 2;
+            dst = (uint8_t*)realloc(dst, cap);
+        }
+        memcpy(dst + used, sp, sl);
+        used += sl;
+        last = code;
+        hi++;
+        if (hi >= overflow) {
+            if (width == LZW_MAXW) { /* table full: no new entries until a clear code */
+                last = LZW_INV;
+                hi--;
+            } else {
+                width++;
+                overflow = 1u << width;
+            }
+        }
+    }
+    *out = dst;
+    *out_len = used;
+    return RIO_OK;
+bad:
+    free(dst);
+    return RIO_ERR_DECOMPRESS;
+}
+
+typedef struct {
+    uint8_t* dst;
+    uint64_t o;
+    uint32_t bits, nbits, width;
+} lzw_w;
+static void lzw_put(lzw_w* w, uint32_t code) { /* writer.go writeLSB */
+    w->bits |= code << w->nbits;
+    w->nbits += w->width;
+    while (w->nbits >= 8) {
+        w->dst[w->o++] = (uint8_t)w->bits;
+        w->bits >>= 8;
+        w->nbits -= 8;
+    }
+}
+
+/* lzw.NewWriter(buf, LSB, 8) + one Write(record) + Close (lzw_compressor.go:12-26): writer.go. The
+ * output is fixed by the algorithm (the hash table only implements the dictionary); dst capacity
+ * >= 2 n + 16. Returns the bytes written. */
+uint64_t orc_lzw_encode(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    enum { TSIZE = 4 << LZW_MAXW, TMASK = TSIZE - 1 };
+    uint32_t* table = (uint32_t*)calloc(TSIZE, sizeof(uint32_t)); /* invalidEntry = 0 */
+    lzw_w w = {dst, 0, 0, 0, 9};
+    uint32_t hi = LZW_EOF, overflow = 1u << 9, code = 0xFFFFFFFFu;
+    if (n) { /* first Write: the clear code, then the first byte is the pending code */
+        lzw_put(&w, LZW_CLEAR);
+        code = src[0];
+        for (uint64_t k = 1; k < n; k++) {
+            const uint32_t lit = src[k], key = code << 8 | lit, hash = (key >> 12 ^ key) & TMASK;
+            int hit = 0;
+            for (uint32_t h = hash, t = table[hash]; t != 0;) {
+                if (key == t >> 12) { code = t & LZW_MAXCODE; hit = 1; break; }
+                h = (h + 1) & TMASK;
+                t = table[h];
+            }
+            if (hit) continue;
+            lzw_put(&w, code);
+            code = lit;
+            /* incHi */
+            if (++hi == overflow) { w.width++; overflow <<= 1; }
+            if (hi == LZW_MAXCODE) { /* out of codes: clear, reset, nothing inserted */
+                lzw_put(&w, LZW_CLEAR);
+                w.width = 9;
+                hi = LZW_EOF;
+                overflow = 1u << 9;
+                memset(table, 0, TSIZE * sizeof(uint32_t));
+                continue;
+            }
+            uint32_t h = hash;
+            while (table[h] != 0) h = (h + 1) & TMASK;
+            table[h] = key << 12 | hi;
+        }
+    }
+    /* Close */
+    if (code != 0xFFFFFFFFu) {
+        lzw_put(&w, code);
+        if (++hi == overflow) { w.width++; overflow <<= 1; }
+        if (hi == LZW_MAXCODE) {
+            lzw_put(&w, LZW_CLEAR);
+            w.width = 9;
+        }
+    } else {
+        lzw_put(&w, LZW_CLEAR);
+    }
+    lzw_put(&w, LZW_EOF);
+    if (w.nbits > 0) dst[w.o++] = (uint8_t)w.bits;
+    free(table);
+    return w.o;
+}
+
 static int decompress(uint32_t comp, const uint8_t* src, uint64_t n, uint8_t** out,
                       uint64_t* out_len) {
     if (comp == RIO_COMP_SNAPPY) return orc_snappy_decode(src, n, out, out_len);
     if (comp == RIO_COMP_GZIP) return gzip_decode(src, n, out, out_len);
-    return RIO_ERR_UNSUPPORTED; /* lzw: no fixture, parity unpinned, not restated */
+    return orc_lzw_decode(src, n, out, out_len);
 }
 
 /* ---------------------------------------------------------------------------------------- */
@@ -375,8 +536,10 @@ static void arena_push(arena_t* a, uint64_t rec_off, const uint8_t* data, uint64
  * record before decoding any): snappy's preamble when decodedLen accepts it and a stream of this
  * length can reach it (orc_snappy_decode's first two checks); gzip's ISIZE trailer when the payload
  * holds a whole member (>= 18 bytes) and DEFLATE's maximum ratio (258 bytes per 2 bits) can reach
- * it; otherwise 0. Not a reference behaviour: the reference returns no bytes for such a record. */
-static uint64_t bad_reserve(uint32_t comp, const uint8_t* pay, uint64_t plen) {
+ * it; lzw: the header's u when an lzw stream of this length can reach it (ORC_LZW_MAX_RATIO bytes per
+ * payload byte); otherwise 0. Not a reference behaviour: the reference returns no bytes for such a record. */
+static uint64_t bad_reserve(uint32_t comp, const uint8_t* pay, uint64_t plen, uint64_t u) {
+    if (comp == RIO_COMP_LZW) return u <= ORC_LZW_MAX_RATIO * plen ? u : 0;
     if (comp == RIO_COMP_SNAPPY) {
         uint64_t d = 0;
         const int k = go_uvarint(pay, plen, &d);
@@ -440,7 +603,7 @@ int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res)
             e = decompress(res->compression, pay, plen, &dec, &dlen);
             if (e == RIO_ERR_DECOMPRESS || e == RIO_EOF_CODEC) {
                 /* ReadNext returns the codec error; the payload is consumed and the loop goes on */
-                const uint64_t rsv = bad_reserve(res->compression, pay, plen);
+                const uint64_t rsv = bad_reserve(res->compression, pay, plen, h.u);
                 uint8_t* z = (uint8_t*)calloc(rsv ? rsv : 1, 1);
                 arena_push(&a, p, z, rsv, 0);
                 free(z);
@@ -907,7 +1070,7 @@ uint64_t orc_snappy_encode(uint8_t* dst, const uint8_t* src, uint64_t n) {
     return d;
 }
 
-/* The file FileWriter writes for these records (compression none or snappy): returns its length,
+/* The file FileWriter writes for these records (compression none, snappy or lzw): returns its length,
  * or 0 when it would exceed cap. rec_off[i] = file offset of record i (Write's return value). */
 uint64_t orc_encode_file(const uint8_t* records, const uint64_t* off, const uint8_t* flags, uint64_t n, uint32_t comp,
                          uint8_t* out, uint64_t cap, uint64_t* rec_off) {
@@ -929,6 +1092,15 @@ uint64_t orc_encode_file(const uint8_t* records, const uint64_t* off, const uint
                 scratch = (uint8_t*)malloc(scap);
             }
             c = orc_snappy_encode(scratch, pay, u);
+            pay = scratch;
+            plen = c;
+        } else if (comp == RIO_COMP_LZW && !nil) {
+            if (scap < 16 + 2 * u) {
+                free(scratch);
+                scap = 16 + 2 * u;
+                scratch = (uint8_t*)malloc(scap);
+            }
+            c = orc_lzw_encode(scratch, pay, u);
             pay = scratch;
             plen = c;
         }

@@ -54,6 +54,13 @@ int orc_seek_next(const uint8_t* f, uint64_t len, uint64_t offset, uint64_t seek
                   uint64_t* rec_offset, uint8_t** out, uint64_t* out_len, int* is_nil);
 /* snappy.Decode of golang/snappy v1.0.0 (decode.go + decode_other.go). *out malloc'd. */
 int orc_snappy_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len);
+/* lzw.NewReader(LSB, 8) drained (LzwCompressor.DecompressWithBuf, lzw_compressor.go:52-63) and
+ * lzw.NewWriter(LSB, 8) Write + Close (:12-26; dst capacity >= 2 n + 16). *out malloc'd. */
+int orc_lzw_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len);
+uint64_t orc_lzw_encode(uint8_t* dst, const uint8_t* src, uint64_t n);
+/* bytes an lzw record may decode to per payload byte, above which the device does not size a
+ * record by its header's u (a 9-bit code yields at most 4096 bytes) */
+#define ORC_LZW_MAX_RATIO 4096ull
 void orc_free(void* p);
 /* multi-threaded CPU baseline: record-parallel ReadNextAt over a known offset table; returns
  * decoded bytes (0 on error). threads <= 0 => 1. */

@@ -343,3 +343,79 @@ def gzip_cases():
                   False))
     cases.append(("gz_v3", gz_file([(len(r), gzip_member(r)) for r in text[:30]], version=3), False))
     return cases
+
+
+# ---------------------------------------------------------------------------------------------
+# lzw-compressed files (compType 3, LzwCompressor: Go compress/lzw, LSB, litWidth 8)
+# ---------------------------------------------------------------------------------------------
+def lzw_file(payloads, version=4):
+    """recordio image with explicit lzw payloads: (header_u, payload) or None (nil)."""
+    out = bytearray(file_header(version, 3))
+    for p in payloads:
+        if p is None:
+            out += header_v4(0, 0, nil=True) if version == 4 else header_v3(0, 0, nil=True)
+            continue
+        u, pay = p
+        out += (header_v4(u, len(pay)) if version == 4 else header_v3(u, len(pay))) + pay
+    return bytes(out)
+
+
+def lzw_codes(codes, width=9):
+    """A raw LSB-first code stream at a fixed width (crafted streams)."""
+    bits = nb = 0
+    out = bytearray()
+    for c in codes:
+        bits |= c << nb
+        nb += width
+        while nb >= 8:
+            out.append(bits & 0xFF)
+            bits >>= 8
+            nb -= 8
+    if nb:
+        out.append(bits & 0xFF)
+    return bytes(out)
+
+
+def lzw_cases():
+    """(name, image) lzw files: every one decodes on the device (no hand-back)."""
+    import oracle_py as orc
+
+    enc = orc.lzw_encode
+    rnd = random.Random(77)
+    text = text_records(80, 13, 1, 1500)
+    cases = [("lzw_text_small", lzw_file([(len(r), enc(r)) for r in text]))]
+    cases.append(("lzw_text_v3", lzw_file([(len(r), enc(r)) for r in text[:40]], version=3)))
+    # random bytes: about one code per byte, so these lengths sit on the width steps (255 / 767 /
+    # 1791 codes) and the writer's clear at 3838 codes
+    rand = [bytes(rnd.randrange(256) for _ in range(n)) for n in
+            (1, 2, 253, 254, 255, 256, 257, 765, 766, 767, 768, 1789, 1790, 1791, 1792, 3837, 3838, 3839, 3840, 9000, 20000)]
+    cases.append(("lzw_width_steps", lzw_file([(len(r), enc(r)) for r in rand])))
+    rep = [b"a" * n for n in (1, 2, 3, 10, 100, 1000, 5000, 70000)] + [b"ab" * 3000, b"abc" * 20000,
+                                                                        bytes(range(256)) * 40]
+    cases.append(("lzw_repetitive", lzw_file([(len(r), enc(r)) for r in rep])))
+    large = text_records(6, 17, 40000, 70000)
+    cases.append(("lzw_large", lzw_file([(len(r), enc(r)) for r in large])))
+    cases.append(("lzw_nil_empty", lzw_file([None, (0, enc(b"")), (len(text[0]), enc(text[0])), None,
+                                             (0, enc(b""))])))
+    good = [(len(r), enc(r)) for r in text[:20]]
+
+    def with_bad(name, k, item):
+        cases.append((name, lzw_file(good[:k] + [item] + good[k:])))
+
+    p = enc(text[5])
+    with_bad("lzw_truncated", 7, (len(text[5]), p[:-2]))
+    with_bad("lzw_empty_payload", 7, (0, b""))
+    with_bad("lzw_empty_payload_u", 7, (100, b""))
+    with_bad("lzw_invalid_code", 7, (3, lzw_codes([256, 97, 300, 257])))
+    with_bad("lzw_invalid_first", 7, (3, lzw_codes([258, 257])))
+    with_bad("lzw_garbage", 7, (50, bytes(rnd.randrange(256) for _ in range(40))))
+    # valid streams the reference's writer would not produce
+    with_bad("lzw_trailing_bytes", 7, (len(text[5]), p + b"\xff\x00\x13"))
+    with_bad("lzw_no_leading_clear", 7, (4, lzw_codes([104, 105, 258, 257])))
+    with_bad("lzw_double_clear", 7, (2, lzw_codes([256, 256, 120, 256, 121, 257])))
+    # header u that is not the decoded length: sized by the decode (resize round)
+    with_bad("lzw_u_small", 7, (len(text[5]) - 10, p))
+    with_bad("lzw_u_large", 7, (len(text[5]) + 300, p))
+    with_bad("lzw_u_absurd", 7, (10 ** 12, p))
+    cases.append(("lzw_u_zero_all", lzw_file([(0, enc(r)) for r in text[:30]])))
+    return cases

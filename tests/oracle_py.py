@@ -71,6 +71,9 @@ def lib():
                                             POINTER(c_int), POINTER(c_uint64), POINTER(c_uint64)]
         L.orc_snappy_encode.restype = c_uint64
         L.orc_snappy_encode.argtypes = [c_void_p, c_void_p, c_uint64]
+        L.orc_lzw_decode.argtypes = [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_uint64)]
+        L.orc_lzw_encode.restype = c_uint64
+        L.orc_lzw_encode.argtypes = [c_void_p, c_void_p, c_uint64]
         L.orc_encode_file.restype = c_uint64
         L.orc_encode_file.argtypes = [c_void_p, c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p]
         _lib = L
@@ -173,6 +176,25 @@ def snappy_decode(data: bytes):
     return st, rec
 
 
+def lzw_decode(data: bytes):
+    """(status, bytes) of LzwCompressor.DecompressWithBuf (Go compress/lzw, LSB, litWidth 8)."""
+    b, n = _buf(data)
+    out, ol = c_void_p(), c_uint64()
+    st = lib().orc_lzw_decode(b, n, byref(out), byref(ol))
+    rec = ctypes.string_at(out.value, ol.value) if st == 0 and ol.value else (b"" if st == 0 else None)
+    if out.value:
+        lib().orc_free(out)
+    return st, rec
+
+
+def lzw_encode(data: bytes) -> bytes:
+    """LzwCompressor.Compress (lzw.NewWriter(LSB, 8) + Write + Close)."""
+    b, n = _buf(data)
+    out = ctypes.create_string_buffer(2 * n + 16)
+    k = lib().orc_lzw_encode(out, b, n)
+    return out.raw[:k]
+
+
 # ---------------------------------------------------------------------------------------------
 # sstables (checker for the device scan): oracle recordio decode + proto.Unmarshal + CRC-64/ISO
 # ---------------------------------------------------------------------------------------------
@@ -262,7 +284,7 @@ def encode_file(records, comp):
     np.cumsum([0 if r is None else len(r) for r in records], out=off[1:])
     blob = b"".join(r or b"" for r in records) + b"\0"
     flags = np.array([1 if r is None else 0 for r in records] + [0], dtype=np.uint8)
-    cap = 8 + n * 40 + int(off[-1]) * 7 // 6 + 32 * n + 64
+    cap = 8 + n * 40 + int(off[-1]) * 3 // 2 + 32 * n + 64  # lzw: <= 12 bits per byte
     out = ctypes.create_string_buffer(cap)
     roff = np.zeros(max(n, 1), dtype=np.uint64)
     ln = lib().orc_encode_file(blob, off.ctypes.data, flags.ctypes.data, n, comp, out, cap, roff.ctypes.data)
