@@ -379,7 +379,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             // (its descriptor landed) or finish the range
             // (a real branch: a lane ends a record every ~130 steps, so most steps of a wave skip it;
             // it holds no memory operation, so the wave's memory schedule stays uniform)
-            const bool at_end = !pdone && rem == 0 && s == s_end;
+            // one condition in a VGPR, one branch: written with && the compiler nested three
+            // branches (and their exec-mask merges) into every step
+            uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
+            pin_v(at_end);
             if (at_end) {
                 const bool bad_len = pd != rd_end;  // snappy: d != len(dst) => ErrCorrupt
                 const bool more = k + 1 < r1;
