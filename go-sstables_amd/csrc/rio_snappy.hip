@@ -134,6 +134,11 @@ __device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& h
 #ifndef RIO_EXP
 #define RIO_EXP 0
 #endif
+// 1: the next emit's window is read after the flush data (the flush store then waits for its own
+// read only); A/B on MI355X: C2 decode -0.2 %, within noise
+#ifndef RIO_FLUSH_FIRST
+#define RIO_FLUSH_FIRST 1
+#endif
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
 }
@@ -244,7 +249,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     uint32_t drain = 0, qsrc = 0;
     // v9: the next emit's source window (three ring chunks) and its funnel shift
     uint4 wA = zero4(), wB = zero4(), wC = zero4();
-    uint32_t wF = 0;
+    uint32_t wF = 0, wN = 0;
     // the parser's input window [s, s + 16), read one step ahead (end of the previous step) so that
     // its LDS latency hides behind the emit and flush
     // (the two raw chunks travel; the funnel runs where the parser needs the bytes)
@@ -279,9 +284,12 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t r2 = d & 15u, cs = (d >> 4) + 2u;
             *L.out(cs << 4) = sel4(N.kind == 0, N.lit, N.aux);
             const uint32_t w = (N.kind == 1 ? N.q : (cs << 4) + N.q) - r2;
+            wN = w;
+#if !RIO_FLUSH_FIRST
             wA = *L.out(w);
             wB = *L.out(w + 16u);
             wC = *L.out(w + 32u);
+#endif
             wF = w & 15u;
         }
 #else
@@ -306,6 +314,13 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
             const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
             const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
+#if RIO_PIPE >= 9 && RIO_FLUSH_FIRST
+            // the next emit's window after the flush data: the store waits for fv only, the window
+            // reads stay in flight through the store and the parse
+            wA = *L.out(wN);
+            wB = *L.out(wN + 16u);
+            wC = *L.out(wN + 32u);
+#endif
             st_out(((ofb >> 31) && !(RIO_EXP & 32)) ? obase[j & 3u] + pos : sink, fv);
             fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
         }
@@ -313,11 +328,11 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         // 4. parse the next piece into this slot (selects only: lanes diverge in data, not flow)
         {
             const uint4 W = (RIO_EXP & 4) ? Wa : funnel16(Wa, Wb, pos & 15u);  // input bytes [s, s + 16)
-            const bool avail = min((pos + 15) >> 4, lastc) < whi;
             // element header at s (golang/snappy decode_other.go tag forms): every form is computed
             // and combined with selects, so divergent tags cost no exec-mask branches
             const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);  // the 4 bytes after the tag
             const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
+            const bool avail = min((pos + 15) >> 4, lastc) < whi;
             const bool is0 = t == 0, is1 = t == 1, is2 = t == 2;
             // literal: x < 60 -> length x + 1; x in [60, 63] -> x - 59 little-endian length bytes follow
             const bool lng = x >= 60;
