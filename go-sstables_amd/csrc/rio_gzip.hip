@@ -48,6 +48,10 @@ constexpr uint32_t kGzSmallWin = 2048;    // records with decoded size <= this: 
 constexpr uint32_t kGzLargeWin = 32768;   // DEFLATE window (maximum distance)
 constexpr uint32_t kFastBits = 9;         // decode-table bits
 constexpr uint32_t kFastSize = 1u << kFastBits;
+// 1: literal runs decoded several symbols per fast-table read (below, in gz_record)
+#ifndef RIO_GZ_RUN
+#define RIO_GZ_RUN 1
+#endif
 constexpr uint64_t kPayFail = 1ull << 63;    // rec_pay marker: no CRC check by k_gzip_crc (inflate failed,
                                               // or several members, whose CRCs the inflate checked)
 constexpr uint64_t kPayResize = 1ull << 62;  // rec_pay marker: output larger than the framing's size
@@ -407,7 +411,43 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             uint8_t* L = T.lens;
             while (i < total) {
                 B.refill(lane);
+#if RIO_GZ_RUN
+                // runs of plain code lengths (symbols 0..15) as in the data loop: every offset looked
+                // up at once, the chain followed through the lanes, the lengths stored in one write
+                int x;
+                {
+                    const uint32_t lim = (uint32_t)min((uint64_t)B.nb, 8ull * slen - min(8ull * slen, B.consumed()));
+                    const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
+                    uint32_t o = 0, cnt = 0, eo = 0, last = prev;
+                    uint64_t m = 0;
+                    while (o < lim) {
+                        eo = __builtin_amdgcn_readlane(e, o);
+                        const uint32_t ln = eo >> 9;
+                        if (ln == 0 || ln > lim - o || (eo & 511u) >= 16 || i + cnt >= total) break;
+                        m |= 1ull << o;
+                        last = eo & 511u;
+                        cnt++;
+                        o += ln;
+                    }
+                    if ((m >> lane) & 1ull) L[i + lane_mbcnt(m)] = (uint8_t)e;
+                    i += cnt;
+                    prev = last;
+                    B.bb = o >= 64 ? 0ull : B.bb >> o;
+                    B.nb -= o;
+                    const uint32_t ln = o < lim ? eo >> 9 : 0u;
+                    if (ln != 0 && ln <= lim - o && i < total) {  // a repeat code, complete in the lookup
+                        B.bits(ln);
+                        B.refill(lane);
+                        x = (int)(eo & 511u);
+                    } else {
+                        __builtin_amdgcn_wave_barrier();
+                        if (cnt) continue;
+                        x = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+                    }
+                }
+#else
                 const int x = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+#endif
                 if (x < 0 || B.overrun()) return kGzCorrupt;
                 uint32_t rep = 1, val = (uint32_t)x;
                 if (x == 16) {
@@ -438,9 +478,55 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             if (!gz_build(L + 288, ndist, T.dcnt, T.dsym, T.dfast, lane)) return kGzCorrupt;
         }
         // ---- compressed data (huffmanBlock) ----
+#ifdef RIO_GZ_EXP
+        if (RIO_GZ_EXP == 1) return kGzOkChecked;  // timing only: headers and tables, no data
+#endif
         for (;;) {
             B.refill(lane);
+#if RIO_GZ_RUN
+            // Literal runs, several symbols per table read: lane l looks up the code starting l bits
+            // into the bit buffer (all 64 offsets at once), then the chain from offset 0 is followed
+            // through the lanes (readlane: scalar, no LDS round trip per symbol) while it yields
+            // literals whose codes lie inside the buffered stream bits; the run's bytes are stored by
+            // their lanes in one LDS write. The symbol the chain stops at is decoded from the same
+            // lookup when its code is a complete fast-table code, else by gz_sym after a refill.
+            // (Matches decoded from the same lookup as well measured slower: the extra uniform state
+            // spills scalar registers inside the loop; C2-gzip 52.1 -> 66.0 ms.)
+            int s;
+            {
+                const uint32_t lim = (uint32_t)min((uint64_t)B.nb, 8ull * slen - min(8ull * slen, B.consumed()));
+                const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
+                uint32_t o = 0, cnt = 0, eo = 0;
+                uint64_t m = 0;
+                while (o < lim) {
+                    eo = __builtin_amdgcn_readlane(e, o);
+                    const uint32_t ln = eo >> 9;
+                    if (ln == 0 || ln > lim - o || (eo & 511u) >= 256 || d + cnt >= cap) break;
+                    m |= 1ull << o;
+                    cnt++;
+                    o += ln;
+                }
+                if ((m >> lane) & 1ull) S.win[(d + lane_mbcnt(m)) & (kWin - 1)] = (uint8_t)e;
+                d += cnt;
+                B.bb = o >= 64 ? 0ull : B.bb >> o;  // (o may be 64: B.bits takes n <= 32)
+                B.nb -= o;
+                const uint32_t ln = o < lim ? eo >> 9 : 0u;
+                if (ln != 0 && ln <= lim - o) {  // the stop symbol's code is complete in the lookup
+                    B.bits(ln);
+                    B.refill(lane);  // a length symbol's extra bits follow (gz_sym's callers refill first)
+                    s = (int)(eo & 511u);
+                } else {
+                    __builtin_amdgcn_wave_barrier();
+                    if (cnt) {
+                        if (!kWhole && d - flushed >= 1024) flush(d & ~1023u);
+                        continue;  // refill, then go on with the run
+                    }
+                    s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+                }
+            }
+#else
             const int s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+#endif
             if (s < 0 || B.overrun()) return kGzCorrupt;
             if (s < 256) {
                 if (d >= cap) return kCount ? kGzUnsupported : kGzResize;
