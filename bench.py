@@ -10,7 +10,7 @@ rio_device_decode call. value = input file bytes decoded by all ranks / max-over
 Multi-GPU: one process per GPU (torchrun); every rank decodes its own file (file sharding, no
 data-path collective; the only collectives are the timing barrier and the max-over-ranks).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2g|c1|c3|c4|c5|wal|idx|enc]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2g|c2l|c1|c3|c4|c5|wal|idx|enc|readat]
 
 c5 (SSTable load + validation + scan), wal (ordered WAL replay from host files) idx (batched
 DiskKeyIndex.Get) and enc (device v4 encode) print their own
@@ -44,6 +44,7 @@ CONFIGS = {
     "c4": (16_384, 65536, 2, 1, "C4: recordio v4, 8 files x 16384 x 64 KiB snappy records (decompress-bound), "
                                 "sharded over the GPUs"),
     "c2g": (1_000_000, 1024, 1, 1, "C2-gzip: recordio v4, 1M x 1 KiB gzip records (text-like), one file per GPU"),
+    "c2l": (1_000_000, 1024, 3, 1, "C2-lzw: recordio v4, 1M x 1 KiB lzw records (text-like), one file per GPU"),
     "wal": (WAL_FILES * WAL_RECORDS_PER_FILE, 1024, 2, 1, "WAL replay: 8 x ~128 MiB snappy WAL files (1 KiB "
                                                           "text-like records) per GPU, sorted, delivered in order"),
     "idx": (1_000_000, 20, 0, 0, "DiskKeyIndex Get: 1M SHA1 keys (half present) against the C5 index.rio "
@@ -60,7 +61,7 @@ WAL_METRIC = "wal replay GiB/s (host WAL files -> ordered host records, PCIe-inc
 IDX_METRIC = "DiskKeyIndex lookups/s (device-resident index.rio, batched Get)"
 ENC_METRIC = "recordio v4 encode GiB/s of records (device-resident, golang/snappy block format)"
 PCIE_PEAK_GBPS = 128.0  # PCIe Gen5 x16, both directions (64 GB/s each)
-DECODE_KERNEL = {0: "k_copy_records", 1: "k_gzip_inflate", 2: "k_snappy_pipe"}
+DECODE_KERNEL = {0: "k_copy_records", 1: "k_gzip_inflate", 2: "k_snappy_pipe", 3: "k_lzw_decode"}
 # configs decoded as a fixed file set sharded over the ranks: name -> (files, first seed)
 MULTI_FILE = {"c4": (8, 100)}
 SST_TABLES = 8  # C5: 10M keys in 8 tables of 1.25M
@@ -983,7 +984,7 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
                 (f", {total_files} files (seeds {MULTI_FILE[args.config][1]}..) sharded over the ranks" if batch
                  else ", one file per rank"),
         "config": {"workload": desc, "records": n, "record_bytes": rec_len, "file_bytes": length,
-                   "decoded_bytes": nb, "compression": {0: "none", 1: "gzip", 2: "snappy"}[comp],
+                   "decoded_bytes": nb, "compression": {0: "none", 1: "gzip", 2: "snappy", 3: "lzw"}[comp],
                    "files_this_rank": len(lengths),
                    "parallelism": f"file-sharded x{world} ({total_files} files), no data-path collectives"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -217,6 +217,83 @@ extern "C" void rio_encode_file_header(uint8_t* buf8, uint32_t version, uint32_t
     for (int i = 0; i < 4; i++) buf8[4 + i] = (uint8_t)(compression >> (8 * i));
 }
 
+// LzwCompressor.Compress (lzw_compressor.go:12-26): Go compress/lzw Writer, LSB bit order, litWidth 8,
+// one Write + Close. A leading clear code, codes of 9..12 bits (the width grows when the next code
+// reaches 512 / 1024 / 2048), a clear code and a reset when the next code would be 4095, then the
+// pending code and the eof code. The dictionary (prefix code, byte) -> code is an open-addressed
+// table whose entries carry a generation, so a reset or a new record costs no clearing.
+namespace {
+struct LzwDict {
+    static constexpr uint32_t kSize = 1u << 14, kMask = kSize - 1;
+    std::vector<uint32_t> key = std::vector<uint32_t>(kSize), gen = std::vector<uint32_t>(kSize, 0);
+    std::vector<uint16_t> code = std::vector<uint16_t>(kSize);
+    uint32_t cur = 0;
+    void reset() { cur++; }
+    int find(uint32_t k) const {
+        for (uint32_t h = (k >> 12 ^ k) & kMask;; h = (h + 1) & kMask) {
+            if (gen[h] != cur) return -1;
+            if (key[h] == k) return code[h];
+        }
+    }
+    void put(uint32_t k, uint32_t c) {
+        uint32_t h = (k >> 12 ^ k) & kMask;
+        while (gen[h] == cur) h = (h + 1) & kMask;
+        gen[h] = cur;
+        key[h] = k;
+        code[h] = (uint16_t)c;
+    }
+};
+}  // namespace
+
+static uint64_t lzw_encode(std::vector<uint8_t>& out, const uint8_t* src, uint64_t n) {
+    thread_local LzwDict D;
+    constexpr uint32_t kClear = 256, kEof = 257, kMaxCode = 4095;
+    out.clear();
+    out.reserve(2 * n + 16);
+    uint32_t bits = 0, nbits = 0, width = 9, hi = kEof, overflow = 512;
+    auto put = [&](uint32_t c) {
+        bits |= c << nbits;
+        nbits += width;
+        for (; nbits >= 8; nbits -= 8, bits >>= 8) out.push_back((uint8_t)bits);
+    };
+    auto inc_hi = [&]() {  // true: out of codes, the dictionary was reset
+        if (++hi == overflow) {
+            width++;
+            overflow <<= 1;
+        }
+        if (hi != kMaxCode) return false;
+        put(kClear);
+        width = 9;
+        hi = kEof;
+        overflow = 512;
+        D.reset();
+        return true;
+    };
+    D.reset();
+    if (n == 0) {
+        put(kClear);
+    } else {
+        put(kClear);
+        uint32_t cur = src[0];
+        for (uint64_t i = 1; i < n; i++) {
+            const uint32_t k = cur << 8 | src[i];
+            const int hit = D.find(k);
+            if (hit >= 0) {
+                cur = (uint32_t)hit;
+                continue;
+            }
+            put(cur);
+            cur = src[i];
+            if (!inc_hi()) D.put(k, hi);
+        }
+        put(cur);
+        inc_hi();
+    }
+    put(kEof);
+    if (nbits) out.push_back((uint8_t)bits);
+    return out.size();
+}
+
 extern "C" uint64_t rio_encode_record_v4(uint8_t* buf, uint64_t cap, uint32_t compression,
                                          const uint8_t* record, uint64_t len) {
     const bool nil = (record == nullptr);
@@ -232,6 +309,10 @@ extern "C" uint64_t rio_encode_record_v4(uint8_t* buf, uint64_t cap, uint32_t co
         plen = c;
     } else if (compression == RIO_COMP_GZIP) {
         c = gzip_encode(comp, record ? record : (const uint8_t*)"", u);
+        payload = comp.data();
+        plen = c;
+    } else if (compression == RIO_COMP_LZW) {
+        c = lzw_encode(comp, record ? record : (const uint8_t*)"", u);
         payload = comp.data();
         plen = c;
     } else if (compression != RIO_COMP_NONE) {
@@ -262,7 +343,6 @@ struct rio_writer {
 
 extern "C" int rio_writer_new(const char* path, uint32_t compression, rio_writer** out) {
     if (!path || !out || compression > RIO_COMP_LZW) return RIO_ERR_ARG;
-    if (compression == RIO_COMP_LZW) return RIO_ERR_UNSUPPORTED;
     FILE* f = fopen(path, "wb");
     if (!f) return RIO_ERR_IO;
     auto* w = new rio_writer();
@@ -278,7 +358,7 @@ extern "C" int rio_writer_new(const char* path, uint32_t compression, rio_writer
 
 extern "C" int rio_writer_write(rio_writer* w, const uint8_t* record, uint64_t len, uint64_t* offset) {
     if (!w || !w->f) return RIO_ERR_STATE;
-    uint64_t bound = RIO_RECORD_HEADER_V4_MAX + rio_snappy_max_encoded_len(len) + len / 100 + 128;
+    uint64_t bound = RIO_RECORD_HEADER_V4_MAX + rio_snappy_max_encoded_len(len) + len + 128;  // (lzw: <= 1.5 len)
     if (w->buf.size() < bound) w->buf.resize(bound);
     uint64_t n = rio_encode_record_v4(w->buf.data(), w->buf.size(), w->compression, record, len);
     if (n == 0) return RIO_ERR_CAPACITY;
@@ -370,6 +450,7 @@ extern "C" uint64_t rio_generate_bound(uint32_t compression, uint64_t n_records,
     uint64_t per = RIO_RECORD_HEADER_V4_MAX + record_len;
     if (compression == RIO_COMP_SNAPPY) per = RIO_RECORD_HEADER_V4_MAX + rio_snappy_max_encoded_len(record_len);
     if (compression == RIO_COMP_GZIP) per = RIO_RECORD_HEADER_V4_MAX + record_len + record_len / 100 + 64;
+    if (compression == RIO_COMP_LZW) per = RIO_RECORD_HEADER_V4_MAX + 2 * record_len + 16;
     return 8 + n_records * per;
 }
 

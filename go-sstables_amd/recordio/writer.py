@@ -54,7 +54,7 @@ def encode_file(records, compression: int = 0) -> bytes:
     parts = [hdr.raw]
     for r in records:
         n = 0 if r is None else len(r)
-        cap = 64 + int(lib.rio_snappy_max_encoded_len(n)) + n // 50 + 64
+        cap = 64 + int(lib.rio_snappy_max_encoded_len(n)) + n // 2 + 64  # lzw: <= 1.5 n + 8
         buf = ctypes.create_string_buffer(cap)
         if r is None:
             w = lib.rio_encode_record_v4(buf, cap, compression, None, 0)

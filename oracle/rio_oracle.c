@@ -1094,7 +1094,7 @@ uint64_t orc_encode_file(const uint8_t* records, const uint64_t* off, const uint
             c = orc_snappy_encode(scratch, pay, u);
             pay = scratch;
             plen = c;
-        } else if (comp == RIO_COMP_LZW && !nil) {
+        } else if (comp == RIO_COMP_LZW) { /* nil records too: c = len(Compress(nil)), file_writer.go:198-207 */
             if (scap < 16 + 2 * u) {
                 free(scratch);
                 scap = 16 + 2 * u;

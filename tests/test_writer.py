@@ -31,7 +31,7 @@ def test_generator_byte_identical_to_reference_writer(name, records, comp):
     assert orc.encode_file(records, comp)[0] == read_fixture("v4_compat", name)
 
 
-@pytest.mark.parametrize("comp", [0, 2])
+@pytest.mark.parametrize("comp", [0, 2, 3])
 def test_oracle_encoder_matches_generator(comp):
     from corpus import mixed_records
 
@@ -96,3 +96,15 @@ def test_generator_deterministic():
     a = generate(500, 64, compression=2, kind=1, seed=3, threads=1)
     b = generate(500, 64, compression=2, kind=1, seed=3, threads=4)
     assert a.tobytes() == b.tobytes()
+
+
+def test_lzw_generator_size_kat():
+    """LzwCompressor (lzw_compressor.go:12-26) in the generator: the reference's size KAT
+    (lzw_compessor_test.go:9-16, "some data" -> 13 bytes) and the empty / nil record (3 bytes)."""
+    img = encode_file([b"some data", b"", None], 3)
+    r = orc.file_reader_decode(img)
+    assert r["records"] == [b"some data", b"", None]
+    p = 8
+    import corpus  # header lengths via the corpus helpers
+    h0 = corpus.header_v4(9, 13)
+    assert img[p:p + len(h0)] == h0
