@@ -84,11 +84,40 @@ __device__ __forceinline__ uint32_t lane_mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// A record is decoded by a group of G lanes: G = 64, the whole wave on wave-uniform state (scalar
+// registers); G = 16, four records per wave, the group-uniform state in vector registers (every lane
+// of a group computes the same value). The group's view of the wave primitives:
+template <uint32_t G>
+struct Grp {
+    static_assert(G == 64 || G == 16, "group of 16 or 64 lanes");
+    __device__ static __forceinline__ uint32_t gl(uint32_t lane) { return lane & (G - 1); }
+    // a value every lane of the group holds (G = 64: into a scalar register)
+    __device__ static __forceinline__ uint32_t uni(uint32_t v) {
+        if constexpr (G == 64) return __builtin_amdgcn_readfirstlane(v); else return v;
+    }
+    // lane l of the group (l group-uniform)
+    __device__ static __forceinline__ uint32_t rl(uint32_t v, uint32_t l, uint32_t lane) {
+        if constexpr (G == 64) return __builtin_amdgcn_readlane(v, l);
+        else return (uint32_t)__shfl((int)v, (int)((lane & ~(G - 1)) + l), 64);
+    }
+    // the group's ballot, bit k = lane k of the group
+    __device__ static __forceinline__ uint64_t ballot(bool p, uint32_t lane) {
+        if constexpr (G == 64) return __ballot(p);
+        else return (__ballot(p) >> (lane & ~(G - 1))) & ((1ull << G) - 1);
+    }
+    // set bits of m below this lane (m a group ballot)
+    __device__ static __forceinline__ uint32_t mbcnt(uint64_t m, uint32_t lane) {
+        if constexpr (G == 64) return lane_mbcnt(m);
+        else return (uint32_t)__builtin_popcountll(m & ((1ull << gl(lane)) - 1ull));
+    }
+};
+
 // Wave-uniform bit reader over the record's DEFLATE stream [0, slen), staged through an LDS ring of
 // kIn bytes refilled kIn / 2 bytes at a time.
-template <uint32_t kIn>
+template <uint32_t kIn, uint32_t G = 64>
 struct BitIn {
     static constexpr uint32_t kBlk = kIn / 2;
+    static_assert(kBlk <= 16 * G, "one pass of the group stages a block");
     const uint8_t* src;  // stream start in HBM
     uint8_t* ring;
     uint32_t slen;
@@ -104,8 +133,8 @@ struct BitIn {
     __device__ void stage(uint32_t p, uint32_t lane) {
         if (p >= loaded || p + kIn < loaded) loaded = p & ~(kBlk - 1);  // jump (stored block skip)
         while (loaded < p + 8 && loaded < slen) {
-            const uint32_t off = loaded + lane * 16;
-            if (lane * 16 < kBlk && off < slen) *reinterpret_cast<uint4*>(ring + (off & (kIn - 1))) = ldu16(src + off);
+            const uint32_t off = loaded + Grp<G>::gl(lane) * 16;
+            if (Grp<G>::gl(lane) * 16 < kBlk && off < slen) *reinterpret_cast<uint4*>(ring + (off & (kIn - 1))) = ldu16(src + off);
             loaded += kBlk;
         }
         __builtin_amdgcn_wave_barrier();
@@ -116,7 +145,7 @@ struct BitIn {
             const uint32_t a = pos & ~3u;
             const uint32_t w0 = *reinterpret_cast<const uint32_t*>(ring + (a & (kIn - 1)));
             const uint32_t w1 = *reinterpret_cast<const uint32_t*>(ring + ((a + 4) & (kIn - 1)));
-            uint32_t v = uni(__builtin_amdgcn_alignbyte(w1, w0, pos & 3u));
+            uint32_t v = Grp<G>::uni(__builtin_amdgcn_alignbyte(w1, w0, pos & 3u));
             const uint32_t valid = pos < slen ? slen - pos : 0u;
             if (valid < 4) v &= valid == 0 ? 0u : (0xFFFFFFFFu >> (32u - 8u * valid));
             bb |= (uint64_t)v << nb;
@@ -139,26 +168,29 @@ struct BitIn {
 // Lane l in [1, 16) owns code length l (its count, first canonical code and first sorted index);
 // uses with a constant l read it back with readlane into a scalar register, so no per-lane arrays
 // of wave-uniform values occupy VGPRs.
+template <uint32_t G = 64>
 __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_t* sym, uint16_t* fast,
-                         uint32_t lane) {
+                         uint32_t lane_w) {
+    using Gr = Grp<G>;
+    const uint32_t lane = Gr::gl(lane_w);
     uint32_t my_c = 0;  // codes of length `lane`
-    for (uint32_t g = 0; g < n; g += 64) {
+    for (uint32_t g = 0; g < n; g += G) {
         const uint32_t s = g + lane;
         const uint32_t L = s < n ? lens[s] : 0u;
 #pragma unroll
         for (int l = 1; l < 16; l++) {
-            const uint32_t k = (uint32_t)__builtin_popcountll(__ballot(L == (uint32_t)l));
+            const uint32_t k = (uint32_t)__builtin_popcountll(Gr::ballot(L == (uint32_t)l, lane_w));
             my_c += lane == (uint32_t)l ? k : 0u;
         }
     }
     uint32_t maxl = 0;
 #pragma unroll
-    for (int l = 1; l < 16; l++) maxl = __builtin_amdgcn_readlane(my_c, l) ? (uint32_t)l : maxl;
+    for (int l = 1; l < 16; l++) maxl = Gr::rl(my_c, l, lane_w) ? (uint32_t)l : maxl;
     // canonical codes (RFC 1951 3.2.2): first code and first sorted index of every length
     uint32_t code = 0, acc = 0, my_next = 0, my_idx = 0;
 #pragma unroll
     for (int l = 1; l < 16; l++) {
-        const uint32_t c = __builtin_amdgcn_readlane(my_c, l);
+        const uint32_t c = Gr::rl(my_c, l, lane_w);
         code <<= 1;
         my_next = lane == (uint32_t)l ? code : my_next;
         my_idx = lane == (uint32_t)l ? acc : my_idx;
@@ -168,7 +200,7 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
     if (lane < 16) cnt[lane] = (uint16_t)(lane ? my_c : 0u);
     __builtin_amdgcn_wave_barrier();
     if (maxl == 0) {
-        for (uint32_t e = lane; e < kFastSize; e += 64) fast[e] = 0;
+        for (uint32_t e = lane; e < kFastSize; e += G) fast[e] = 0;
         __builtin_amdgcn_wave_barrier();
         return true;
     }
@@ -177,27 +209,38 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
     if (full != (1u << maxl) && !(full == 1 && maxl == 1)) return false;
     // symbols sorted by (length, symbol): rank of each symbol among equal lengths via ballots
     uint32_t my_off = my_idx;  // next free sorted slot of length `lane`
-    for (uint32_t g = 0; g < n; g += 64) {
+    for (uint32_t g = 0; g < n; g += G) {
         const uint32_t s = g + lane;
         const uint32_t L = s < n ? lens[s] : 0u;
 #pragma unroll
         for (int l = 1; l < 16; l++) {
-            const uint64_t m = __ballot(L == (uint32_t)l);
-            const uint32_t base = __builtin_amdgcn_readlane(my_off, l);
-            if (L == (uint32_t)l) sym[base + lane_mbcnt(m)] = (uint16_t)s;
+            const uint64_t m = Gr::ballot(L == (uint32_t)l, lane_w);
+            const uint32_t base = Gr::rl(my_off, l, lane_w);
+            if (L == (uint32_t)l) sym[base + Gr::mbcnt(m, lane_w)] = (uint16_t)s;
             my_off += lane == (uint32_t)l ? (uint32_t)__builtin_popcountll(m) : 0u;
         }
     }
     __builtin_amdgcn_wave_barrier();
     // fast table: entry e = the next kFastBits stream bits (first bit = code MSB)
-    for (uint32_t e = lane; e < kFastSize; e += 64) {
+    // G = 16: the group's per-length values read once (through the LDS crossbar), not per entry
+    uint32_t nxl[kFastBits + 1], cl[kFastBits + 1], il[kFastBits + 1];
+    if constexpr (G != 64) {
+#pragma unroll
+        for (int l = 1; l <= (int)kFastBits; l++) {
+            nxl[l] = Gr::rl(my_next, l, lane_w);
+            cl[l] = Gr::rl(my_c, l, lane_w);
+            il[l] = Gr::rl(my_idx, l, lane_w);
+        }
+    }
+    for (uint32_t e = lane; e < kFastSize; e += G) {
         uint32_t v = 0, ent = 0;
 #pragma unroll
         for (int l = 1; l <= (int)kFastBits; l++) {
             v = (v << 1) | ((e >> (l - 1)) & 1u);
-            const uint32_t nx = __builtin_amdgcn_readlane(my_next, l), c = __builtin_amdgcn_readlane(my_c, l);
-            if (ent == 0 && v - nx < c)
-                ent = (uint32_t)sym[__builtin_amdgcn_readlane(my_idx, l) + v - nx] | ((uint32_t)l << 9);
+            const uint32_t nx = G == 64 ? __builtin_amdgcn_readlane(my_next, l) : nxl[l];
+            const uint32_t c = G == 64 ? __builtin_amdgcn_readlane(my_c, l) : cl[l];
+            const uint32_t ix = G == 64 ? __builtin_amdgcn_readlane(my_idx, l) : il[l];
+            if (ent == 0 && v - nx < c) ent = (uint32_t)sym[ix + v - nx] | ((uint32_t)l << 9);
         }
         fast[e] = (uint16_t)ent;
     }
@@ -206,9 +249,10 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
 }
 
 // One symbol; -1 if the bits match no code (incomplete / empty code).
-template <uint32_t kIn>
-__device__ __forceinline__ int gz_sym(BitIn<kIn>& B, const uint16_t* fast, const uint16_t* cnt, const uint16_t* sym) {
-    const uint32_t e = uni(fast[(uint32_t)B.bb & (kFastSize - 1)]);
+template <uint32_t kIn, uint32_t G>
+__device__ __forceinline__ int gz_sym(BitIn<kIn, G>& B, const uint16_t* fast, const uint16_t* cnt, const uint16_t* sym) {
+    using Gr = Grp<G>;
+    const uint32_t e = Gr::uni(fast[(uint32_t)B.bb & (kFastSize - 1)]);
     if (e) {
         B.bits(e >> 9);
         return (int)(e & 511u);
@@ -216,10 +260,10 @@ __device__ __forceinline__ int gz_sym(BitIn<kIn>& B, const uint16_t* fast, const
     uint32_t code = 0, first = 0, index = 0;
     for (uint32_t l = 1; l < 16; l++) {
         code |= (uint32_t)(B.bb >> (l - 1)) & 1u;
-        const uint32_t c = uni(cnt[l]);
+        const uint32_t c = Gr::uni(cnt[l]);
         if (code - first < c) {
             B.bits(l);
-            return (int)uni(sym[index + code - first]);
+            return (int)Gr::uni(sym[index + code - first]);
         }
         index += c;
         first = (first + c) << 1;
@@ -260,13 +304,13 @@ __constant__ CrcTab kCrc = CrcTab();
 
 // running CRC-32 register (pre/post-inverted by the caller) over n bytes of the LDS window from w0
 // (`win`) or of global memory (`g`); lane 0 computes, every lane gets the result
-template <uint32_t kWin>
+template <uint32_t kWin, uint32_t G = 64>
 __device__ uint32_t gz_crc_run(uint32_t c, const uint8_t* win, uint32_t w0, const uint8_t* g, uint32_t n,
                                uint32_t lane) {
-    if (lane == 0)
+    if (Grp<G>::gl(lane) == 0)
         for (uint32_t k = 0; k < n; k++) c = kCrc.t[(c ^ (win ? win[(w0 + k) & (kWin - 1)] : g[k])) & 0xFFu] ^ (c >> 8);
     __builtin_amdgcn_wave_barrier();
-    return uni(c);
+    return Grp<G>::rl(c, 0, lane);
 }
 
 // Inflate one record's gzip members into `out` (dlen bytes, the size the framing or k_gz_resize gave
@@ -274,25 +318,27 @@ __device__ uint32_t gz_crc_run(uint32_t c, const uint8_t* win, uint32_t w0, cons
 // the record is decoded through the window but nothing is stored, every member's CRC-32 and ISIZE
 // are checked, *total = the output of every member; a record Go's reader fails on is kGzCorrupt.
 // Output past dlen is never stored: kGzResize (k_gz_resize decides).
-template <uint32_t kWin, uint32_t kIn, bool kCount = false>
+template <uint32_t kWin, uint32_t kIn, bool kCount = false, uint32_t G = 64>
 __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen, uint8_t* out, uint32_t dlen,
                          uint32_t lane, uint64_t* total = nullptr) {
+    using Gr = Grp<G>;
+    const uint32_t gl = Gr::gl(lane);
     constexpr bool kWhole = kWin < kGzLargeWin && !kCount;
     constexpr uint32_t kMaxOut = 0xFFFFFFF0u;  // counted sizes past this are handed back
     const uint32_t cap = kCount ? kMaxOut : dlen;
     GzTables& T = S.t;
-    BitIn<kIn> B{src, S.in, slen, 0, 0, 0ull, 0};
+    BitIn<kIn, G> B{src, S.in, slen, 0, 0, 0ull, 0};
     uint32_t d = 0, flushed = 0, dm = 0;  // dm: output position where the current member starts
     uint32_t mcrc = 0xFFFFFFFFu;          // kCount: CRC-32 register of the member's flushed bytes
     bool multi = false;
     auto flush = [&](uint32_t upto) {  // window bytes [flushed, upto) -> HBM, 16 per lane
         if (kCount) {  // nothing stored: the bytes leaving the window go into the member's CRC
-            mcrc = gz_crc_run<kWin>(mcrc, S.win, flushed, nullptr, upto - flushed, lane);
+            mcrc = gz_crc_run<kWin, G>(mcrc, S.win, flushed, nullptr, upto - flushed, lane);
             flushed = upto;
             return;
         }
         while (flushed < upto) {
-            const uint32_t q = flushed + lane * 16;
+            const uint32_t q = flushed + gl * 16;
             if (q < upto) {
                 const uint4 v = *reinterpret_cast<const uint4*>(S.win + (q & (kWin - 1)));
                 if (q + 16 <= upto)
@@ -300,7 +346,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                 else
                     st_partial(out + q, v, upto - q);
             }
-            flushed = min(upto, flushed + 1024);
+            flushed = min(upto, flushed + 16 * G);
         }
     };
   for (;;) {  // members
@@ -372,7 +418,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             // 1 KiB at a time, flushing in between: the window never overruns unflushed bytes
             for (uint32_t k0 = 0; k0 < ln; k0 += 1024) {
                 const uint32_t m = min(1024u, ln - k0);
-                for (uint32_t k = lane; k < m; k += 64) S.win[(d + k) & (kWin - 1)] = src[p0 + k0 + k];
+                for (uint32_t k = gl; k < m; k += G) S.win[(d + k) & (kWin - 1)] = src[p0 + k0 + k];
                 __builtin_amdgcn_wave_barrier();
                 d += m;
                 if (!kWhole && d - flushed >= 1024) flush(d & ~1023u);
@@ -384,26 +430,26 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
         }
         if (type == 3) return kGzCorrupt;
         if (type == 1) {  // fixed Huffman (RFC 1951 3.2.6)
-            for (uint32_t s = lane; s < 288 + 32; s += 64)
+            for (uint32_t s = gl; s < 288 + 32; s += G)
                 T.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
             __builtin_amdgcn_wave_barrier();
-            gz_build(T.lens, 288, T.lcnt, T.lsym, T.lfast, lane);
-            gz_build(T.lens + 288, 32, T.dcnt, T.dsym, T.dfast, lane);
+            gz_build<G>(T.lens, 288, T.lcnt, T.lsym, T.lfast, lane);
+            gz_build<G>(T.lens + 288, 32, T.dcnt, T.dsym, T.dfast, lane);
         } else {  // dynamic (readHuffman)
             B.refill(lane);
             const uint32_t nlit = B.bits(5) + 257, ndist = B.bits(5) + 1, nclen = B.bits(4) + 4;
             if (nlit > 286 || ndist > 30) return kGzCorrupt;
             // code-length code lengths, in the RFC's order, into lens[0..19)
-            if (lane < 19) T.lens[lane] = 0;
+            for (uint32_t k = gl; k < 19; k += G) T.lens[k] = 0;
             __builtin_amdgcn_wave_barrier();
             for (uint32_t k = 0; k < nclen; k++) {
                 B.refill(lane);
                 const uint32_t v = B.bits(3);
-                if (lane == 0) T.lens[kClenOrder[k]] = (uint8_t)v;
+                if (gl == 0) T.lens[kClenOrder[k]] = (uint8_t)v;
             }
             if (B.overrun()) return kGzCorrupt;
             __builtin_amdgcn_wave_barrier();
-            if (!gz_build(T.lens, 19, T.lcnt, T.lsym, T.lfast, lane)) return kGzCorrupt;
+            if (!gz_build<G>(T.lens, 19, T.lcnt, T.lsym, T.lfast, lane)) return kGzCorrupt;
             // litlen + distance code lengths with the code-length code (runs 16 / 17 / 18); they
             // overwrite lens[0..19), whose code now lives in lfast / lcnt / lsym
             uint32_t i = 0, prev = 0;
@@ -412,9 +458,10 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             while (i < total) {
                 B.refill(lane);
 #if RIO_GZ_RUN
+              int x;
+              if constexpr (G == 64) {
                 // runs of plain code lengths (symbols 0..15) as in the data loop: every offset looked
                 // up at once, the chain followed through the lanes, the lengths stored in one write
-                int x;
                 {
                     const uint32_t lim = (uint32_t)min((uint64_t)B.nb, 8ull * slen - min(8ull * slen, B.consumed()));
                     const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
@@ -445,6 +492,9 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                         x = gz_sym(B, T.lfast, T.lcnt, T.lsym);
                     }
                 }
+              } else {
+                x = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+              }
 #else
                 const int x = gz_sym(B, T.lfast, T.lcnt, T.lsym);
 #endif
@@ -462,20 +512,29 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                     val = 0;
                 }
                 if (B.overrun() || i + rep > total) return kGzCorrupt;
-                for (uint32_t k = lane; k < rep; k += 64) L[i + k] = (uint8_t)val;
+                for (uint32_t k = gl; k < rep; k += G) L[i + k] = (uint8_t)val;
                 __builtin_amdgcn_wave_barrier();
                 i += rep;
                 prev = val;
             }
             // distance lengths live at lens[nlit..): move them behind the 288 litlen slots
-            for (uint32_t k = lane; k < 32; k += 64) {
-                const uint8_t v = k < ndist ? L[nlit + k] : 0;
+            {
+                // every source byte read before any is written (the ranges may overlap)
+                constexpr uint32_t kJ = (32 + G - 1) / G;
+                uint8_t v[kJ];
+#pragma unroll
+                for (uint32_t j = 0; j < kJ; j++) {
+                    const uint32_t k = gl + j * G;
+                    v[j] = k < ndist ? L[nlit + k] : 0;
+                }
                 __builtin_amdgcn_wave_barrier();
-                L[288 + k] = v;
+#pragma unroll
+                for (uint32_t j = 0; j < kJ; j++)
+                    if (gl + j * G < 32) L[288 + gl + j * G] = v[j];
             }
             __builtin_amdgcn_wave_barrier();
-            if (!gz_build(L, nlit, T.lcnt, T.lsym, T.lfast, lane)) return kGzCorrupt;
-            if (!gz_build(L + 288, ndist, T.dcnt, T.dsym, T.dfast, lane)) return kGzCorrupt;
+            if (!gz_build<G>(L, nlit, T.lcnt, T.lsym, T.lfast, lane)) return kGzCorrupt;
+            if (!gz_build<G>(L + 288, ndist, T.dcnt, T.dsym, T.dfast, lane)) return kGzCorrupt;
         }
         // ---- compressed data (huffmanBlock) ----
 #ifdef RIO_GZ_EXP
@@ -484,6 +543,8 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
         for (;;) {
             B.refill(lane);
 #if RIO_GZ_RUN
+            int s;
+            if constexpr (G == 64) {
             // Literal runs, several symbols per table read: lane l looks up the code starting l bits
             // into the bit buffer (all 64 offsets at once), then the chain from offset 0 is followed
             // through the lanes (readlane: scalar, no LDS round trip per symbol) while it yields
@@ -492,7 +553,6 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             // lookup when its code is a complete fast-table code, else by gz_sym after a refill.
             // (Matches decoded from the same lookup as well measured slower: the extra uniform state
             // spills scalar registers inside the loop; C2-gzip 52.1 -> 66.0 ms.)
-            int s;
             {
                 const uint32_t lim = (uint32_t)min((uint64_t)B.nb, 8ull * slen - min(8ull * slen, B.consumed()));
                 const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
@@ -524,13 +584,16 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                     s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
                 }
             }
+            } else {
+                s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
+            }
 #else
             const int s = gz_sym(B, T.lfast, T.lcnt, T.lsym);
 #endif
             if (s < 0 || B.overrun()) return kGzCorrupt;
             if (s < 256) {
                 if (d >= cap) return kCount ? kGzUnsupported : kGzResize;
-                if (lane == 0) S.win[d & (kWin - 1)] = (uint8_t)s;
+                if (gl == 0) S.win[d & (kWin - 1)] = (uint8_t)s;
                 d++;
             } else if (s == 256) {
                 break;
@@ -547,8 +610,8 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                 if (len > cap - d) return kCount ? kGzUnsupported : kGzResize;
                 // source bytes all precede d: k mod dist repeats the last `dist` bytes
                 const float rc = 1.0f / (float)dist;
-                for (uint32_t k0 = 0; k0 < len; k0 += 64) {
-                    const uint32_t k = k0 + lane;
+                for (uint32_t k0 = 0; k0 < len; k0 += G) {
+                    const uint32_t k = k0 + gl;
                     if (k < len) {
                         int q = (int)((float)k * rc);
                         int r = (int)k - q * (int)dist;
@@ -584,7 +647,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             got = mcrc ^ 0xFFFFFFFFu;
             mcrc = 0xFFFFFFFFu;
         } else if (kWhole) {
-            got = gz_crc_run<kWin>(0xFFFFFFFFu, S.win, dm, nullptr, d - dm, lane) ^ 0xFFFFFFFFu;
+            got = gz_crc_run<kWin, G>(0xFFFFFFFFu, S.win, dm, nullptr, d - dm, lane) ^ 0xFFFFFFFFu;
         } else {
             // bytes already flushed from the arena, the rest from the window (no extra flush: the
             // flush position stays 1 KiB aligned, so no 16-byte read straddles the window's end)
@@ -592,9 +655,9 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             uint32_t c = 0xFFFFFFFFu;
             if (g_end > dm) {
                 __threadfence_block();  // the member's stores complete before lane 0 reads them back
-                c = gz_crc_run<kWin>(c, nullptr, 0, out + dm, g_end - dm, lane);
+                c = gz_crc_run<kWin, G>(c, nullptr, 0, out + dm, g_end - dm, lane);
             }
-            got = gz_crc_run<kWin>(c, S.win, g_end, nullptr, d - g_end, lane) ^ 0xFFFFFFFFu;
+            got = gz_crc_run<kWin, G>(c, S.win, g_end, nullptr, d - g_end, lane) ^ 0xFFFFFFFFu;
         }
         if (got != want_crc) return kGzCorrupt;  // gzip.ErrChecksum
     }
@@ -631,22 +694,37 @@ __device__ __forceinline__ void gz_fail(const FrameParams& P, uint64_t i, int rc
 #ifndef RIO_GZ_TINY_WGS
 #define RIO_GZ_TINY_WGS 7
 #endif
+// records per wave of the tiny class (RIO_GZ_GROUP lanes per record: 16 = four records per wave,
+// 64 = the wave on one record)
+#ifndef RIO_GZ_GROUP
+#define RIO_GZ_GROUP 16
+#endif
+constexpr uint32_t kGzTinyG = RIO_GZ_GROUP;
 template <uint32_t kWin>
-constexpr int gz_wgs() { return kWin == kGzTinyWin ? RIO_GZ_TINY_WGS : kWin == kGzSmallWin ? 5 : 1; }
+constexpr uint32_t gz_group() { return kWin == kGzTinyWin ? kGzTinyG : 64u; }
 template <uint32_t kWin>
-constexpr uint32_t gz_in() { return kWin == kGzTinyWin ? kGzTinyIn : kGzIn; }
+constexpr int gz_wgs() {
+    return kWin == kGzTinyWin ? (kGzTinyG == 64 ? RIO_GZ_TINY_WGS : 2) : kWin == kGzSmallWin ? 5 : 1;
+}
+// input ring per record: a block is staged by one pass of the group (16 bytes per lane)
+template <uint32_t kWin>
+constexpr uint32_t gz_in() { return kWin == kGzTinyWin ? (kGzTinyG == 64 ? kGzTinyIn : 32 * kGzTinyG) : kGzIn; }
+template <uint32_t kWin>
+constexpr size_t gz_lds_bytes() { return (size_t)kGzWaves * (64 / gz_group<kWin>()) * sizeof(GzLds<kWin, gz_in<kWin>()>); }
 
 template <uint32_t kWin>
 __global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(FrameParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     ScanState* st = P.state;
     if (!gzip_active(P, st) || (P.redo && !st->gz_redo)) return;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    constexpr uint32_t G = gz_group<kWin>(), kPer = 64 / G;  // lanes per record, records per wave
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, grp = lane / G;
+    const bool lead = (lane & (G - 1)) == 0;
     using Lds = GzLds<kWin, gz_in<kWin>()>;
-    Lds& S = *reinterpret_cast<Lds*>(lds + wv * sizeof(Lds));
+    Lds& S = *reinterpret_cast<Lds*>(lds + (wv * kPer + grp) * sizeof(Lds));
     const uint64_t n = st->n_records;
-    const uint64_t waves = (uint64_t)gridDim.x * kGzWaves;
-    for (uint64_t i = (uint64_t)blockIdx.x * kGzWaves + wv; i < n; i += waves) {
+    const uint64_t groups = (uint64_t)gridDim.x * kGzWaves * kPer;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kGzWaves + wv) * kPer + grp; i < n; i += groups) {
         if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;  // nil / failed at framing
         const uint64_t o0 = P.out_off[i], dlen = P.out_off[i + 1] - o0;
         // size classes: (0, 1 KiB], (1 KiB, 2 KiB] held whole in LDS, larger ones through the DEFLATE window
@@ -655,12 +733,12 @@ __global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(
         const uint64_t pay = P.rec_pay[i];
         const uint64_t slen = (pay & kPayLen) >> 8;
         if (slen >= 0xFFFFFFF0ull || dlen >= 0xFFFFFFF0ull) {
-            if (lane == 0) gz_fail(P, i, kGzUnsupported);
+            if (lead) gz_fail(P, i, kGzUnsupported);
             continue;
         }
-        const int rc = gz_record<kWin, gz_in<kWin>()>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen, P.out + o0,
-                                       (uint32_t)dlen, lane);
-        if (lane == 0) {
+        const int rc = gz_record<kWin, gz_in<kWin>(), false, G>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen,
+                                                              P.out + o0, (uint32_t)dlen, lane);
+        if (lead) {
             if (rc == kGzOkChecked) {
                 P.rec_pay[i] = pay | kPayFail;  // every member's CRC checked here
             } else if (rc == kGzResize && !P.redo) {
@@ -766,11 +844,9 @@ hipError_t launch_gzip_resize(const FrameParams& P, hipStream_t s) {
 
 hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s) {
     hipLaunchKernelGGL(k_gzip_inflate<kGzTinyWin>, dim3(256 * gz_wgs<kGzTinyWin>()), dim3(64 * kGzWaves),
-                       kGzWaves * sizeof(GzLds<kGzTinyWin, kGzTinyIn>), s, P);
-    hipLaunchKernelGGL(k_gzip_inflate<kGzSmallWin>, dim3(1280), dim3(64 * kGzWaves),
-                       kGzWaves * sizeof(GzLds<kGzSmallWin, kGzIn>), s, P);
-    hipLaunchKernelGGL(k_gzip_inflate<kGzLargeWin>, dim3(256), dim3(64 * kGzWaves),
-                       kGzWaves * sizeof(GzLds<kGzLargeWin, kGzIn>), s, P);
+                       gz_lds_bytes<kGzTinyWin>(), s, P);
+    hipLaunchKernelGGL(k_gzip_inflate<kGzSmallWin>, dim3(1280), dim3(64 * kGzWaves), gz_lds_bytes<kGzSmallWin>(), s, P);
+    hipLaunchKernelGGL(k_gzip_inflate<kGzLargeWin>, dim3(256), dim3(64 * kGzWaves), gz_lds_bytes<kGzLargeWin>(), s, P);
     hipLaunchKernelGGL(k_gzip_crc, dim3(512), dim3(256), 0, s, P);
     return hipGetLastError();
 }
