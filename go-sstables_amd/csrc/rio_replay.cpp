@@ -420,7 +420,8 @@ struct rio_stream {
 
     void run_driver() {
         uint8_t hdr[RIO_FILE_HEADER_BYTES] = {0};
-        const bool whole = len <= RIO_FILE_HEADER_BYTES + window;
+        // (saturating: a window near 2^64 is a whole-file window, not a wrapped sum)
+        const bool whole = len <= RIO_FILE_HEADER_BYTES || window >= len - RIO_FILE_HEADER_BYTES;
         if (!whole && src.read(hdr, 0, RIO_FILE_HEADER_BYTES)) return post_fatal(0, RIO_ERR_IO);
         uint64_t s = whole ? 0 : RIO_FILE_HEADER_BYTES, first = 0;
         for (uint64_t k = 0;; k++) {
@@ -434,7 +435,7 @@ struct rio_stream {
             rio_file_info fi{};
             bool terminal = false;
             for (;;) {
-                const uint64_t e = whole ? len : std::min(len, s + w);
+                const uint64_t e = whole ? len : s + std::min(w, len - s);
                 const uint64_t hl = whole ? 0 : RIO_FILE_HEADER_BYTES, n = hl + (e - s);
                 Fill f{&src, s, hdr, hl};
                 if (int rc = rio::frame_fill(ctx[c], n, &Fill::fn, &f, &fi)) return post_fatal(k, rc);
@@ -444,7 +445,7 @@ struct rio_stream {
                 } else if (p > s) {
                     next_s = p;
                 } else if (cut_type(fi.status)) {
-                    w *= 2;
+                    w = w > (len - s) / 2 ? len - s : 2 * w;  // (reaches the file end, never wraps)
                     continue;
                 } else {
                     terminal = true;

@@ -129,6 +129,7 @@ def test_golden_fixtures(path, window):
     (600, 1024, 1, 1, 50_000),
     (20000, 64, 2, 1, 30_000),
     (40, 65536, 2, 1, 4096),  # every record larger than the window: the window doubles
+    (1500, 1024, 3, 1, 40_000),  # lzw
 ])
 def test_generated_workloads(n, rec_len, comp, kind, window):
     data = bytes(generate(n, rec_len, comp, kind=kind, seed=n + comp))
@@ -222,3 +223,22 @@ def test_file_reader_windows_large_files_by_default(tmp_path):
     assert n == exp["n_records"] == 300_000
     assert h.digest() == hashlib.sha1(exp["out"].tobytes()).digest()
     assert "EOF" in str(err)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_lzw_random_damage_random_windows(tmp_path, seed):
+    """Damaged lzw files: a flipped payload byte may leave a valid stream of another length (the
+    resize round), an invalid code, or a stream cut short; headers may break too."""
+    from test_gpu_fuzz import damage
+
+    rng = random.Random(900 + seed)
+    recs = mixed_records(rng.randint(20, 200), seed + 70, max_len=3000)
+    data = damage(rng, encode_file(recs, 3))
+    window = rng.choice([7, rng.randint(8, 600), rng.randint(600, 20_000), NEVER])
+    check_stream(data, window, depth=rng.choice([1, 2, 4]))
+    from gpu_util import assert_same_as_oracle
+
+    assert_same_as_oracle(gpu_decode_arrays(data), orc.file_reader_decode_arrays(data), f"lzw damage {seed}")
+    p = tmp_path / "l.rio"
+    p.write_bytes(data)
+    assert reader_loop(str(p), window) == reader_loop(str(p), NEVER)
