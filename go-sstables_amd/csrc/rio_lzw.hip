@@ -36,16 +36,22 @@ namespace rio {
 
 namespace {
 constexpr uint32_t kLzMaxK = 3840;             // codes of an epoch a later code may reference (258 + k <= 4095)
+// size classes: a record of slen payload bytes holds at most 8 slen / 9 codes, so records up to
+// kLzSmallLen bytes never index past kLzSmallK codes and take a table of 6 KiB (25 waves per CU
+// instead of 6)
+constexpr uint32_t kLzSmallK = 1024, kLzSmallLen = kLzSmallK * 9 / 8;
+constexpr uint32_t kLzSmallGrid = 256 * 24;
 constexpr uint64_t kLzResize = 1ull << 62;     // rec_pay marker: output size differs from the framing's
 constexpr uint64_t kLzLen = ~(3ull << 62);
 constexpr uint32_t kLzGrid = 1536;             // one-wave workgroups: 23 KiB of LDS each, 6 per CU
 enum : uint32_t { kLit = 0, kCopy = 1, kClear = 2, kEnd = 3, kBad = 4, kMissing = 5 };
 enum : int { kLzOk = 0, kLzResize_ = 1, kLzCorrupt = 2, kLzUnsupported = 3 };
 
+template <uint32_t kMaxK>
 struct LzLds {
-    uint32_t pos[kLzMaxK];  // record output position of code k of the current epoch
-    uint16_t len[kLzMaxK];  // its output length (<= 3840)
-    uint8_t slot[64];       // code starts of the current output window
+    uint32_t pos[kMaxK];  // record output position of code k of the current epoch
+    uint16_t len[kMaxK];  // its output length (<= 3840)
+    uint8_t slot[64];     // code starts of the current output window
 };
 
 // width and epoch bit offset of code k (writer.go incHi / reader.go decode: 9 bits for codes 0..254,
@@ -74,8 +80,8 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v, uint32_t lane) {
 }
 
 // one record: stream p[0, slen) -> out[0, dlen). kCount: nothing stored, *total = decoded length.
-template <bool kCount>
-__device__ int lz_record(LzLds& S, const uint8_t* p, uint32_t slen, uint8_t* out, uint32_t dlen, uint32_t lane,
+template <bool kCount, uint32_t kMaxK>
+__device__ int lz_record(LzLds<kMaxK>& S, const uint8_t* p, uint32_t slen, uint8_t* out, uint32_t dlen, uint32_t lane,
                          uint64_t* total) {
     const uint64_t nbits = 8ull * slen;
     // the payload's aligned base: every code is read from two aligned dwords (the padded file makes
@@ -137,7 +143,7 @@ __device__ int lz_record(LzLds& S, const uint8_t* p, uint32_t slen, uint8_t* out
         uint64_t src = 0;
         if (valid && kind == kCopy) src = j < k0 ? (uint64_t)S.pos[j] : pos_j;
         __builtin_amdgcn_wave_barrier();
-        if (valid && k < kLzMaxK) {
+        if (valid && k < kMaxK) {
             S.pos[k] = (uint32_t)pos;
             S.len[k] = (uint16_t)acc;
         }
@@ -216,8 +222,10 @@ __device__ __forceinline__ bool lzw_active(const FrameParams& P, const ScanState
 }
 }  // namespace
 
+template <uint32_t kMaxK>
 __global__ void __launch_bounds__(64) k_lzw_decode(FrameParams P) {
-    __shared__ LzLds S;
+    __shared__ LzLds<kMaxK> S;
+    constexpr bool kSmall = kMaxK == kLzSmallK;
     ScanState* st = P.state;
     if (!lzw_active(P, st) || (P.redo && !st->gz_redo)) return;
     const uint32_t lane = threadIdx.x;
@@ -227,11 +235,12 @@ __global__ void __launch_bounds__(64) k_lzw_decode(FrameParams P) {
         const uint64_t o0 = P.out_off[i], dlen = P.out_off[i + 1] - o0;
         const uint64_t pay = P.rec_pay[i];
         const uint64_t slen = (pay & kLzLen) >> 8;
+        if ((slen <= kLzSmallLen) != kSmall) continue;  // the other size class's
         if (slen >= 0xFFFFFFF0ull || dlen >= 0xFFFFFFF0ull) {  // past 32-bit positions: the reference reader's
             if (lane == 0) atomicMin((unsigned long long*)&st->unsupported_rec, (unsigned long long)i);
             continue;
         }
-        const int rc = lz_record<false>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen, P.out + o0,
+        const int rc = lz_record<false, kMaxK>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen, P.out + o0,
                                         (uint32_t)dlen, lane, nullptr);
         if (lane == 0) {
             if (rc == kLzResize_ && !P.redo) {
@@ -250,7 +259,7 @@ __global__ void __launch_bounds__(64) k_lzw_decode(FrameParams P) {
 // ChunkPlace, as in k_place). A file whose placement came from the sequential repair is handed back
 // at the first such record instead. (k_gz_resize's structure; the redo flags are shared.)
 __global__ void __launch_bounds__(64) k_lzw_resize(FrameParams P) {
-    __shared__ LzLds S;
+    __shared__ LzLds<kLzMaxK> S;
     ScanState* st = P.state;
     if (!st->gz_resize || !lzw_active(P, st)) return;
     const uint32_t lane = threadIdx.x;
@@ -272,7 +281,7 @@ __global__ void __launch_bounds__(64) k_lzw_resize(FrameParams P) {
                 continue;
             }
             uint64_t total = 0;
-            const int rc = lz_record<true>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)((pay & kLzLen) >> 8),
+            const int rc = lz_record<true, kLzMaxK>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)((pay & kLzLen) >> 8),
                                            nullptr, 0, lane, &total);
             if (lane == 0) {
                 if (rc == kLzOk && total < 0xFFFFFFF0ull) {
@@ -290,7 +299,8 @@ __global__ void __launch_bounds__(64) k_lzw_resize(FrameParams P) {
 }
 
 hipError_t launch_lzw_decode(const FrameParams& P, hipStream_t s) {
-    hipLaunchKernelGGL(k_lzw_decode, dim3(kLzGrid), dim3(64), 0, s, P);
+    hipLaunchKernelGGL(k_lzw_decode<kLzSmallK>, dim3(kLzSmallGrid), dim3(64), 0, s, P);
+    hipLaunchKernelGGL(k_lzw_decode<kLzMaxK>, dim3(kLzGrid), dim3(64), 0, s, P);
     return hipGetLastError();
 }
 
