@@ -61,9 +61,10 @@ constexpr uint64_t kPayLen = ~(kPayFail | kPayResize);
 __constant__ uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // per-wave decode tables
+template <uint32_t kDB = kFastBits>
 struct GzTables {
     uint16_t lfast[kFastSize];  // litlen (also the code-length code): sym | len << 9, 0 = longer code
-    uint16_t dfast[kFastSize];  // distance
+    uint16_t dfast[1u << kDB];  // distance (kDB index bits: the tiny class keeps 7, distances there are short)
     uint16_t lsym[288];         // symbols sorted by (code length, symbol)
     uint16_t dsym[32];
     uint16_t lcnt[16];          // codes per length
@@ -71,9 +72,9 @@ struct GzTables {
     uint8_t lens[288 + 32 + 8];  // code lengths being read (litlen then distance)
 };
 
-template <uint32_t kWin, uint32_t kIn>
+template <uint32_t kWin, uint32_t kIn, uint32_t kDB = kFastBits>
 struct GzLds {
-    GzTables t;
+    GzTables<kDB> t;
     uint8_t in[kIn] __attribute__((aligned(16)));
     uint8_t win[kWin] __attribute__((aligned(16)));
 };
@@ -168,7 +169,7 @@ struct BitIn {
 // Lane l in [1, 16) owns code length l (its count, first canonical code and first sorted index);
 // uses with a constant l read it back with readlane into a scalar register, so no per-lane arrays
 // of wave-uniform values occupy VGPRs.
-template <uint32_t G = 64>
+template <uint32_t G = 64, uint32_t kBits = kFastBits>
 __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_t* sym, uint16_t* fast,
                          uint32_t lane_w) {
     using Gr = Grp<G>;
@@ -200,7 +201,7 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
     if (lane < 16) cnt[lane] = (uint16_t)(lane ? my_c : 0u);
     __builtin_amdgcn_wave_barrier();
     if (maxl == 0) {
-        for (uint32_t e = lane; e < kFastSize; e += G) fast[e] = 0;
+        for (uint32_t e = lane; e < (1u << kBits); e += G) fast[e] = 0;
         __builtin_amdgcn_wave_barrier();
         return true;
     }
@@ -223,19 +224,19 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
     __builtin_amdgcn_wave_barrier();
     // fast table: entry e = the next kFastBits stream bits (first bit = code MSB)
     // G = 16: the group's per-length values read once (through the LDS crossbar), not per entry
-    uint32_t nxl[kFastBits + 1], cl[kFastBits + 1], il[kFastBits + 1];
+    uint32_t nxl[kBits + 1], cl[kBits + 1], il[kBits + 1];
     if constexpr (G != 64) {
 #pragma unroll
-        for (int l = 1; l <= (int)kFastBits; l++) {
+        for (int l = 1; l <= (int)kBits; l++) {
             nxl[l] = Gr::rl(my_next, l, lane_w);
             cl[l] = Gr::rl(my_c, l, lane_w);
             il[l] = Gr::rl(my_idx, l, lane_w);
         }
     }
-    for (uint32_t e = lane; e < kFastSize; e += G) {
+    for (uint32_t e = lane; e < (1u << kBits); e += G) {
         uint32_t v = 0, ent = 0;
 #pragma unroll
-        for (int l = 1; l <= (int)kFastBits; l++) {
+        for (int l = 1; l <= (int)kBits; l++) {
             v = (v << 1) | ((e >> (l - 1)) & 1u);
             const uint32_t nx = G == 64 ? __builtin_amdgcn_readlane(my_next, l) : nxl[l];
             const uint32_t c = G == 64 ? __builtin_amdgcn_readlane(my_c, l) : cl[l];
@@ -249,10 +250,10 @@ __device__ bool gz_build(const uint8_t* lens, uint32_t n, uint16_t* cnt, uint16_
 }
 
 // One symbol; -1 if the bits match no code (incomplete / empty code).
-template <uint32_t kIn, uint32_t G>
+template <uint32_t kIn, uint32_t G, uint32_t kBits = kFastBits>
 __device__ __forceinline__ int gz_sym(BitIn<kIn, G>& B, const uint16_t* fast, const uint16_t* cnt, const uint16_t* sym) {
     using Gr = Grp<G>;
-    const uint32_t e = Gr::uni(fast[(uint32_t)B.bb & (kFastSize - 1)]);
+    const uint32_t e = Gr::uni(fast[(uint32_t)B.bb & ((1u << kBits) - 1)]);
     if (e) {
         B.bits(e >> 9);
         return (int)(e & 511u);
@@ -318,15 +319,15 @@ __device__ uint32_t gz_crc_run(uint32_t c, const uint8_t* win, uint32_t w0, cons
 // the record is decoded through the window but nothing is stored, every member's CRC-32 and ISIZE
 // are checked, *total = the output of every member; a record Go's reader fails on is kGzCorrupt.
 // Output past dlen is never stored: kGzResize (k_gz_resize decides).
-template <uint32_t kWin, uint32_t kIn, bool kCount = false, uint32_t G = 64>
-__device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen, uint8_t* out, uint32_t dlen,
+template <uint32_t kWin, uint32_t kIn, bool kCount = false, uint32_t G = 64, uint32_t kDB = kFastBits>
+__device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t slen, uint8_t* out, uint32_t dlen,
                          uint32_t lane, uint64_t* total = nullptr) {
     using Gr = Grp<G>;
     const uint32_t gl = Gr::gl(lane);
     constexpr bool kWhole = kWin < kGzLargeWin && !kCount;
     constexpr uint32_t kMaxOut = 0xFFFFFFF0u;  // counted sizes past this are handed back
     const uint32_t cap = kCount ? kMaxOut : dlen;
-    GzTables& T = S.t;
+    GzTables<kDB>& T = S.t;
     BitIn<kIn, G> B{src, S.in, slen, 0, 0, 0ull, 0};
     uint32_t d = 0, flushed = 0, dm = 0;  // dm: output position where the current member starts
     uint32_t mcrc = 0xFFFFFFFFu;          // kCount: CRC-32 register of the member's flushed bytes
@@ -434,7 +435,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                 T.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
             __builtin_amdgcn_wave_barrier();
             gz_build<G>(T.lens, 288, T.lcnt, T.lsym, T.lfast, lane);
-            gz_build<G>(T.lens + 288, 32, T.dcnt, T.dsym, T.dfast, lane);
+            gz_build<G, kDB>(T.lens + 288, 32, T.dcnt, T.dsym, T.dfast, lane);
         } else {  // dynamic (readHuffman)
             B.refill(lane);
             const uint32_t nlit = B.bits(5) + 257, ndist = B.bits(5) + 1, nclen = B.bits(4) + 4;
@@ -534,7 +535,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
             }
             __builtin_amdgcn_wave_barrier();
             if (!gz_build<G>(L, nlit, T.lcnt, T.lsym, T.lfast, lane)) return kGzCorrupt;
-            if (!gz_build<G>(L + 288, ndist, T.dcnt, T.dsym, T.dfast, lane)) return kGzCorrupt;
+            if (!gz_build<G, kDB>(L + 288, ndist, T.dcnt, T.dsym, T.dfast, lane)) return kGzCorrupt;
         }
         // ---- compressed data (huffmanBlock) ----
 #ifdef RIO_GZ_EXP
@@ -602,7 +603,7 @@ __device__ int gz_record(GzLds<kWin, kIn>& S, const uint8_t* src, uint32_t slen,
                 uint32_t eb;
                 const uint32_t len = len_base((uint32_t)s, eb) + B.bits(eb);
                 B.refill(lane);
-                const int ds = gz_sym(B, T.dfast, T.dcnt, T.dsym);
+                const int ds = gz_sym<kIn, G, kDB>(B, T.dfast, T.dcnt, T.dsym);
                 if (ds < 0 || ds >= 30) return kGzCorrupt;
                 uint32_t deb;
                 const uint32_t dist = dist_base((uint32_t)ds, deb) + B.bits(deb);
@@ -690,6 +691,16 @@ __device__ __forceinline__ void gz_fail(const FrameParams& P, uint64_t i, int rc
 }
 }  // namespace
 
+// waves per workgroup of the four-records-per-wave class: two (28.7 KB of LDS, 5 workgroups = 40
+// records per CU). A/B on MI355X, C2-gzip: 4 waves 46.7 ms (2 workgroups fit), 2 waves 41.9, 1 wave 64.1
+#ifndef RIO_GZ_TW
+#define RIO_GZ_TW 2
+#endif
+// minimum workgroups per CU the tiny four-records-per-wave kernel is built for (register budget:
+// 3 -> 133 VGPRs, no scratch, 41.9 ms; 4 -> 128 + 16 B scratch, 42.3; 5 -> 96 + 176 B, 42.8; 6 -> 49.4)
+#ifndef RIO_GZ_TMIN
+#define RIO_GZ_TMIN 3
+#endif
 // waves per SIMD the LDS allows: tiny 5.1 KB per wave -> 7 workgroups of 4 waves, small 7.2 KB -> 5
 #ifndef RIO_GZ_TINY_WGS
 #define RIO_GZ_TINY_WGS 7
@@ -704,27 +715,46 @@ template <uint32_t kWin>
 constexpr uint32_t gz_group() { return kWin == kGzTinyWin ? kGzTinyG : 64u; }
 template <uint32_t kWin>
 constexpr int gz_wgs() {
-    return kWin == kGzTinyWin ? (kGzTinyG == 64 ? RIO_GZ_TINY_WGS : 2) : kWin == kGzSmallWin ? 5 : 1;
+    return kWin == kGzTinyWin ? (kGzTinyG == 64 ? RIO_GZ_TINY_WGS : RIO_GZ_TMIN) : kWin == kGzSmallWin ? 5 : 1;
 }
 // input ring per record: a block is staged by one pass of the group (16 bytes per lane)
 template <uint32_t kWin>
-constexpr uint32_t gz_in() { return kWin == kGzTinyWin ? (kGzTinyG == 64 ? kGzTinyIn : 32 * kGzTinyG) : kGzIn; }
+#ifndef RIO_GZ_TIN
+#define RIO_GZ_TIN 16
+#endif
+#ifndef RIO_GZ_DBITS
+#define RIO_GZ_DBITS 7
+#endif
+constexpr uint32_t gz_in() { return kWin == kGzTinyWin ? (kGzTinyG == 64 ? kGzTinyIn : RIO_GZ_TIN * kGzTinyG) : kGzIn; }
+// distance fast-table bits: records of <= 1 KiB reach back < 1 KiB (distance codes <= 19, short codes)
 template <uint32_t kWin>
-constexpr size_t gz_lds_bytes() { return (size_t)kGzWaves * (64 / gz_group<kWin>()) * sizeof(GzLds<kWin, gz_in<kWin>()>); }
+constexpr uint32_t gz_dbits() { return kWin == kGzTinyWin && kGzTinyG != 64 ? RIO_GZ_DBITS : kFastBits; }
+template <uint32_t kWin>
+using GzLdsOf = GzLds<kWin, gz_in<kWin>(), gz_dbits<kWin>()>;
+template <uint32_t kWin>
+constexpr uint32_t gz_waves() { return kWin == kGzTinyWin && kGzTinyG != 64 ? RIO_GZ_TW : kGzWaves; }
+template <uint32_t kWin>
+constexpr size_t gz_lds_bytes() { return (size_t)gz_waves<kWin>() * (64 / gz_group<kWin>()) * sizeof(GzLdsOf<kWin>); }
+template <uint32_t kWin>
+constexpr uint32_t gz_grid() {
+    return kWin == kGzTinyWin ? (kGzTinyG == 64 ? 256 * RIO_GZ_TINY_WGS : 256 * (8 / RIO_GZ_TW + (RIO_GZ_TW == 2))) :
+           kWin == kGzSmallWin ? 1280 : 256;
+}
 
 template <uint32_t kWin>
-__global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(FrameParams P) {
+__global__ void __launch_bounds__(64 * gz_waves<kWin>(), gz_wgs<kWin>()) k_gzip_inflate(FrameParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     ScanState* st = P.state;
     if (!gzip_active(P, st) || (P.redo && !st->gz_redo)) return;
     constexpr uint32_t G = gz_group<kWin>(), kPer = 64 / G;  // lanes per record, records per wave
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, grp = lane / G;
     const bool lead = (lane & (G - 1)) == 0;
-    using Lds = GzLds<kWin, gz_in<kWin>()>;
+    using Lds = GzLdsOf<kWin>;
     Lds& S = *reinterpret_cast<Lds*>(lds + (wv * kPer + grp) * sizeof(Lds));
     const uint64_t n = st->n_records;
-    const uint64_t groups = (uint64_t)gridDim.x * kGzWaves * kPer;
-    for (uint64_t i = ((uint64_t)blockIdx.x * kGzWaves + wv) * kPer + grp; i < n; i += groups) {
+    constexpr uint32_t kW = gz_waves<kWin>();
+    const uint64_t groups = (uint64_t)gridDim.x * kW * kPer;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kW + wv) * kPer + grp; i < n; i += groups) {
         if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;  // nil / failed at framing
         const uint64_t o0 = P.out_off[i], dlen = P.out_off[i + 1] - o0;
         // size classes: (0, 1 KiB], (1 KiB, 2 KiB] held whole in LDS, larger ones through the DEFLATE window
@@ -736,7 +766,7 @@ __global__ void __launch_bounds__(64 * kGzWaves, gz_wgs<kWin>()) k_gzip_inflate(
             if (lead) gz_fail(P, i, kGzUnsupported);
             continue;
         }
-        const int rc = gz_record<kWin, gz_in<kWin>(), false, G>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen,
+        const int rc = gz_record<kWin, gz_in<kWin>(), false, G, gz_dbits<kWin>()>(S, P.file + P.rec_off[i] + (pay & 0xFF), (uint32_t)slen,
                                                               P.out + o0, (uint32_t)dlen, lane);
         if (lead) {
             if (rc == kGzOkChecked) {
@@ -843,10 +873,12 @@ hipError_t launch_gzip_resize(const FrameParams& P, hipStream_t s) {
 }
 
 hipError_t launch_gzip_decode(const FrameParams& P, hipStream_t s) {
-    hipLaunchKernelGGL(k_gzip_inflate<kGzTinyWin>, dim3(256 * gz_wgs<kGzTinyWin>()), dim3(64 * kGzWaves),
+    hipLaunchKernelGGL(k_gzip_inflate<kGzTinyWin>, dim3(gz_grid<kGzTinyWin>()), dim3(64 * gz_waves<kGzTinyWin>()),
                        gz_lds_bytes<kGzTinyWin>(), s, P);
-    hipLaunchKernelGGL(k_gzip_inflate<kGzSmallWin>, dim3(1280), dim3(64 * kGzWaves), gz_lds_bytes<kGzSmallWin>(), s, P);
-    hipLaunchKernelGGL(k_gzip_inflate<kGzLargeWin>, dim3(256), dim3(64 * kGzWaves), gz_lds_bytes<kGzLargeWin>(), s, P);
+    hipLaunchKernelGGL(k_gzip_inflate<kGzSmallWin>, dim3(gz_grid<kGzSmallWin>()), dim3(64 * kGzWaves),
+                       gz_lds_bytes<kGzSmallWin>(), s, P);
+    hipLaunchKernelGGL(k_gzip_inflate<kGzLargeWin>, dim3(gz_grid<kGzLargeWin>()), dim3(64 * kGzWaves),
+                       gz_lds_bytes<kGzLargeWin>(), s, P);
     hipLaunchKernelGGL(k_gzip_crc, dim3(512), dim3(256), 0, s, P);
     return hipGetLastError();
 }
