@@ -62,22 +62,21 @@ __device__ __forceinline__ uint64_t lz_bits(uint32_t k) {
     return 9 * a + 10 * b + 11 * c + 12 * d;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        v += lane >= d ? y : 0u;
-    }
+// wave-wide inclusive scans on DPP (row shifts within 16-lane rows, then row broadcasts 15 / 31):
+// VALU latency instead of the LDS round trips of __shfl_up (as the Snappy wave decoder's)
+template <bool kMax>
+__device__ __forceinline__ uint32_t wave_incl(uint32_t v) {
+    auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : a + b; };
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
 }
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        v = lane >= d && y > v ? y : v;
-    }
-    return v;
-}
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v, uint32_t) { return wave_incl<false>(v); }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v, uint32_t) { return wave_incl<true>(v); }
 
 // one record: stream p[0, slen) -> out[0, dlen). kCount: nothing stored, *total = decoded length.
 template <bool kCount, uint32_t kMaxK>
