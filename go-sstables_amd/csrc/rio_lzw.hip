@@ -29,6 +29,8 @@
 // the counted sizes (the gzip redo round of rio_kernels.hip).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rio_device.h"
 #include "rio_dev_util.h"
 
@@ -40,18 +42,22 @@ constexpr uint32_t kLzMaxK = 3840;             // codes of an epoch a later code
 // kLzSmallLen bytes never index past kLzSmallK codes and take a table of 6 KiB (25 waves per CU
 // instead of 6)
 constexpr uint32_t kLzSmallK = 1024, kLzSmallLen = kLzSmallK * 9 / 8;
-constexpr uint32_t kLzSmallGrid = 256 * 24;
+constexpr uint32_t kLzSmallGrid = 256 * 32;
 constexpr uint64_t kLzResize = 1ull << 62;     // rec_pay marker: output size differs from the framing's
 constexpr uint64_t kLzLen = ~(3ull << 62);
 constexpr uint32_t kLzGrid = 1536;             // one-wave workgroups: 23 KiB of LDS each, 6 per CU
 enum : uint32_t { kLit = 0, kCopy = 1, kClear = 2, kEnd = 3, kBad = 4, kMissing = 5 };
 enum : int { kLzOk = 0, kLzResize_ = 1, kLzCorrupt = 2, kLzUnsupported = 3 };
 
+// positions as 16-bit values in the small class (records decoding to < 64 KiB): 4 KiB of LDS per
+// wave, 8 waves per SIMD
+template <uint32_t kMaxK>
+using LzPos = typename std::conditional<kMaxK == 1024, uint16_t, uint32_t>::type;
 template <uint32_t kMaxK>
 struct LzLds {
-    uint32_t pos[kMaxK];  // record output position of code k of the current epoch
-    uint16_t len[kMaxK];  // its output length (<= 3840)
-    uint8_t slot[64];     // code starts of the current output window
+    LzPos<kMaxK> pos[kMaxK];  // record output position of code k of the current epoch
+    uint16_t len[kMaxK];      // its output length (<= 3840)
+    uint8_t slot[64];         // code starts of the current output window
 };
 
 // width and epoch bit offset of code k (writer.go incHi / reader.go decode: 9 bits for codes 0..254,
@@ -143,7 +149,7 @@ __device__ int lz_record(LzLds<kMaxK>& S, const uint8_t* p, uint32_t slen, uint8
         if (valid && kind == kCopy) src = j < k0 ? (uint64_t)S.pos[j] : pos_j;
         __builtin_amdgcn_wave_barrier();
         if (valid && k < kMaxK) {
-            S.pos[k] = (uint32_t)pos;
+            S.pos[k] = (LzPos<kMaxK>)pos;
             S.len[k] = (uint16_t)acc;
         }
         const uint64_t d2 = d + T;
@@ -234,7 +240,7 @@ __global__ void __launch_bounds__(64) k_lzw_decode(FrameParams P) {
         const uint64_t o0 = P.out_off[i], dlen = P.out_off[i + 1] - o0;
         const uint64_t pay = P.rec_pay[i];
         const uint64_t slen = (pay & kLzLen) >> 8;
-        if ((slen <= kLzSmallLen) != kSmall) continue;  // the other size class's
+        if ((slen <= kLzSmallLen && dlen < 65536) != kSmall) continue;  // the other size class's
         if (slen >= 0xFFFFFFF0ull || dlen >= 0xFFFFFFF0ull) {  // past 32-bit positions: the reference reader's
             if (lane == 0) atomicMin((unsigned long long*)&st->unsupported_rec, (unsigned long long)i);
             continue;
