@@ -145,17 +145,19 @@ __device__ __forceinline__ uint64_t win8(const uint32_t (&w)[8], uint32_t k) {
     return r ? (a >> r) | (b << (64 - r)) : a;
 }
 
+// 7-bit groups of the four bytes of x packed (LEB128 payload bits of bytes 0..3)
+__device__ __forceinline__ uint32_t leb_pack4(uint32_t x) {
+    return (x & 0x7Fu) | ((x >> 1) & 0x3F80u) | ((x >> 2) & 0x1FC000u) | ((x >> 3) & 0x0FE00000u);
+}
+
 // LEB128 of at most 8 bytes at the bottom of x: returns the byte count (0 if longer than 8)
 __device__ __forceinline__ uint32_t varint8(uint64_t x, uint64_t& v) {
     const uint64_t stop = ~x & 0x8080808080808080ull;
-    if (!stop) return 0;
-    const uint32_t nb = (__builtin_ctzll(stop) >> 3) + 1;
-    const uint64_t m = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
-    const uint64_t y = x & m;
-    uint64_t r = 0;
-#pragma unroll
-    for (uint32_t g = 0; g < 8; g++) r |= ((y >> (8 * g)) & 0x7F) << (7 * g);
-    v = r;
+    const uint32_t nb = stop ? (__builtin_ctzll(stop) >> 3) + 1 : 0u;
+    const uint64_t y = x & (nb >= 8 || nb == 0 ? ~0ull : ((1ull << (8 * nb)) - 1));
+    // two 32-bit halves of 28 payload bits each (the 64-bit group loop cost ~45 VALU per call)
+    const uint32_t lo = leb_pack4((uint32_t)y), hi = leb_pack4((uint32_t)(y >> 32));
+    v = ((uint64_t)hi << 28) | lo;
     return nb;
 }
 
@@ -505,6 +507,32 @@ __device__ __forceinline__ T wave_excl_scan(T v, uint32_t lane) {
     return x - v;
 }
 
+// Wave-wide inclusive sum on DPP (row shifts within 16-lane rows, then row broadcasts 15 / 31):
+// VALU latency instead of the LDS round trips of __shfl_up
+__device__ __forceinline__ uint32_t wave_incl_sum32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+
+// exclusive prefix of 64-bit values and the wave total: 32-bit DPP when every value is below 2^26
+// (64 of them sum below 2^32), else the shuffle scan
+__device__ __forceinline__ uint64_t wave_excl_scan64(uint64_t v, uint32_t lane, uint64_t& total) {
+    if (__all(v < (1ull << 26))) {
+        const uint32_t x = wave_incl_sum32((uint32_t)v);
+        total = lane63(x);
+        return x - (uint32_t)v;
+    }
+    const uint64_t e = wave_excl_scan(v, lane);
+    total = __shfl(e + v, 63);
+    return e;
+}
+
 // Cooperative chunk walk: one wave per chunk, processed in windows of up to 64 candidates.
 //   1. fill: the wave reads 4 KiB at a time (four 1 KiB coalesced blocks, loads in flight
 //      together) and compacts the positions of the canonical magic bytes 91 8d 4c (find_entry's
@@ -535,6 +563,13 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 __device__ __forceinline__ uint32_t lane_ffs(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+
+// lane k's value for a wave-uniform k < 64: v_readlane into scalars (no LDS round trip of __shfl)
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t k) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
+    return ((uint64_t)hi << 32) | lo;
+}
 
 // exact per-byte equality with a byte value: bit 7 of every byte of the result = (byte == v)
 __device__ __forceinline__ uint32_t bytes_eq(uint32_t d, uint32_t v4) {
@@ -568,11 +603,12 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
     return mask;
 }
 
-// minimum waves per SIMD for k_walk (0 = the compiler's choice): 6 spills 60 B to scratch
-// but hides more latency: walk 0.210 -> 0.185 ms on C2, 0.378 -> 0.359 on C3 (5 waves: 97 VGPRs; 8 waves: 132 B
-// of scratch, slower)
+// minimum waves per SIMD for k_walk (0 = the compiler's choice, 4 waves). Round 1: 6 waves with 60 B
+// spilled to scratch beat 5 (walk 0.210 -> 0.185 ms on C2). With the packed DPP fill scans and the
+// 32-bit LEB128 packing the spills landed in the fill loop: 6 waves 0.413 ms on C3, 5 waves (96
+// VGPRs, no scratch) 0.300 ms, against 0.363 before (C2 0.183 -> 0.164 ms)
 #ifndef RIO_WALK_OCC
-#define RIO_WALK_OCC 6
+#define RIO_WALK_OCC 5
 #endif
 #if RIO_WALK_OCC
 __global__ void __launch_bounds__(64 * kWalkWaves, RIO_WALK_OCC) k_walk(FrameParams P) {
@@ -618,17 +654,32 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
                     tail[j] = *reinterpret_cast<const uint32_t*>(f + q + 16);
                 }
             }
+            uint32_t masks[4];
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
                 const uint64_t q = rd + 1024 * j + 16 * lane;
-                uint32_t mask = 0;
+                masks[j] = 0;
                 if (q < ce) {
                     const uint32_t d[5] = {blk[j].x, blk[j].y, blk[j].z, blk[j].w, tail[j]};
-                    mask = magic_mask(d, q, ws, ce, P.len);
+                    masks[j] = magic_mask(d, q, ws, ce, P.len);
                 }
-                const uint32_t cnt = __popc(mask);
-                const uint32_t excl = wave_excl_scan(cnt, lane);
-                uint32_t k = total + excl;
+            }
+            // list slots of the four blocks' candidates (file order: block j, then lane) from two
+            // packed DPP scans (16-bit fields: a block holds at most 1024 candidates)
+            const uint32_t c01 = __popc(masks[0]) | (__popc(masks[1]) << 16);
+            const uint32_t c23 = __popc(masks[2]) | (__popc(masks[3]) << 16);
+            const uint32_t i01 = wave_incl_sum32(c01), i23 = wave_incl_sum32(c23);
+            const uint32_t t01 = lane63(i01), t23 = lane63(i23);
+            const uint32_t e01 = i01 - c01, e23 = i23 - c23;
+            const uint32_t T0 = t01 & 0xFFFFu, T1 = t01 >> 16, T2 = t23 & 0xFFFFu;
+            const uint32_t kb[4] = {total + (e01 & 0xFFFFu), total + T0 + (e01 >> 16), total + T0 + T1 + (e23 & 0xFFFFu),
+                                    total + T0 + T1 + T2 + (e23 >> 16)};
+            total += T0 + T1 + T2 + (t23 >> 16);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint64_t q = rd + 1024 * j + 16 * lane;
+                uint32_t mask = masks[j];
+                uint32_t k = kb[j];
                 while (mask) {
                     const uint32_t i = __ffs(mask) - 1;
                     mask &= mask - 1;
@@ -638,7 +689,6 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
                         L.overflow = q + i;
                     k++;
                 }
-                total += __shfl(excl + cnt, 63);
             }
             rd += 4096;
         }
@@ -661,7 +711,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         if (mode == 0) {
             const uint32_t k = lane_ffs(ok_mask);
             if (k < 64) {
-                p = __shfl(cpos, k);
+                p = readlane64(cpos, k);
                 mode = 1;
             }
             entry = p;
@@ -670,7 +720,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         while (mode == 1 && p < we) {
             // the candidate at p, if listed and framed
             const uint32_t e0 = lane_ffs(__ballot(have && cpos >= p));
-            if (e0 >= nst || __shfl(cpos, e0) != p || !((ok_mask >> e0) & 1)) {
+            if (e0 >= nst || readlane64(cpos, e0) != p || !((ok_mask >> e0) & 1)) {
                 mode = 2;  // serial takeover at p
                 break;
             }
@@ -684,7 +734,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
             const uint32_t last = bok ? b : b - 1;  // b > e0 when !bok (e0 frames)
             if (lane >= e0 && lane <= last) slot = (uint32_t)count + (lane - e0);
             count += last - e0 + 1;
-            p = bok ? __shfl(nx, b) : __shfl(cpos, b);
+            p = bok ? readlane64(nx, b) : readlane64(cpos, b);
         }
         // 4. scratch slots of the chained candidates + their decoded bytes
         const uint64_t mylen = slot != ~0u ? ol : 0;
@@ -693,7 +743,9 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
             sl[slot] = ol | lf | (h.nil ? kNilBit : 0);
             sp[slot] = pd;
         }
-        bytes += __shfl(wave_excl_scan(mylen, lane) + mylen, 63);
+        uint64_t wsum;
+        wave_excl_scan64(mylen, lane, wsum);
+        bytes += wsum;
         wave_sync_lds();
         ws = we;
     }
@@ -995,7 +1047,8 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
         const uint64_t k = k0 + lane;
         const bool v = k < pl.owned;
         const uint64_t l = v ? sl[k] : 0, len = l & kLenMask;
-        const uint64_t excl = wave_excl_scan(len, lane);
+        uint64_t wsum;
+        const uint64_t excl = wave_excl_scan64(len, lane, wsum);
         if (v) {
             const uint64_t i = pl.base_idx + k;
             const uint64_t ro = so[k], pay = sp[k], start = ro + (pay & 0xFF), slen = pay >> 8;
@@ -1015,7 +1068,7 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
             // (what golang/snappy emits for incompressible input) decodes as a copy
             if (snappy && fl == 0) mixed |= !snappy_single_literal(P.file + start, slen, len);
         }
-        carry += __shfl(excl + len, 63);
+        carry += wsum;
     }
     // every writer stores the same 1: a plain store, not an atomic (17 k same-address atomics from
     // the chunk waves of a 1 M-record file serialized at L2 and cost 0.35 ms)

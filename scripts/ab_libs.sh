@@ -9,6 +9,6 @@ for r in $(seq 1 $R); do
     out=$(timeout -k 10 180 python bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline --no-e2e 2>&1 | grep '^{')
     rc=$?
     if [ $rc -ne 0 ]; then echo "$lib failed"; exit 1; fi
-    echo "$lib $(echo "$out" | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['stages_ms']['decode'], d['value'])")"
+    echo "$lib $(echo "$out" | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['stages_ms'], d['value'])")"
   done
 done
