@@ -71,6 +71,10 @@ def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    # rehearsal of the N-rank path on a one-GPU box: every rank decodes on device 0 (never set by the
+    # driver's scaling runs, where rank i owns GPU i)
+    if os.environ.get("RIO_BENCH_ONE_DEVICE") == "1":
+        local = 0
     return ws, rank, local
 
 
