@@ -1040,18 +1040,32 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint64_t* sl = P.scratch_len + c * P.slots;
     const uint64_t* sp = P.scratch_pay + c * P.slots;
     // once any wave has found a mixed record the file takes k_snappy_pipe: later waves skip the probe
-    const bool snappy = st->compression == RIO_COMP_SNAPPY && !*(volatile const uint32_t*)&st->any_mixed;
+    // (and within a wave: the probe stops once one of its lanes has found a mixed record)
+    bool snappy = st->compression == RIO_COMP_SNAPPY && !*(volatile const uint32_t*)&st->any_mixed;
     bool mixed = false;
     uint64_t carry = pl.base_bytes;
+    // scratch of the next 64 records loaded before this step's stores: on CDNA vmcnt retires loads
+    // and stores in issue order, so a load issued after the stores would wait for them
+    uint64_t l_n = 0, ro_n = 0, pay_n = 0;
+    if (lane < pl.owned) {
+        l_n = sl[lane];
+        ro_n = so[lane];
+        pay_n = sp[lane];
+    }
     for (uint64_t k0 = 0; k0 < pl.owned; k0 += 64) {
         const uint64_t k = k0 + lane;
         const bool v = k < pl.owned;
-        const uint64_t l = v ? sl[k] : 0, len = l & kLenMask;
+        const uint64_t l = l_n, ro = ro_n, pay = pay_n, len = v ? l & kLenMask : 0;
+        if (k + 64 < pl.owned) {
+            l_n = sl[k + 64];
+            ro_n = so[k + 64];
+            pay_n = sp[k + 64];
+        }
         uint64_t wsum;
         const uint64_t excl = wave_excl_scan64(len, lane, wsum);
         if (v) {
             const uint64_t i = pl.base_idx + k;
-            const uint64_t ro = so[k], pay = sp[k], start = ro + (pay & 0xFF), slen = pay >> 8;
+            const uint64_t start = ro + (pay & 0xFF), slen = pay >> 8;
             P.rec_off[i] = ro;
             P.rec_pay[i] = pay;
             P.out_off[i] = carry + excl;
@@ -1069,10 +1083,12 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
             if (snappy && fl == 0) mixed |= !snappy_single_literal(P.file + start, slen, len);
         }
         carry += wsum;
+        snappy = snappy && !__any(mixed);
+        mixed = mixed || !snappy;  // keep the wave's verdict for the store below
     }
     // every writer stores the same 1: a plain store, not an atomic (17 k same-address atomics from
     // the chunk waves of a 1 M-record file serialized at L2 and cost 0.35 ms)
-    if (snappy && __any(mixed) && lane == 0) P.state->any_mixed = 1u;
+    if (st->compression == RIO_COMP_SNAPPY && __any(mixed) && lane == 0) P.state->any_mixed = 1u;
 }
 
 __global__ void __launch_bounds__(256) k_zero(FrameParams P) {
