@@ -131,7 +131,7 @@ __device__ __forceinline__ int parse_header(const uint8_t* f, uint64_t p, uint64
 }
 
 // ---- register-window header parse (fast path) --------------------------------------------
-// 8 bytes starting at byte k (0..24) of a 32-byte window held in 8 dwords
+// 8 bytes starting at byte k (0..23: dwords j .. j + 2 with j <= 5) of a 32-byte window held in 8 dwords
 __device__ __forceinline__ uint64_t win8(const uint32_t (&w)[8], uint32_t k) {
     const uint32_t j = k >> 2, r = 8 * (k & 3);
     uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
@@ -255,7 +255,7 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
                 const uint64_t avail = len - p - hl;
                 uint64_t dl = plen;
                 uint32_t k = 0;
-                if (!nil && comp == RIO_COMP_SNAPPY && hl <= 24) {
+                if (!nil && comp == RIO_COMP_SNAPPY && hl <= 20) {  // win8 covers k <= 20 with 8 bytes inside the window
                     k = varint8(win8(w, hl), dl);
                     ok = k && k <= plen && dl <= 0xFFFFFFFFull && dl <= 22ull * (plen - k) + 64;
                 } else if (!nil && comp == RIO_COMP_LZW) {

@@ -130,6 +130,21 @@ def cases():
     h = header_v4(len(pay), 0, magic=b"\x91\x8d\xcc\x00", u_bytes=padded_uvarint(len(pay), 3))
     body = encode_file([asc(100)] * 60, 0)
     out.append(("noncanonical_magic", body + h + pay + encode_file([b"after"] * 50, 0)[8:]))
+    # snappy records whose padded header varints put the payload's preamble 20..25 bytes into the
+    # record (the device's 32-byte header window: the preamble fast path ends at 20)
+    from recordio import _lib as L
+    import ctypes
+
+    raw = b"long-header-record " * 6
+    cap = int(L.lib().rio_snappy_max_encoded_len(len(raw)))
+    sbuf = ctypes.create_string_buffer(cap + 1)
+    spay = sbuf.raw[: L.lib().rio_snappy_encode(sbuf, cap, ctypes.c_char_p(raw), len(raw))]
+    sbody = encode_file([asc(100)] * 40, 2)
+    for target in range(20, 26):
+        nc = target - 9 - 8  # hl = 4 + nu (8) + nc + ncrc (5)
+        pre = b"\x91\x8d\x4c\x00" + padded_uvarint(len(raw), 8) + padded_uvarint(len(spay), nc)
+        hdr = pre + padded_uvarint(crc32c(pre), 5)
+        out.append((f"snappy_padded_header_hl{target}", sbody + hdr + spay + encode_file([b"after"] * 30, 2)[8:]))
     # header longer than the 36-byte checksum cache
     long_pre = padded_uvarint(0x130691, 10) + b"\x00" + padded_uvarint(1, 10) + padded_uvarint(0, 10)
     long_h = long_pre + padded_uvarint(crc32c(long_pre), 6)
