@@ -548,8 +548,14 @@ __device__ __forceinline__ uint64_t wave_excl_scan64(uint64_t v, uint32_t lane, 
 // Result and slots are identical to find_entry + walk_chunk (the serial thread-per-chunk walk,
 // which paid ~50 dependent global round trips per 4 KiB chunk).
 constexpr uint32_t kWalkWaves = 4;      // chunks per workgroup
-constexpr uint32_t kWalkFill = 48;      // stop filling a window at this many candidates
-constexpr uint32_t kWalkFillMax = 4;    // ... or after this many 4 KiB fill rounds
+#ifndef RIO_WALK_FILL
+#define RIO_WALK_FILL 56
+#endif
+#ifndef RIO_WALK_FILL_MAX
+#define RIO_WALK_FILL_MAX 8
+#endif
+constexpr uint32_t kWalkFill = RIO_WALK_FILL;         // stop filling a window at this many candidates
+constexpr uint32_t kWalkFillMax = RIO_WALK_FILL_MAX;  // ... or after this many 4 KiB fill rounds
 
 struct WalkLds {
     uint64_t pos[64];
@@ -643,7 +649,11 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         if (lane == 0) L.overflow = kNone;
         uint32_t total = 0;
         uint64_t rd = ws & ~15ull;  // next 16-B aligned read position
-        for (uint32_t r = 0; r < kWalkFillMax && rd < ce && total < kWalkFill && total <= 64; r++) {
+        // a round that lists no new candidate after some were found ends the fill (long records: the
+        // rest of the window would be payload the chain jumps over)
+        uint32_t added = 1;
+        for (uint32_t r = 0; r < kWalkFillMax && rd < ce && total < kWalkFill && total <= 64 && (total == 0 || added);
+             r++) {
             uint4 blk[4];
             uint32_t tail[4];
 #pragma unroll
@@ -674,7 +684,8 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
             const uint32_t T0 = t01 & 0xFFFFu, T1 = t01 >> 16, T2 = t23 & 0xFFFFu;
             const uint32_t kb[4] = {total + (e01 & 0xFFFFu), total + T0 + (e01 >> 16), total + T0 + T1 + (e23 & 0xFFFFu),
                                     total + T0 + T1 + T2 + (e23 >> 16)};
-            total += T0 + T1 + T2 + (t23 >> 16);
+            added = T0 + T1 + T2 + (t23 >> 16);
+            total += added;
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
                 const uint64_t q = rd + 1024 * j + 16 * lane;
