@@ -300,7 +300,7 @@ def run_sstable(args, world, rank, local, device):
     import torch
 
     from recordio import _lib as L
-    from recordio.device import DeviceDecoder, to_device_file
+    from recordio.device import DeviceDecoder, header_codec, to_device_file
 
     n = CONFIGS["c5"][0]
     mine = shard_files(SST_TABLES, world, rank)
@@ -317,8 +317,10 @@ def run_sstable(args, world, rank, local, device):
         T = {"index_img": index_img, "data_img": data_img}
         T["d_index"], T["li"] = to_device_file(index_img, local)
         T["d_data"], T["ld"] = to_device_file(data_img, local)
-        T["ib"], ii = dec.decode(T["d_index"], T["li"])
-        T["db"], di = dec.decode(T["d_data"], T["ld"])
+        # the files' header codecs as decode hints: only those codecs' kernels are launched
+        T["ci"], T["cd"] = header_codec(index_img), header_codec(data_img)
+        T["ib"], ii = dec.decode(T["d_index"], T["li"], comp=T["ci"])
+        T["db"], di = dec.decode(T["d_data"], T["ld"], comp=T["cd"])
         if ii["n_records"] != n or di["n_records"] != n:
             raise RuntimeError(f"sstable decode failed: {ii} {di}")
         T["nb_d"] = di["total_out_bytes"]
@@ -332,13 +334,13 @@ def run_sstable(args, world, rank, local, device):
         for T in tables:
             marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if ev is not None else None
             if marks: marks[0].record(stream)
-            dec.launch(T["d_index"], T["li"], T["ib"], stream)
+            dec.launch(T["d_index"], T["li"], T["ib"], stream, T["ci"])
             if marks: marks[1].record(stream)
             lib.rio_sst_index_parse(dec.ctx, T["ib"].out.data_ptr(), T["ib"].out_off.data_ptr(), n,
                                     T["key_off"].data_ptr(), T["key_len"].data_ptr(), T["value_off"].data_ptr(),
                                     T["checksum"].data_ptr(), T["pres"].data_ptr(), sp)
             if marks: marks[2].record(stream)
-            dec.launch(T["d_data"], T["ld"], T["db"], stream)
+            dec.launch(T["d_data"], T["ld"], T["db"], stream, T["cd"])
             if marks: marks[3].record(stream)
             lib.rio_sst_validate(dec.ctx, T["db"].out.data_ptr(), T["db"].out_off.data_ptr(),
                                  T["db"].rec_off.data_ptr(), n, T["value_off"].data_ptr(), T["checksum"].data_ptr(), n,

@@ -42,6 +42,17 @@ def to_device_file(image, device: int = 0) -> tuple[torch.Tensor, int]:
     return t, n
 
 
+def header_codec(img) -> int | None:
+    """The compression type in a file image's 8-byte header (readFileHeaderFromBuffer,
+    common_reader.go:22-44: version, then the compression type from version 2 on), as the decode's
+    codec hint; None when the header is short, older or names no codec the device decodes."""
+    if len(img) < 8:
+        return None
+    version = int.from_bytes(bytes(img[0:4]), "little")
+    comp = int.from_bytes(bytes(img[4:8]), "little")
+    return comp if version >= 2 and comp <= 3 else None
+
+
 class DeviceDecoder:
     def __init__(self, device: int = 0):
         self.device = device

@@ -98,7 +98,7 @@ class _DeviceTable:
     def __init__(self, base: str, device: int, need_crc: bool):
         import torch
 
-        from recordio.device import DeviceDecoder, to_device_file
+        from recordio.device import DeviceDecoder, header_codec, to_device_file
 
         self.dec = DeviceDecoder(device)
         dev = f"cuda:{device}"
@@ -108,7 +108,8 @@ class _DeviceTable:
             with open(os.path.join(base, name), "rb") as fh:
                 img = fh.read()
             d, n = to_device_file(img, device)
-            b, info = self.dec.decode(d, n)
+            # the header's codec: only that codec's kernels are launched
+            b, info = self.dec.decode(d, n, comp=header_codec(img))
             return img, b, info
 
         self.index_img, self.ib, ii = decode(IndexFileName)
