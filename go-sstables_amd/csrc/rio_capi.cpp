@@ -282,6 +282,8 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     return RIO_OK;
 }
 
+extern "C" int rio_ctx_device(const rio_ctx* c) { return c ? c->device : -1; }
+
 extern "C" void rio_ctx_destroy(rio_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
@@ -568,6 +570,9 @@ static int h2d_fill(rio_ctx* c, void* dst, uint64_t n, rio::FillFn fill, void* u
 static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const uint8_t* file, rio::FillFn fill,
                         void* user) {
     HIP_TRY(hipSetDevice(ctx->device));
+    // the host API shares the ctx arenas with the device API: wait for a device-API call still
+    // running on another stream, and make the next device-API call wait for this one
+    if (int rc = order_before(ctx, ctx->stream)) return rc;
     ctx->framed = false;
     HIP_TRY(ctx->file.ensure(len + RIO_DEVICE_PAD));
     int rc = fill ? h2d_fill(ctx, ctx->file.p, len, fill, user) : h2d_staged(ctx, ctx->file.p, file, len);
@@ -627,7 +632,7 @@ static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const u
     ctx->last = P;
     ctx->framed = true;
     ctx->file_len = len;
-    return RIO_OK;
+    return order_after(ctx, ctx->stream);
 }
 
 extern "C" int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_file_info* info) {
@@ -655,6 +660,7 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
     }
     const uint64_t n = fi.n_records, nb = fi.total_out_bytes;
     if (rec_cap < n || out_cap < nb || (n && (!out_off || !rec_off || !flags)) || (nb && !out)) return RIO_ERR_CAPACITY;
+    if (int rc = order_before(ctx, ctx->stream)) return rc;
     if (ctx->predecoded) {  // gzip: rio_frame decoded the file (its sizes are the decoded ones)
         const FrameParams& P = ctx->last;
         int rc;
@@ -665,7 +671,7 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
             if ((rc = d2h_staged(ctx, flags, P.flags, n))) return rc;
         }
         *info = fi;
-        return RIO_OK;
+        return order_after(ctx, ctx->stream);
     }
     HIP_TRY(ctx->out.ensure(nb + 16));
     HIP_TRY(ctx->out_off.ensure((n + 1) * 8));
@@ -696,7 +702,7 @@ extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t
         if ((rc = d2h_staged(ctx, flags, P.flags, fin.n_records))) return rc;
     }
     *info = fin;
-    return RIO_OK;
+    return order_after(ctx, ctx->stream);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1048,8 +1054,10 @@ extern "C" int rio_reader_skip_next(rio_reader* r) {
     const int s = terminal(r);
     switch (s) {
     case RIO_EOF_ZERO_TAIL: return RIO_ERR_MAGIC;  // SkipNext does not test for a zero tail
-    case RIO_EOF_PAYLOAD:
-    case RIO_ERR_UNEXPECTED_EOF:  // header parsed fine: SkipNext seeks past the payload
+    case RIO_ERR_UNEXPECTED_EOF:  // detail0 == 1: raised by the payload read, else inside a header varint
+        if (r->info.detail0 != 1) return s;
+        [[fallthrough]];
+    case RIO_EOF_PAYLOAD:  // header parsed fine: SkipNext seeks past the payload
         r->past_end = true;
         return RIO_OK;
     default: return s;
@@ -1064,16 +1072,31 @@ extern "C" int rio_reader_skip_next(rio_reader* r) {
 // bytes) runs the single-record kernels (k_read_at / k_seek_next) under the reader's lock, exactly
 // as before; for gzip files those kernels locate the record and the host serves the payload from the
 // index when the offset is a record start.
+// Largest decoded size (and record count) the index is built for: a file past it keeps n = 0 and
+// every ReadNextAt / SeekNext takes the single-record kernels (no whole-file host copy, no
+// first-call decode of a huge file). The framing's sizes are what the records claim, so a damaged
+// header cannot make this allocate more than the cap. RIO_READAT_INDEX_MAX overrides (bytes).
+static uint64_t readat_index_cap() {
+    static const uint64_t cap = env_u64("RIO_READAT_INDEX_MAX", 4ull << 30);
+    return cap;
+}
+
 static void build_readat_index(rio_reader* r, ReadAtIndex& x) {
     rio_ctx* ctx = r->ctx;
     std::lock_guard<std::mutex> cg(ctx->mu);
     rio_file_info fi{};
     if (rio_frame(ctx, r->map, r->size, &fi) != RIO_OK) return;
     const uint64_t n0 = fi.n_records;
-    x.out.assign(fi.total_out_bytes + 1, 0);
-    x.out_off.assign(n0 + 1, 0);
-    x.rec_off.assign(n0 + 1, 0);
-    x.flags.assign(n0 + 1, 0);
+    if (fi.total_out_bytes > readat_index_cap() || n0 > readat_index_cap() / 16) return;
+    try {
+        x.out.assign(fi.total_out_bytes + 1, 0);
+        x.out_off.assign(n0 + 1, 0);
+        x.rec_off.assign(n0 + 1, 0);
+        x.flags.assign(n0 + 1, 0);
+    } catch (const std::bad_alloc&) {  // never through the C-ABI: the kernels answer instead
+        x = ReadAtIndex{};
+        return;
+    }
     if (rio_decode(ctx, x.out.data(), fi.total_out_bytes, x.out_off.data(), x.rec_off.data(), x.flags.data(), n0, &fi) !=
         RIO_OK)
         return;
@@ -1166,8 +1189,10 @@ extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* re
     const uint64_t seek_len = r->seek_len.load(std::memory_order_relaxed);
     const ReadAtIndex* x = readat_index(r);
     uint64_t s = offset;  // the scan's position: a fresh SeekNext from s continues it exactly
-    // with windows of >= 3 bytes the walk is fixed by the first 0x91 at or after s (build_seek_map)
-    if (seek_len >= 3 && s <= r->size && x->n) {
+    // with windows of >= 4 bytes the walk is fixed by the first 0x91 at or after s (build_seek_map).
+    // Not at 3: mmap_reader.go:89-98 leaves the window once ix >= numRead, also right after the third
+    // marker byte, so with seekLen 3 every marker ends the scan in io.EOF (k_seek_next reproduces it)
+    if (seek_len >= 4 && s <= r->size && x->n) {
         const uint64_t k = (uint64_t)(std::lower_bound(x->P.begin(), x->P.end(), s) - x->P.begin());
         if (k < x->P.size() && x->R[k] != kSeekOther) {
             const uint64_t i = x->R[k];
@@ -1267,12 +1292,18 @@ extern "C" int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t in
     HIP_TRY(hipSetDevice(ctx->device));
     auto* t = new rio_sst();
     rio_sst_info& I = t->info;
-    I.first_bad_proto = I.first_bad_crc = I.first_unplaced = ~0ull;
+    I.first_bad_proto = I.first_bad_crc = I.first_unplaced = I.index_bad = ~0ull;
     int rc = sst_decode_host(ctx, index_file, index_len, t->index, t->index_off, t->index_rec_off, t->index_flags, I.index);
     uint64_t n = 0;
     if (!rc && !sst_header_level(I.index.status) && I.index.status != RIO_ERR_UNSUPPORTED) {
         // the index arena is on the device (ctx->out / ctx->out_off): parse it there
         n = I.index.n_records;
+        // an index record that does not decompress ends Load's ReadNext loop (slice_key_index.go:
+        // 117-126): ErrCorrupt fails the load there, gzip's bare io.EOF ends the index cleanly
+        if (I.index.n_bad && I.index.first_bad < n) {
+            if (t->index_flags[I.index.first_bad] & RIO_FLAG_CORRUPT) I.index_bad = I.index.first_bad;
+            n = I.index.first_bad;
+        }
         const uint64_t nn = std::max<uint64_t>(n, 1);
         if (ctx->sst_fields.ensure(nn * 32) || ctx->sst_crc.ensure(nn * 8) || ctx->sst_res.ensure(32)) rc = RIO_ERR_HIP;
         uint64_t* f = ctx->sst_fields.as<uint64_t>();

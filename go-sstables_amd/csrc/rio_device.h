@@ -13,7 +13,7 @@ constexpr uint64_t kNilBit = 1ull << 63;  // nil record
 constexpr uint64_t kBadBit = 1ull << 62;  // payload fails already at framing (codec preamble / size)
 constexpr uint64_t kEofBit = 1ull << 61;  // gzip: empty payload (gzip.NewReader's io.EOF)
 constexpr uint64_t kLenMask = kEofBit - 1;
-// lanes of the Snappy lane decoder that met a corrupt record are listed for k_snappy_verify
+// lanes of the Snappy lane decoder that met a corrupt record are listed for k_finish (re-checked there)
 constexpr uint32_t kFailLanes = 1024;
 
 // Snappy decode launch shape (k_snappy_pipe): every wave owns one 64-byte sink line that absorbs
@@ -77,7 +77,7 @@ struct ScanState {
     uint64_t unsupported_rec;  // first record the device path hands back (absurd gzip sizes)
     uint32_t n_fail_lanes;     // Snappy lane-decoder lanes listed in fail_lanes (> kFailLanes: all)
     uint32_t capacity_fail;
-    uint32_t huge_streams;  // a record stream exceeds 32-bit positions: k_snappy_global runs
+    uint32_t huge_streams;  // a record stream exceeds 32-bit positions: the wave decoder (coop_file) runs, one thread per record
     uint32_t any_mixed;     // snappy: some record is not one literal covering its output (k_place);
                             // 0 => every record is copied by k_copy_records instead of k_snappy_pipe
     uint32_t scan_ticket;   // k_scan_blocks: the last block to finish runs the top-level scan

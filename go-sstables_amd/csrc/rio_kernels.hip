@@ -1422,7 +1422,7 @@ __global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64
 // visits positions from its offset one by one; only a 0x91 byte changes the walk: 91 X (X != 8d)
 // jumps to p+2, 91 8d Y (Y != 4c) to p+3, and a marker 91 8d 4c runs a trial ReadNextAt whose
 // io.EOF / magic / header-CRC class continues at p+3 while anything else ends the call. With windows
-// of >= 3 bytes the walk does not depend on where windows start (a marker cut by a window end is
+// of >= 4 bytes the walk does not depend on where windows start (a marker cut by a window end is
 // re-read from its start). So the answer from offset s is fixed by the first 0x91 at or after s:
 // P = every 0x91 position in file order, R[k] = the walk's end from P[k] — a record j of the decoded
 // sequence (its trial is record j, answered from the decoded arena) or kSeekOther (a trial outside

@@ -258,7 +258,7 @@ int decode_file(rio_ctx* ctx, const std::string& path, Decoded& d) {
 struct rio_replay {
     std::vector<std::string> paths;
     uint32_t depth = 2;
-    int device = 0;
+    std::vector<int> devs;       // worker w's device
     std::vector<rio_ctx*> ctxs;  // one per worker (from CtxPool): own stream, arenas and pinned staging
     std::vector<std::thread> workers;
     std::mutex mu;
@@ -289,26 +289,38 @@ struct rio_replay {
 
 extern "C" int rio_replay_open(int device, const char* const* paths, uint64_t n_paths, uint32_t depth,
                                uint32_t workers, rio_replay** out) {
-    if (!out || (n_paths && !paths)) return RIO_ERR_ARG;
+    return rio_replay_open_devices(&device, 1, paths, n_paths, depth, workers, out);
+}
+
+// Workers are dealt to the devices round-robin (worker w on devices[w % n_devices]), each with a
+// pooled context of its device; file i goes to worker i % W as before, so consecutive files decode
+// on different GPUs and the ordered hand-out interleaves them (one host thread and
+// context per GPU, no communication between them).
+extern "C" int rio_replay_open_devices(const int* devices, uint32_t n_devices, const char* const* paths,
+                                       uint64_t n_paths, uint32_t depth, uint32_t workers_per_device,
+                                       rio_replay** out) {
+    if (!out || !devices || !n_devices || (n_paths && !paths)) return RIO_ERR_ARG;
     *out = nullptr;
     for (uint64_t i = 0; i < n_paths; i++)
         if (!paths[i]) return RIO_ERR_ARG;
     auto* r = new rio_replay();
-    r->device = device;
     r->paths.assign(paths, paths + n_paths);
-    r->depth = depth ? depth : 2;
-    uint32_t W = workers ? workers : 2;
-    W = std::min<uint32_t>(W, r->depth);
+    const uint32_t per = workers_per_device ? workers_per_device : 2;
+    uint32_t W = per * n_devices;
+    // at least one file in flight per worker, never fewer than the caller's depth
+    r->depth = std::max<uint32_t>(depth ? depth : 2, W);
     W = (uint32_t)std::min<uint64_t>(W, std::max<uint64_t>(n_paths, 1));
     for (uint32_t w = 0; w < W; w++) {
+        const int dev = devices[w % n_devices];
         rio_ctx* c = nullptr;
-        int rc = CtxPool::get().take(device, &c);
+        int rc = CtxPool::get().take(dev, &c);
         if (rc) {
-            for (rio_ctx* x : r->ctxs) CtxPool::get().give(device, x);
+            for (size_t x = 0; x < r->ctxs.size(); x++) CtxPool::get().give(r->devs[x], r->ctxs[x]);
             delete r;
             return rc;
         }
         r->ctxs.push_back(c);
+        r->devs.push_back(dev);
     }
     for (uint32_t w = 0; w < W; w++) r->workers.emplace_back([r, w, W] { r->run(w, W); });
     *out = r;
@@ -346,9 +358,100 @@ extern "C" void rio_replay_free(rio_replay* r) {
     }
     for (auto& t : r->workers)
         if (t.joinable()) t.join();
-    for (rio_ctx* c : r->ctxs) CtxPool::get().give(r->device, c);
+    for (size_t x = 0; x < r->ctxs.size(); x++) CtxPool::get().give(r->devs[x], r->ctxs[x]);
     delete r;
 }
+
+// ---- pooled contexts for per-file readers (the Go adapter's Open / Close) ---------------------
+extern "C" int rio_ctx_acquire(int device, rio_ctx** out) {
+    if (!out) return RIO_ERR_ARG;
+    *out = nullptr;
+    return CtxPool::get().take(device, out);
+}
+
+extern "C" void rio_ctx_release(rio_ctx* ctx) {
+    if (ctx) CtxPool::get().give(rio_ctx_device(ctx), ctx);
+}
+
+// ---- a file set decoded over several devices (rio_fileset_*) ----------------------------------
+// One host thread per device, each with a pooled context of its device; files are assigned by
+// longest-processing-time first on their sizes (LPT over GPUs, round-robin for equal
+// sizes), and a thread decodes its files in that order into page-locked blocks. No communication
+// between the threads: the files are independent (a WAL directory, the tables of an SSTable set).
+struct rio_fileset {
+    std::vector<std::unique_ptr<Decoded>> files;
+    std::vector<int> device;  // device that decoded file i
+};
+
+extern "C" int rio_fileset_decode(const int* devices, uint32_t n_devices, const char* const* paths, uint64_t n_paths,
+                                  rio_fileset** out) {
+    if (!out || !devices || !n_devices || (n_paths && !paths)) return RIO_ERR_ARG;
+    *out = nullptr;
+    std::vector<uint64_t> size(n_paths, 0);
+    for (uint64_t i = 0; i < n_paths; i++) {
+        if (!paths[i]) return RIO_ERR_ARG;
+        struct stat st;
+        if (stat(paths[i], &st) == 0 && S_ISREG(st.st_mode)) size[i] = (uint64_t)st.st_size;
+    }
+    // LPT: largest file first, each to the device with the least assigned bytes (ties: lowest index)
+    std::vector<uint64_t> order(n_paths);
+    for (uint64_t i = 0; i < n_paths; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return size[a] > size[b]; });
+    std::vector<std::vector<uint64_t>> mine(n_devices);
+    std::vector<uint64_t> load(n_devices, 0);
+    auto* fs = new rio_fileset();
+    fs->files.resize(n_paths);
+    fs->device.assign(n_paths, -1);
+    for (uint64_t i : order) {
+        uint32_t best = 0;
+        for (uint32_t d = 1; d < n_devices; d++)
+            if (load[d] < load[best]) best = d;
+        load[best] += size[i] + 1;
+        mine[best].push_back(i);
+        fs->device[i] = devices[best];
+    }
+    std::atomic<int> fail{RIO_OK};
+    std::vector<std::thread> th;
+    for (uint32_t d = 0; d < n_devices; d++) {
+        if (mine[d].empty()) continue;
+        th.emplace_back([&, d] {
+            rio_ctx* c = nullptr;
+            if (int rc = CtxPool::get().take(devices[d], &c)) {
+                fail = rc;
+                return;
+            }
+            for (uint64_t i : mine[d]) {
+                auto f = std::make_unique<Decoded>();
+                f->index = i;
+                f->rc = decode_file(c, paths[i], *f);
+                fs->files[i] = std::move(f);
+            }
+            CtxPool::get().give(devices[d], c);
+        });
+    }
+    for (auto& t : th) t.join();
+    if (fail.load() != RIO_OK) {
+        delete fs;
+        return fail.load();
+    }
+    *out = fs;
+    return RIO_OK;
+}
+
+extern "C" int rio_fileset_get(const rio_fileset* s, uint64_t i, const uint8_t** out, const uint64_t** out_off,
+                               const uint64_t** rec_off, const uint8_t** flags, rio_file_info* info, int* device) {
+    if (!s || i >= s->files.size() || !s->files[i]) return RIO_ERR_ARG;
+    const Decoded& d = *s->files[i];
+    if (out) *out = d.out;
+    if (out_off) *out_off = d.out_off;
+    if (rec_off) *rec_off = d.rec_off;
+    if (flags) *flags = d.flags;
+    if (info) *info = d.info;
+    if (device) *device = s->device[i];
+    return d.rc;
+}
+
+extern "C" void rio_fileset_free(rio_fileset* s) { delete s; }
 
 // ---- windowed sequential decode of one file (rio_stream_*) ------------------------------------
 //

@@ -37,20 +37,14 @@ namespace rio {
 namespace {
 constexpr uint32_t kOutCh = 16;                  // history ring: 16 chunks = 256 bytes per lane
 constexpr uint32_t kInCh = 4;                    // input ring: 4 chunks = 64 bytes per lane
-constexpr uint32_t kWaveLds = (kOutCh + kInCh) * 64 * 16;  // 20 KiB per wave
-// emitter generation: 9 = every piece through one destination-aligned funnel (below), 8 = the
-// source funnel + placement shifts of round 1 (kept for A/B builds: make variant VDEFS=-DRIO_PIPE=8)
-#ifndef RIO_PIPE
-#define RIO_PIPE 9
-#endif
 constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 // copies reaching further back than kFarOff read the output arena (flushed: see snappy_lane)
-constexpr uint32_t kFarOff = RIO_PIPE >= 9 ? 16 * (kD - 1) + 16 + 128 : kOutCh * 16 - 48;
+constexpr uint32_t kFarOff = 16 * (kD - 1) + 16 + 128;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
 static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128, "far history must be flushed before the parser reads it");
 // v9: a ring copy's source window starts >= 16 * (chunk(d) - kFarOff / 16), and ring chunk chunk(d) + 2
 // (= chunk(d) - 14 mod 16) serves as the staging chunk of literal / far bytes: it must be dead
-static_assert(RIO_PIPE < 9 || (kOutCh == 16 && kFarOff <= 16 * 13), "staging chunk must hold no live history");
+static_assert(kOutCh == 16 && kFarOff <= 16 * 13, "staging chunk must hold no live history");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
 
 // bytes [r, r + 16) of the 32-byte little-endian concatenation (a, b), r in [0, 16): dword
@@ -63,16 +57,6 @@ __device__ __forceinline__ uint4 funnel16(uint4 a, uint4 b, uint32_t r) {
     const uint32_t e0 = h2 ? p2 : p0, e1 = h2 ? p3 : p1, e2 = h2 ? p4 : p2, e3 = h2 ? p5 : p3, e4 = h2 ? p6 : p4;
     return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
                       __builtin_amdgcn_alignbyte(e3, e2, sh), __builtin_amdgcn_alignbyte(e4, e3, sh));
-}
-
-// bytes [sh, sh + 16) of the 32-byte concatenation (w, 0) for sh in [0, 7] (a literal's header
-// length): one select level instead of funnel16's two
-__device__ __forceinline__ uint4 shift_small(uint4 w, uint32_t sh) {
-    const uint32_t b = sh & 3u;
-    const bool h = (sh & 4u) != 0;
-    const uint32_t e0 = h ? w.y : w.x, e1 = h ? w.z : w.y, e2 = h ? w.w : w.z, e3 = h ? 0u : w.w;
-    return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, b), __builtin_amdgcn_alignbyte(e2, e1, b),
-                      __builtin_amdgcn_alignbyte(e3, e2, b), __builtin_amdgcn_alignbyte(0u, e3, b));
 }
 
 // materialize x in a VGPR here: the selects that use it can no longer be turned into branches that
@@ -112,32 +96,12 @@ __device__ __forceinline__ uint4 merge_at(uint4 st, uint4 v, uint32_t r) {
                       (v.w & m3) | (st.w & ~m3));
 }
 
-// place v at byte offset r of a 32-byte window: lo = v << 8r (bytes of the chunk holding the
-// position), hi = v >> 8(16 - r) (bytes spilling into the next chunk)
-__device__ __forceinline__ void place16(uint4 v, uint32_t r, uint4& lo, uint4& hi) {
-    const uint32_t t = (16u - r) & 15u;
-    const uint4 a = funnel16(zero4(), v, t), b = funnel16(v, zero4(), t);
-    lo = sel4(r != 0, a, b);  // r == 0: a = 0, b = v
-    hi = sel4(r != 0, b, a);
-}
-
 // cache policy (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads. Default 1: the
 // arena stores no longer push the lanes' input lines out of L2 between their 16-byte reads (C2
 // decode: HBM reads 4.1 -> 3.4 GB and writes 1.12 -> 1.03 GB per launch, 0.9 % slower, because far
 // copies then miss L2 more often; C4: 3 % faster). 2 and 3 were slower (+5 %, +8 %).
 #ifndef RIO_NT
 #define RIO_NT 1
-#endif
-// timing-only experiment knobs (wrong output): 1 = no out16 funnel, 2 = no place16, 4 = no in16 funnel,
-// 8 = no flush bpermutes of the owner base, 16 = far-history loads to the sink (traffic attribution),
-// 32 = flush stores to the sink
-#ifndef RIO_EXP
-#define RIO_EXP 0
-#endif
-// 1: the next emit's window is read after the flush data (the flush store then waits for its own
-// read only); A/B on MI355X: C2 decode -0.2 %, within noise
-#ifndef RIO_FLUSH_FIRST
-#define RIO_FLUSH_FIRST 1
 #endif
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
@@ -152,14 +116,6 @@ struct LaneLds {
     uint8_t* i;  // wave input-ring image + lane * 16
     __device__ uint4* out(uint32_t pos) const { return reinterpret_cast<uint4*>(h + ((pos >> 4) & (kOutCh - 1)) * 1024); }
     __device__ uint4* in(uint32_t c) const { return reinterpret_cast<uint4*>(i + (c & (kInCh - 1)) * 1024); }
-    // 16 bytes of history at output position q
-    __device__ uint4 out16(uint32_t q) const {
-        return (RIO_EXP & 1) ? *out(q) : funnel16(*out(q), *out(q + 16), q & 15u);
-    }
-    // 16 bytes of input at aligned-frame position pos
-    __device__ uint4 in16(uint32_t pos) const {
-        return (RIO_EXP & 4) ? *in(pos >> 4) : funnel16(*in(pos >> 4), *in((pos >> 4) + 1), pos & 15u);
-    }
 };
 
 // one pipeline slot: a parsed piece plus the two loads issued with it
@@ -263,7 +219,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         const uint32_t pos = s;
 
         // 2. emit the piece parsed kD iterations ago (a bubble appends nothing)
-#if RIO_PIPE >= 9
         // Destination-aligned: a literal's or far copy's 16 bytes are first stored to the dead ring
         // chunk chunk(d) + 2, so every piece is "bytes [w, w + 32) of the ring, w = source - r" with
         // r = d & 15: one funnel over three ring chunks yields the destination chunk and its
@@ -285,27 +240,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             *L.out(cs << 4) = sel4(N.kind == 0, N.lit, N.aux);
             const uint32_t w = (N.kind == 1 ? N.q : (cs << 4) + N.q) - r2;
             wN = w;
-#if !RIO_FLUSH_FIRST
-            wA = *L.out(w);
-            wB = *L.out(w + 16u);
-            wC = *L.out(w + 32u);
-#endif
             wF = w & 15u;
         }
-#else
-        {
-            const uint4 h = L.out16(S.q);
-            const uint4 v = keep_bytes(sel4(S.kind == 0, S.lit, sel4(S.kind == 2, S.aux, h)), S.n);
-            const uint32_t r = d & 15u;
-            uint4 lo, hi;
-            if (RIO_EXP & 2) { lo = v; hi = v; } else place16(v, r, lo, hi);
-            lo = or4(stage, lo);
-            *L.out(d) = lo;       // chunk holding d: staged head + new bytes
-            *L.out(d + 16) = hi;  // next chunk: only bytes not yet final
-            stage = sel4(r + S.n >= 16, hi, lo);
-            d += S.n;
-        }
-#endif
 
         // 3. cooperative flush: lane writes 16 bytes of owner o's next 64-byte block if complete
         {
@@ -314,20 +250,18 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
             const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
             const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
-#if RIO_PIPE >= 9 && RIO_FLUSH_FIRST
             // the next emit's window after the flush data: the store waits for fv only, the window
             // reads stay in flight through the store and the parse
             wA = *L.out(wN);
             wB = *L.out(wN + 16u);
             wC = *L.out(wN + 32u);
-#endif
-            st_out(((ofb >> 31) && !(RIO_EXP & 32)) ? obase[j & 3u] + pos : sink, fv);
+            st_out((ofb >> 31) ? obase[j & 3u] + pos : sink, fv);
             fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
         }
 
         // 4. parse the next piece into this slot (selects only: lanes diverge in data, not flow)
         {
-            const uint4 W = (RIO_EXP & 4) ? Wa : funnel16(Wa, Wb, pos & 15u);  // input bytes [s, s + 16)
+            const uint4 W = funnel16(Wa, Wb, pos & 15u);  // input bytes [s, s + 16)
             // element header at s (golang/snappy decode_other.go tag forms): every form is computed
             // and combined with selects, so divergent tags cost no exec-mask branches
             const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);  // the 4 bytes after the tag
@@ -372,15 +306,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.n = n;
             S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
             qsrc = pd - eff1;
-#if RIO_PIPE >= 9
             // the literal starts sh bytes into W; the emitter's funnel absorbs that shift (S.q = sh),
             // a far copy's bytes sit at the start of the staging chunk (S.q = 0)
             S.q = S.kind == 1 ? qsrc : (S.kind == 0 ? sh : 0u);
             S.lit = W;
-#else
-            S.q = qsrc;
-            S.lit = shift_small(W, sh);
-#endif
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
@@ -388,7 +317,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             islit = lit1;
             // a record that does not decode is not the end of the lane: its remaining input is skipped
             // and the rest of its announced output is filled (16-byte ring pieces of unspecified
-            // bytes), then the next record starts; k_snappy_verify flags it
+            // bytes), then the next record starts; k_finish re-checks the lane and flags it
             s = badn ? s_end : s;
             // record boundary: stream consumed -> the record must be complete; switch to the next
             // (its descriptor landed) or finish the range
@@ -422,7 +351,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const bool want_desc = S.kind != 2 && nds == 0;
             S.desc = want_desc ? 1u : 0u;
             nds = want_desc ? 1u : nds;
-            const uint8_t* ap = S.kind == 2 ? ((RIO_EXP & 16) ? sink : gout + qsrc)
+            const uint8_t* ap = S.kind == 2 ? gout + qsrc
                                             : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
             S.aux = ld_far(ap);
         }

@@ -80,6 +80,7 @@ class SstInfo(ctypes.Structure):
         ("first_bad_proto", c_uint64),
         ("first_bad_crc", c_uint64),
         ("first_unplaced", c_uint64),
+        ("index_bad", c_uint64),
     ]
 
 
@@ -102,6 +103,9 @@ _SIGS = {
     "rio_build_info": (c_char_p, []),
     "rio_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
     "rio_ctx_destroy": (None, [c_void_p]),
+    "rio_ctx_device": (c_int, [c_void_p]),
+    "rio_ctx_acquire": (c_int, [c_int, POINTER(c_void_p)]),
+    "rio_ctx_release": (None, [c_void_p]),
     "rio_device_count": (c_int, [POINTER(c_int)]),
     "rio_frame": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(FileInfo)]),
     "rio_decode": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, POINTER(FileInfo)]),
@@ -168,6 +172,11 @@ _SIGS = {
     "rio_replay_next": (
         c_int, [c_void_p, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(FileInfo)]),
     "rio_replay_free": (None, [c_void_p]),
+    "rio_replay_open_devices": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, c_uint32, c_uint32, POINTER(c_void_p)]),
+    "rio_fileset_decode": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, POINTER(c_void_p)]),
+    "rio_fileset_get": (c_int, [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),
+                                POINTER(c_void_p), POINTER(FileInfo), POINTER(c_int)]),
+    "rio_fileset_free": (None, [c_void_p]),
     "rio_stream_open": (c_int, [c_int, c_char_p, c_uint64, c_uint32, POINTER(c_void_p)]),
     "rio_stream_open_host": (c_int, [c_int, c_void_p, c_uint64, c_uint64, c_uint32, POINTER(c_void_p)]),
     "rio_stream_next": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p),

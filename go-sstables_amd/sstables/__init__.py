@@ -281,7 +281,9 @@ def NewSSTableReader(*options):  # noqa: N802
         t = _DeviceTable(o.basePath, o.device, True)
     except UnsupportedError as e:
         return None, e
-    if t.index_info["status"] not in L.EOF_CLASS:
+    # a flagged index record ends Load's loop before any later terminal status is reached
+    # (slice_key_index.go:117-126: ErrCorrupt returns, gzip's bare io.EOF breaks)
+    if t.index_info["n_bad"] == 0 and t.index_info["status"] not in L.EOF_CLASS:
         return None, GoError(f"error while reading index of sstable in '{o.basePath}': "
                              f"{L.strerror(t.index_info['status'])}")
     if t.index_bad != _NONE and (t.bad_proto == _NONE or t.index_bad <= t.bad_proto):

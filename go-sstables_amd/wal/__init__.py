@@ -64,9 +64,10 @@ def ReaderFactory(factory):  # noqa: N802
     return f
 
 
-def ReplayOnDevice(device: int, depth: int = 2, workers: int = 2):  # noqa: N802
-    """Not in the reference: the GPU, the number of files decoded ahead of `process` and the number
-    of decode workers (each its own stream)."""
+def ReplayOnDevice(device, depth: int = 2, workers: int = 2):  # noqa: N802
+    """Not in the reference: the GPU (or a list of GPUs: workers per device on each, files dealt
+    round-robin, rio_replay_open_devices), the number of files decoded ahead of `process` and the
+    number of decode workers per device (each its own stream)."""
     def f(o):
         o.device, o.depth, o.workers = device, depth, workers
     return f
@@ -147,8 +148,14 @@ class Replayer:
             return None
         arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
         h = ctypes.c_void_p()
-        rc = lib.rio_replay_open(self.walOptions.device, arr, len(paths), self.walOptions.depth,
-                                 self.walOptions.workers, ctypes.byref(h))
+        dev = self.walOptions.device
+        if isinstance(dev, (list, tuple)):
+            devs = (ctypes.c_int * len(dev))(*dev)
+            rc = lib.rio_replay_open_devices(devs, len(dev), arr, len(paths), self.walOptions.depth,
+                                             self.walOptions.workers, ctypes.byref(h))
+        else:
+            rc = lib.rio_replay_open(dev, arr, len(paths), self.walOptions.depth, self.walOptions.workers,
+                                     ctypes.byref(h))
         if rc != L.RIO_OK:
             return GoError(f"error while starting the WAL replay pipeline under '{self.walOptions.basePath}': "
                            f"{L.strerror(rc)}")

@@ -140,6 +140,14 @@ typedef struct rio_ctx rio_ctx;
 int rio_ctx_create(int device, rio_ctx** out);
 void rio_ctx_destroy(rio_ctx* ctx);
 int rio_device_count(int* out);
+int rio_ctx_device(const rio_ctx* ctx); /* the context's device, -1 for NULL */
+/* Pooled contexts for per-file readers (the Go adapter's FileReader.Open / Close,
+ * file_reader.go:26-59): rio_ctx_acquire hands out an idle context of `device` from a process-wide
+ * pool (creating one when none is idle), rio_ctx_release returns it (up to 4 idle per device are
+ * kept, the rest destroyed). A fresh context grows every device arena on its first file (12-16 ms
+ * for a 128 MiB file against 4.7 ms warm), so a reader per file should not create one. */
+int rio_ctx_acquire(int device, rio_ctx** out);
+void rio_ctx_release(rio_ctx* ctx);
 
 /* ---- host-memory two-phase API (the cgo binding: one call pair per file) --------------------
  * rio_frame: H2D copy of the file through pinned staging, device framing (record boundaries,
@@ -241,6 +249,10 @@ typedef struct rio_sst_info {
     uint64_t first_bad_proto; /* ~0 = none */
     uint64_t first_bad_crc;   /* ~0 = none */
     uint64_t first_unplaced;  /* ~0 = none */
+    uint64_t index_bad;       /* first index record that does not decompress (RIO_FLAG_CORRUPT): Load's
+                                 ReadNext error there, before any later index status; ~0 = none.
+                                 n_entries stops at the first flagged index record (gzip's bare io.EOF
+                                 ends the index cleanly, slice_key_index.go:117-126) */
 } rio_sst_info;
 typedef struct rio_sst rio_sst;
 int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, const uint8_t* data_file,
@@ -318,6 +330,12 @@ void rio_index_free(rio_index* idx);
 typedef struct rio_replay rio_replay;
 int rio_replay_open(int device, const char* const* paths, uint64_t n_paths, uint32_t depth, uint32_t workers,
                     rio_replay** out);
+/* The same over several GPUs of one node (one host thread + context per GPU, no
+ * communication): workers_per_device workers per device, worker w on devices[w % n_devices], file i
+ * to worker i % W; files are still handed out strictly in list order. A device may be listed twice
+ * (two workers' contexts on one GPU). */
+int rio_replay_open_devices(const int* devices, uint32_t n_devices, const char* const* paths, uint64_t n_paths,
+                            uint32_t depth, uint32_t workers_per_device, rio_replay** out);
 int rio_replay_next(rio_replay* r, uint64_t* index, const uint8_t** out, const uint64_t** out_off,
                     const uint8_t** flags, rio_file_info* info);
 void rio_replay_free(rio_replay* r);
@@ -338,6 +356,20 @@ void rio_replay_free(rio_replay* r);
  * continues with the reference reader after SkipNext over the records already delivered.
  * rio_stream_open_host reads from host memory instead of a path (the caller keeps it alive until
  * rio_stream_free). */
+/* ---- a file set over several GPUs (independent files sharded over the GPUs of a node,
+ * the 8 tables of an SSTable set, a WAL directory decoded without ordering): rio_fileset_decode
+ * assigns the files to `devices` longest-processing-time first on their sizes, runs one host thread
+ * with a pooled context per device (read, H2D, device decode, D2H into page-locked blocks) and
+ * returns when every file is decoded. rio_fileset_get: file i's arrays (layout as rio_replay_next,
+ * plus rec_off[n]), its info, the device that decoded it; rc RIO_OK or the file's RIO_ERR_IO /
+ * RIO_ERR_HIP. Valid until rio_fileset_free. A device may be listed twice. */
+typedef struct rio_fileset rio_fileset;
+int rio_fileset_decode(const int* devices, uint32_t n_devices, const char* const* paths, uint64_t n_paths,
+                       rio_fileset** out);
+int rio_fileset_get(const rio_fileset* s, uint64_t i, const uint8_t** out, const uint64_t** out_off,
+                    const uint64_t** rec_off, const uint8_t** flags, rio_file_info* info, int* device);
+void rio_fileset_free(rio_fileset* s);
+
 typedef struct rio_stream rio_stream;
 int rio_stream_open(int device, const char* path, uint64_t window_bytes, uint32_t depth, rio_stream** out);
 int rio_stream_open_host(int device, const uint8_t* data, uint64_t len, uint64_t window_bytes, uint32_t depth,
@@ -376,7 +408,7 @@ int rio_reader_read_next(rio_reader* r, const uint8_t** data, uint64_t* len, int
 int rio_reader_skip_next(rio_reader* r);
 /* ReadAtI (recordio.go:91-105), thread-safe: any number of threads may call these on one handle.
  * The first call decodes the whole file once; after that ReadNextAt at a record start, and SeekNext
- * (seek_len >= 3) whose scan lands on a decoded record, are a binary search on the calling thread
+ * (seek_len >= 4) whose scan lands on a decoded record, are a binary search on the calling thread
  * (no kernel, no lock) and *data points into the reader's decoded arena, valid until rio_reader_free.
  * Other offsets run the single-record kernels on a per-call stream; *data is then valid until the
  * calling thread's next ReadNextAt / SeekNext. Detail values are per thread (rio_reader_last_detail). */

@@ -32,8 +32,7 @@ def common(v):
         "recordio_SnappyWriterMultiRecord_asc": {"records": ASC_255, "end": "EOF", "compression": 2},
         "recordio_UncompressedSingleRecord_v0": {"open": ["VERSION", 0]},
         "recordio_UncompressedSingleRecord_v256": {"open": ["VERSION", 256]},
-        "recordio_UncompressedSingleRecord_comp1": {"compression": 1, "records": [{"asc": 1337}], "end": "EOF",
-                                                    "gpu": "UNSUPPORTED"},
+        "recordio_UncompressedSingleRecord_comp1": {"compression": 1, "records": [{"asc": 1337}], "end": "EOF"},
         "recordio_UncompressedSingleRecord_comp2": {"compression": 2, "records": [{"asc": 1337}], "end": "EOF"},
         "recordio_UncompressedSingleRecord_comp300": {"open": ["COMPRESSION_TYPE", 300]},
         "recordio_UncompressedSingleRecord_mnm": {"records": [], "end": "MAGIC"},

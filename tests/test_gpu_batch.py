@@ -1,7 +1,9 @@
 """rio_device_decode_batch (GPU): several device-resident files in one call, each exactly the oracle's.
 
 BASELINE configs[3] decodes 8 files of 64 KiB Snappy records per GPU in one step; the batch runs the
-framing per file and the large-record decoder (k_snappy_coop_batch) once across the files. Every file
+framing per file and one decode launch across the files (k_snappy_pipe_batch, the lane decoder, with
+the waves dealt to the files by record count; files past 32-bit positions, or every file when
+RIO_COOP_MIN says so, take the wave-per-record decoder k_snappy_coop_batch instead). Every file
 of a batch must come out as the FileReader.ReadNext loop restated by the oracle
 (file_reader.go:61-131) says, whatever else shares the batch: large- and small-record Snappy files,
 gzip, uncompressed, damaged files, header-only files, and more files than one launch group holds.
@@ -96,3 +98,62 @@ def test_batch_equals_single_calls():
         assert info["status"] == i1["status"] and info["n_records"] == i1["n_records"]
         nb = info["total_out_bytes"]
         assert bytes(b.out[:nb].cpu().numpy()) == bytes(b1.out[:nb].cpu().numpy())
+
+
+def test_full_c4_file_exact():
+    """One whole C4 file (BASELINE configs[3]: 16384 x 64 KiB text-like Snappy records, seed 100, as
+    bench.py generates it) through rio_device_decode_batch, every byte and offset against the oracle.
+    A second, small file shares the batch so the launch deals its waves over two files."""
+    big = generate(16384, 65536, 2, kind=1, seed=100, threads=16)
+    small = generate(3000, 1024, 2, kind=1, seed=5)
+    files = [to_device_file(big), to_device_file(small)]
+    got = decoder().decode_batch(files)
+    del files
+    for k, (img, (b, info)) in enumerate(zip((big, small), got)):
+        assert info["status"] == 1 and info["n_records"] == (16384, 3000)[k], info
+        o = orc.file_reader_decode_arrays(img)
+        assert_same_as_oracle(_host(b, info), o, f"c4-full[{k}]")
+
+
+@pytest.fixture
+def coop_decoder(monkeypatch):
+    """A decoder whose ctx sends every Snappy file to the wave-per-record decoder (RIO_COOP_MIN=0)."""
+    import ctypes
+
+    from recordio import _lib as L
+    from recordio.device import DeviceDecoder
+
+    monkeypatch.setenv("RIO_COOP_MIN", "0")
+    h = ctypes.c_void_p()
+    assert L.lib().rio_ctx_create(0, ctypes.byref(h)) == 0
+    dec = DeviceDecoder.__new__(DeviceDecoder)
+    dec.device, dec.ctx = 0, h.value
+    yield dec
+    L.lib().rio_ctx_destroy(h)
+
+
+def test_coop_batch_over_several_files(coop_decoder):
+    """k_snappy_coop_batch across files: waves are numbered blockIdx * waves + wave over the grid for
+    every file in turn, so files of different record counts, damaged records, a gzip file and an
+    uncompressed file (both skipped by the Snappy decoders) share one launch."""
+    base = generate(150, 65536, 2, kind=1, seed=9).tobytes()
+    imgs = [generate(700, 3000, 2, kind=1, seed=21).tobytes(),
+            _damage_records(base, 5, 3),
+            generate(20, 200000, 2, kind=1, seed=22).tobytes(),
+            generate(4000, 100, 2, kind=1, seed=23).tobytes(),
+            generate(100, 4096, 1, kind=1, seed=24).tobytes(),
+            generate(500, 900, 0, kind=0, seed=25).tobytes(),
+            corpus.encode_file([], 2),
+            generate(1, 65536, 2, kind=2, seed=26).tobytes()]
+    files = [to_device_file(img) for img in imgs]
+    got = coop_decoder.decode_batch(files)
+    for k, (img, (b, info)) in enumerate(zip(imgs, got)):
+        assert_same_as_oracle(_host(b, info), orc.file_reader_decode_arrays(img), f"coop-batch[{k}]")
+
+
+def test_coop_batch_more_files_than_one_group(coop_decoder):
+    imgs = [generate(9 + 5 * k, 40000, 2, kind=1, seed=400 + k).tobytes() for k in range(19)]
+    files = [to_device_file(img) for img in imgs]
+    got = coop_decoder.decode_batch(files)
+    for k, (img, (b, info)) in enumerate(zip(imgs, got)):
+        assert_same_as_oracle(_host(b, info), orc.file_reader_decode_arrays(img), f"coop-19[{k}]")

@@ -96,13 +96,14 @@ def test_many_threads_one_reader(tmp_path, kind):
 
 def test_seek_next_fast_and_kernel_paths_agree_everywhere(tmp_path):
     """Random payloads put 0x91 bytes in most gaps: SeekNext from every offset of a small file
-    (both the host answers and the kernel scans), with the default window and a 5-byte one."""
+    (both the host answers and the kernel scans), with the default window and 5-, 4- and 3-byte
+    ones (at 3 the reference ends every marker in io.EOF: mmap_reader.go:89-98)."""
     recs = [bytes(random.Random(i).getrandbits(8) for _ in range(60 + 7 * i)) for i in range(40)]
     recs[5] = b"\x91" * 30 + b"\x91\x8d\x4c\x00" + b"x" * 10  # a marker-like run inside a payload
     recs[6] = b"ab\x91"  # ends in 0x91: the scan's skip rule passes over the next record's magic
     img = corpus.encode_file(recs, 0)
     r, path = _open(tmp_path, img)
-    for seek_len in (4096, 5):
+    for seek_len in (4096, 5, 4, 3):
         r.seekLen = seek_len
         for off in range(len(img) + 2):
             st, ro, rec = orc.seek_next(img, off, seek_len)

@@ -248,3 +248,111 @@ def test_host_handle_mismatch_and_handback(tmp_path):
                   tamper=lambda i, e, off: b"\x0a\x7fab" if i == 6 else e)
     rc, info, _ = sst_open_host(base2)
     assert rc == 0 and info.first_bad_proto == 6
+
+
+def test_full_size_c5_table_exact():
+    """One whole C5 table (BASELINE configs[4]: 1.25M SHA1 keys x 1 KiB values, table 0 exactly as
+    bench.py builds it) through the device calls bench.py times: decode of index.rio and data.rio,
+    rio_sst_index_parse, rio_sst_validate. Decoded arenas equal the oracle's byte for byte; every
+    parsed key / valueOffset / checksum equals what the writer put in; every CRC-64 equals the oracle's;
+    the oracle's own scan (orc_sst_scan) accepts the same table."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    import bench
+    from gpu_util import assert_same_as_oracle, decoder
+    from recordio import _lib as L
+    from recordio.device import header_codec, to_device_file
+
+    n = bench.CONFIGS["c5"][0]
+    index_img, data_img = bench.sstable_images(n, 0)
+    dec = decoder()
+    lib = L.lib()
+    host = {}
+    for name, img in (("index", index_img), ("data", data_img)):
+        d, ln = to_device_file(img)
+        b, info = dec.decode(d, ln, comp=header_codec(img))
+        assert info["status"] == 1 and info["n_records"] == n, (name, info)
+        k, nb = info["n_records"], info["total_out_bytes"]
+        g = dict(info, out=b.out[:nb].cpu().numpy(), out_off=b.out_off[:k + 1].cpu().numpy(),
+                 rec_off=b.rec_off[:k].cpu().numpy(), flags=b.flags[:k].cpu().numpy())
+        assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), f"c5 {name}.rio")
+        host[name] = (b, g)
+    ib, gi = host["index"]
+    db, gd = host["data"]
+    i64 = dict(dtype=torch.int64, device="cuda:0")
+    ko, kl, vo, cs, crc = (torch.empty(n, **i64) for _ in range(5))
+    pres, vres = torch.empty(2, **i64), torch.empty(2, **i64)
+    assert lib.rio_sst_index_parse(dec.ctx, ib.out.data_ptr(), ib.out_off.data_ptr(), n, ko.data_ptr(), kl.data_ptr(),
+                                   vo.data_ptr(), cs.data_ptr(), pres.data_ptr(), None) == 0
+    assert lib.rio_sst_validate(dec.ctx, db.out.data_ptr(), db.out_off.data_ptr(), db.rec_off.data_ptr(), n,
+                                vo.data_ptr(), cs.data_ptr(), n, crc.data_ptr(), vres.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert pres[0].item() == -1 and vres.tolist() == [-1, -1]
+    # what the writer put in (bench.sstable_images): sorted SHA1 keys, value i at data record i
+    import hashlib
+    import struct
+
+    keys = np.frombuffer(b"".join(sorted(hashlib.sha1(struct.pack(">I", i)).digest() for i in range(n))),
+                         np.uint8).reshape(n, 20)
+    kl_h, ko_h = kl.cpu().numpy(), ko.cpu().numpy()
+    assert np.all(kl_h == 20)
+    got_keys = gi["out"][ko_h[:, None] + np.arange(20)[None, :]]
+    np.testing.assert_array_equal(got_keys, keys)
+    np.testing.assert_array_equal(vo.cpu().numpy(), gd["rec_off"])
+    value = gd["out"][gd["out_off"][0]:gd["out_off"][1]].tobytes()
+    want_cs = orc.crc64_iso(value)
+    assert np.all(cs.cpu().numpy().astype(np.uint64) == np.uint64(want_cs))
+    assert np.all(crc.cpu().numpy().astype(np.uint64) == np.uint64(want_cs))
+    # the oracle's parse of a sample of index records, and its whole-table scan
+    for i in range(0, n, 9973):
+        a, b2 = int(gi["out_off"][i]), int(gi["out_off"][i + 1])
+        k, v_off, c = orc.index_entry(gi["out"][a:b2].tobytes())
+        assert (k, v_off, c) == (keys[i].tobytes(), int(gd["rec_off"][i]), want_cs), i
+    bad = ctypes.c_uint64()
+    assert orc.lib().orc_sst_scan(index_img.ctypes.data, len(index_img), data_img.ctypes.data, len(data_img),
+                                  ctypes.byref(bad)) == n
+
+
+def _table_with_index(base, items, index_img):
+    """data.rio as the writer makes it for `items`, index.rio replaced by `index_img`."""
+    write_triples(base, triples_for(items))
+    with open(os.path.join(base, "index.rio"), "wb") as fh:
+        fh.write(index_img)
+
+
+@pytest.mark.parametrize("flag", ["corrupt", "eof"])
+def test_flagged_index_record_comes_before_a_later_index_error(tmp_path, flag):
+    """Load's ReadNext loop over index.rio (slice_key_index.go:117-126) stops at the first record that
+    does not decompress: ErrCorrupt fails the load there, gzip's bare io.EOF ends the index with the
+    entries before it. A later index error (a torn header at the end) is never reached."""
+    import corpus
+    from recordio import _lib as L
+
+    items = [(be(i), be(i + 7)) for i in range(12)]
+    base = str(tmp_path / "t")
+    write_triples(base, triples_for(items))
+    ents = [proto.encode_index_entry(k, off, cs) for k, off, cs in
+            zip([k for k, _ in items], orc.file_reader_decode(open(os.path.join(base, "data.rio"), "rb").read())["rec_off"],
+                [crc64_iso(v) for _, v in items])]
+    if flag == "corrupt":
+        recs = [(len(e), corpus.gzip_member(e)) for e in ents]
+        recs[4] = (len(ents[4]), recs[4][1][:-8] + bytes([recs[4][1][-8] ^ 1]) + recs[4][1][-7:])  # bad CRC-32
+    else:
+        recs = [(len(e), corpus.gzip_member(e)) for e in ents]
+        recs[4] = (len(ents[4]), b"")  # empty payload: gzip.NewReader's bare io.EOF
+    index_img = corpus.gz_file(recs) + b"\x91\x8d"  # then a torn header: io.ErrUnexpectedEOF
+    _table_with_index(base, items, index_img)
+    rc, info, ents_got = sst_open_host(base)
+    assert rc == 0 and info.n_entries == 4
+    none = (1 << 64) - 1
+    assert info.index_bad == (4 if flag == "corrupt" else none)
+    r, err = S.NewSSTableReader(S.ReadBasePath(base))
+    if flag == "corrupt":
+        assert r is None and "error while reading index records" in str(err), str(err)
+    else:
+        assert err is None
+        got, serr = scan_all(r)
+        assert serr is None and got == items[:4]

@@ -221,3 +221,18 @@ def test_empty_directory(tmp_path):
     opts, _ = W.NewWriteAheadLogOptions(W.BasePath(str(d)))
     assert replay(opts) == ([], None)
     assert errors_is(EOF, EOF)
+
+
+@pytest.mark.parametrize("devices,workers", [([0, 0], 1), ([0, 0, 0], 2)])
+def test_replay_over_a_device_list(tmp_path, devices, workers):
+    """rio_replay_open_devices: workers spread over several devices (all mapped to the box's GPU),
+    files still handed out in order; same records and error as the reference's loop."""
+    a = appender(tmp_path, 2, max_size=64 << 10)
+    rec = mixed_records(3000, seed=41, max_len=3000)
+    for r in rec:
+        assert (a.AppendSync(r) if r is not None else a.AppendSync(b"")) is None
+    assert a.Close() is None
+    exp, _, _ = expected(a.walOptions.basePath)
+    opts, _ = W.NewWriteAheadLogOptions(W.BasePath(a.walOptions.basePath), W.ReplayOnDevice(devices, 3, workers))
+    got, err = replay(opts)
+    assert err is None and got == exp
