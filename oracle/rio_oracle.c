@@ -594,6 +594,9 @@ int orc_file_reader_decode(const uint8_t* f, uint64_t len, orc_file_result* res)
         uint64_t avail = len - p - h.hdr_len;
         if (plen > avail) { /* io.ReadFull: 0 bytes => io.EOF, partial => ErrUnexpectedEOF */
             status = (avail == 0) ? RIO_EOF_PAYLOAD : RIO_ERR_UNEXPECTED_EOF;
+            /* detail0 = 1: raised by the payload read (file_reader.go:104-107), not inside a header
+             * varint; the error's text and SkipNext's answer (:146-148 vs :157-168) differ */
+            if (status == RIO_ERR_UNEXPECTED_EOF) res->detail0 = 1;
             break;
         }
         const uint8_t* pay = f + p + h.hdr_len;
