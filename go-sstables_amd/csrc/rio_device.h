@@ -25,6 +25,13 @@ constexpr unsigned kSnappyBlock = 256;
 #endif
 constexpr unsigned kSnappyGrid = RIO_SNAPPY_GRID;
 constexpr uint64_t kSinkBytes = (uint64_t)kSnappyBlock / 64 * kSnappyGrid * 64;
+// k_snappy_pair: one parser + one emitter wave per workgroup, seven per CU (256 CUs); its parser
+// waves use one sink line each
+#ifndef RIO_PAIR_GRID
+#define RIO_PAIR_GRID 1792
+#endif
+constexpr unsigned kPairGrid = RIO_PAIR_GRID;
+static_assert(kPairGrid * 64ull <= kSinkBytes, "a sink line per parser wave");
 
 // Framing chunk: a byte range [cs, ce) of the file; a chunk OWNS the records whose header starts
 // in its range. Written by the walk kernel, consumed by the scan / place kernels.
@@ -121,6 +128,9 @@ struct FrameParams {
     // Snappy: files whose mean decoded record is at least this many bytes (and files past 32-bit
     // lane positions) take the wave-per-record decoder k_snappy_coop instead of k_snappy_pipe
     uint64_t coop_min;
+    // 1: the lane-decoder files run on the two-wave decoder (k_snappy_pair: parser + emitter wave)
+    uint32_t pair;
+    uint32_t pad0;
     // the file header's compression type as the host knows it (RIO_COMP_UNKNOWN: every decoder is
     // launched and exits unless the file is its own); k_finish rejects a file that contradicts it
     uint32_t comp_hint;

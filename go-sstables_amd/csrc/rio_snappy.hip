@@ -38,6 +38,11 @@ namespace {
 constexpr uint32_t kOutCh = 16;                  // history ring: 16 chunks = 256 bytes per lane
 constexpr uint32_t kInCh = 4;                    // input ring: 4 chunks = 64 bytes per lane
 constexpr uint32_t kD = 4;                       // pipeline depth in iterations
+// chunks per wave: the balance against the per-chunk drain and setup (A/B on MI355X, records per lane
+// per chunk: C3 64-B records 19 -> 9: decode 0.906 -> 0.870 ms; 4: 0.922, 1: 1.92; C2 stays at 1)
+#ifndef RIO_CHUNKS_PER_WAVE
+#define RIO_CHUNKS_PER_WAVE 8
+#endif
 // copies reaching further back than kFarOff read the output arena (flushed: see snappy_lane)
 constexpr uint32_t kFarOff = 16 * (kD - 1) + 16 + 128;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
@@ -103,6 +108,14 @@ __device__ __forceinline__ uint4 merge_at(uint4 st, uint4 v, uint32_t r) {
 #ifndef RIO_NT
 #define RIO_NT 1
 #endif
+// 1: the element header decoded through one value-field width (fewer selects); A/B build knob
+#ifndef RIO_PARSE2
+#define RIO_PARSE2 0
+#endif
+// 1: waves whose lanes hold one record each run a step without the record switch; A/B build knob
+#ifndef RIO_SINGLE_REC
+#define RIO_SINGLE_REC 0
+#endif
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
 }
@@ -158,9 +171,11 @@ __device__ __forceinline__ bool snappy_wide(const FrameParams& P, const ScanStat
 // lanes writes one owner's next complete 64-byte block (16 B per lane, 64 contiguous bytes of one
 // stream): a wave store touches 16 streams instead of 64, which the L2 absorbs ~3x faster.
 // Returns false with *bad_rec = the failing record if a record does not decode.
-__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint8_t* wi,
-                                            uint32_t lane,
-                            uint8_t* sink, uint64_t* bad_rec) {
+// kMulti = false: every lane of the wave has at most one record (C2's chunks), so the record switch
+// and the next-descriptor fetch are compiled out of the step.
+template <bool kMulti>
+__device__ __forceinline__ bool snappy_lane_t(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint8_t* wi,
+                                              uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
     const LaneLds L{wl + lane * 16, wi + lane * 16};
     const bool live = r0 < r1;
     uint8_t* const out = P.out;
@@ -214,8 +229,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     auto step = [&](Slot& S, const Slot& N, const uint32_t j) __attribute__((always_inline)) {
         drain += pdone ? 1u : 0u;
         // 1. the next record's descriptor, if this slot fetched it
-        nd = sel4(S.desc != 0, S.aux, nd);
-        nds = S.desc ? 2u : nds;
+        if constexpr (kMulti) {
+            nd = sel4(S.desc != 0, S.aux, nd);
+            nds = S.desc ? 2u : nds;
+        }
         const uint32_t pos = s;
 
         // 2. emit the piece parsed kD iterations ago (a bubble appends nothing)
@@ -267,7 +284,21 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);  // the 4 bytes after the tag
             const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
             const bool avail = min((pos + 15) >> 4, lastc) < whi;
-            const bool is0 = t == 0, is1 = t == 1, is2 = t == 2;
+            const bool is0 = t == 0, is1 = t == 1;
+#if RIO_PARSE2
+            // One value field after the tag, of wf bits: a literal with x >= 60 carries x - 59 length
+            // bytes, copy-1 one offset byte (the high 3 offset bits are in the tag), copy-2 two, copy-4
+            // four; so hl = 1 + wf / 8 and the field is the low wf bits of W1 for every form.
+            const bool lng = x >= 60;
+            uint32_t wf = is0 ? (lng ? 8u * x - 472u : 0u) : (4u << t);
+            pin_v(wf);
+            const uint32_t shf = (32u - wf) & 31u;
+            const uint32_t fld = (W1 << shf) >> shf;  // wf = 0 (short literal): unused
+            const uint32_t hl = 1u + (wf >> 3);
+            const uint32_t len = (is0 && lng ? fld : (is1 ? (x & 7u) + 3u : x)) + 1u;
+            const uint32_t off = is1 ? (((tag & 0xE0u) << 3) | fld) : fld;
+#else
+            const bool is2 = t == 2;
             // literal: x < 60 -> length x + 1; x in [60, 63] -> x - 59 little-endian length bytes follow
             const bool lng = x >= 60;
             const uint32_t lmask = 0xFFFFFFFFu >> (((63u - x) << 3) & 31u);
@@ -287,6 +318,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
             const uint32_t hl = is0 ? lit_hl : cp_hl;
             const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
+#endif
             // golang/snappy bounds, per record: header bytes present; literal source room or copy
             // offset in [1, bytes produced] (length / offset 0 wrap to the maximum key); output room
             const uint32_t sleft = s_end - s;
@@ -329,26 +361,30 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             pin_v(at_end);
             if (at_end) {
                 const bool bad_len = pd != rd_end;  // snappy: d != len(dst) => ErrCorrupt
-                const bool more = k + 1 < r1;
-                const bool sw = !bad_len && more && nds == 2;
                 bad = bad || bad_len;
                 // fill (rd_end > pd: output room is checked per element)
                 rem = bad_len ? rd_end - pd : rem;
                 eff = bad_len ? 16u : eff;
                 islit = islit && !bad_len;
-                pdone = pdone || (!bad_len && !more);
-                k += sw ? 1u : 0u;
-                const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
-                s = sw ? (uint32_t)(nstart - base) : s;
-                s_end = sw ? s + nd.z : s_end;
-                rd_start = sw ? pd : rd_start;
-                rd_end = sw ? pd + nd.w : rd_end;
-                nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
+                if constexpr (kMulti) {
+                    const bool more = k + 1 < r1;
+                    const bool sw = !bad_len && more && nds == 2;
+                    pdone = pdone || (!bad_len && !more);
+                    k += sw ? 1u : 0u;
+                    const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
+                    s = sw ? (uint32_t)(nstart - base) : s;
+                    s_end = sw ? s + nd.z : s_end;
+                    rd_start = sw ? pd : rd_start;
+                    rd_end = sw ? pd + nd.w : rd_end;
+                    nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
+                } else {
+                    pdone = pdone || !bad_len;
+                }
             }
         }
         // far history (flushed: see header), or the next record's descriptor, or a placeholder load
         {
-            const bool want_desc = S.kind != 2 && nds == 0;
+            const bool want_desc = kMulti && S.kind != 2 && nds == 0;
             S.desc = want_desc ? 1u : 0u;
             nds = want_desc ? 1u : nds;
             const uint8_t* ap = S.kind == 2 ? gout + qsrc
@@ -396,6 +432,14 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     }
     *bad_rec = r0;
     return !bad;
+}
+
+__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint8_t* wi,
+                                            uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
+#if RIO_SINGLE_REC
+    if (__all(r1 - r0 <= 1)) return snappy_lane_t<false>(P, r0, r1, wl, wi, lane, sink, bad_rec);
+#endif
+    return snappy_lane_t<true>(P, r0, r1, wl, wi, lane, sink, bad_rec);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -765,6 +809,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
     if (!st->any_mixed) return;  // every record is one literal: k_copy_records copies them
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (P.pair && !coop_active(P, st)) return;  // k_snappy_pair decodes the file
     if (coop_active(P, st)) {  // large records / past 32-bit positions: the wave-per-record decoder
         coop_file(P, *reinterpret_cast<CoopLds*>(hist[wave]), lane, (uint64_t)blockIdx.x * (kSnappyBlock / 64) + wave,
                   (uint64_t)gridDim.x * (kSnappyBlock / 64));
@@ -778,11 +823,6 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     // range: one stream, no drain between its records). Chunk g is wave g's; a wave that finishes
     // takes the next unclaimed chunk, so waves whose records decode slower, or that start later, do
     // not hold the kernel's tail. About eight chunks per wave.
-// chunks per wave: the balance against the per-chunk drain and setup (A/B on MI355X, records per lane
-// per chunk: C3 64-B records 19 -> 9: decode 0.906 -> 0.870 ms; 4: 0.922, 1: 1.92; C2 stays at 1)
-#ifndef RIO_CHUNKS_PER_WAVE
-#define RIO_CHUNKS_PER_WAVE 8
-#endif
     constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
     const uint64_t rpc = n >= kCpw * 64 * waves ? n / (kCpw * 64 * waves) : 1;
     const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
@@ -805,6 +845,315 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// The lane decoder split over the two waves of a workgroup (k_snappy_pair, k_snappy_pair_batch).
+//
+// Measured on C2: the one-wave decoder above is issue-bound per wave — a wave issues at
+// most one instruction per 4 cycles, 338 per step, and its 20 KiB of LDS (history + input ring)
+// leaves two waves per SIMD, so the SIMD's VALU pipe (one wave64 instruction per 2 cycles) idles
+// half the time. Here the same per-record stream is served by two waves with lane l of both on
+// record stream l:
+//   * the PARSER wave reads the input (its input ring), decodes the element headers, checks them,
+//     switches records, issues the far-history and input loads, and flushes completed 64-byte
+//     blocks of the history ring to the output arena (cooperative 4-group flush, as above);
+//   * the EMITTER wave owns nothing but the history ring: per step it takes one piece from the
+//     handoff slot, stages its literal / far bytes, funnels the source window into place and writes
+//     the two destination chunks.
+// Each wave's step is about half the instructions, and the parser needs no history LDS, so seven
+// pairs (14 waves, 23 KiB each) fit a CU where the one-wave decoder fits eight waves.
+// Step i of a chunk: the parser hands off the piece it parsed at step i-2 (its far bytes were loaded
+// then) in slot i&1 and parses the next; the emitter emits the piece handed off at step i-1. One
+// workgroup barrier per step (LDS visibility only: lgkmcnt(0), then s_barrier; vector-memory
+// operations stay in flight across it).
+// Far history: the parser flushes (its own stores, issued before its far loads in program order, as
+// in the one-wave decoder) and at step i the emitter has emitted up to the start of piece i-3, so the
+// parser's lead is three pieces (48 bytes) and kFarOff = 48 + 16 + 128 holds unchanged.
+// ------------------------------------------------------------------------------------------
+namespace {
+struct PairLds {
+    uint8_t hist[kOutCh * 1024];   // emitter history rings, [chunk][lane][16 B]
+    uint8_t inring[kInCh * 1024];  // parser input rings, [chunk][lane][16 B]
+    uint4 hdata[2][64];            // handoff: a piece's literal window / far bytes
+    uint32_t hdesc[2][64];         // handoff: n | kind << 5 | (q & 255) << 8
+    uint32_t ctrl[4];              // [0] chunk of the pair, [2 + (i & 1)] continue after step i
+};
+static_assert(sizeof(PairLds) <= 23 * 1024 + 128, "seven pairs per CU");
+constexpr uint32_t kPairBlock = 128;  // parser wave 0, emitter wave 1
+
+// LDS visibility between the two waves: every LDS access of this wave completed, then the barrier.
+// (__syncthreads() would also wait for vmcnt(0): the in-flight far and input loads.)
+__device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct PSlot {
+    uint4 aux;      // far-history bytes (kind 2) or the next record's descriptor (desc)
+    uint4 lit;      // literal window (kind 0)
+    uint32_t n, q, kind, desc;
+};
+__device__ __forceinline__ PSlot pempty() {
+    PSlot S;
+    S.aux = zero4();
+    S.lit = zero4();
+    S.n = 0;
+    S.q = 0;
+    S.kind = 1;
+    S.desc = 0;
+    return S;
+}
+struct ISlot {
+    uint4 v;     // input chunk in flight
+    uint32_t c;  // its chunk index (kNoChunk: nothing)
+};
+
+// Parser side of one chunk: lane = record range [r0, r1). Returns false if a record of the range
+// does not decode (k_finish re-checks the lane's records).
+__device__ __forceinline__ bool pair_parse(const FrameParams& P, uint64_t r0, uint64_t r1, PairLds& S,
+                                           uint32_t lane, uint8_t* sink) {
+    const LaneLds L{S.hist + lane * 16, S.inring + lane * 16};
+    const bool live = r0 < r1;
+    uint8_t* const out = P.out;
+    const uint4 d0 = live ? P.rec_desc[r0] : zero4();
+    const uint64_t o0 = live ? P.out_off[r0] : 0;
+    uint8_t* const gout = out + o0;
+    const uint64_t start0 = ((uint64_t)d0.y << 32) | d0.x;
+    const uint64_t base = start0 & ~15ull;
+    const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
+    const uint32_t lastc = live && base < P.len ? (uint32_t)min((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
+    uint32_t whi = live ? min(kInCh, lastc + 1) : 0u;
+    for (uint32_t c = 0; c < whi; c++) *L.in(c) = sa[c];
+    uint32_t cn = live ? whi : 0xFFFFFFFFu;
+
+    uint64_t k = r0;
+    uint32_t s = (uint32_t)(start0 - base), s_end = s + d0.z;
+    uint32_t pd = 0, rd_start = 0, rd_end = d0.w;
+    uint32_t rem = 0, eff = 0;
+    bool islit = false, bad = false, pdone = !live;
+    uint4 nd = zero4();
+    uint32_t nds = (live && r0 + 1 < r1) ? 0u : 3u;
+    // flush state: de = bytes the emitter has written (as of its previous step), fb = flushed
+    uint32_t de = 0, fb = 0, h1 = 0, h2 = 0;
+    uint8_t* obase[4];
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++) {
+        const int src = (int)((16u * jj + (lane >> 2)) * 4);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
+        obase[jj] = out + (((uint64_t)hi << 32) | lo);
+    }
+    PSlot S0 = pempty(), S1 = pempty();
+    ISlot I0{zero4(), kNoChunk}, I1{zero4(), kNoChunk}, I2{zero4(), kNoChunk}, I3{zero4(), kNoChunk};
+    uint32_t drain = 0, qsrc = 0;
+    uint4 Wa = *L.in(s >> 4), Wb = *L.in((s >> 4) + 1);
+    S.hdesc[1][lane] = 0;  // the emitter's step 0 reads slot 1: a bubble
+    pair_barrier();        // chunk start: the emitter's ring is free, the bubble is visible
+
+    auto step = [&](PSlot& X, ISlot& IX, const ISlot& IN, const uint32_t j) __attribute__((always_inline)) {
+        drain += pdone ? 1u : 0u;
+        // 1. X was parsed two steps ago; its far bytes / descriptor load has landed
+        nd = sel4(X.desc != 0, X.aux, nd);
+        nds = X.desc ? 2u : nds;
+        // 2. the emitter finished the piece handed off two steps ago
+        de += h2;
+        h2 = h1;
+        h1 = X.n;
+        // 3. cooperative flush of completed 64-byte blocks (bytes < de are in the ring)
+        {
+            const uint32_t o = 16u * (j & 3u) + (lane >> 2), part = lane & 3u;
+            const bool ready = de - fb >= 64;
+            const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
+            const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
+            const uint4 fv = *reinterpret_cast<const uint4*>(S.hist + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
+            st_out((ofb >> 31) ? obase[j & 3u] + pos : sink, fv);
+            fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
+        }
+        // 4. hand X off to the emitter (slot j & 1, read at its next step)
+        S.hdata[j & 1u][lane] = sel4(X.kind == 0, X.lit, X.aux);
+        S.hdesc[j & 1u][lane] = X.n | (X.kind << 5) | ((X.q & 255u) << 8);
+        // 5. parse the next piece into X (as snappy_lane step 4)
+        const uint32_t pos = s;
+        {
+            const uint4 W = funnel16(Wa, Wb, pos & 15u);
+            const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);
+            const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
+            const bool avail = min((pos + 15) >> 4, lastc) < whi;
+            const bool is0 = t == 0, is1 = t == 1, is2 = t == 2;
+            const bool lng = x >= 60;
+            const uint32_t lmask = 0xFFFFFFFFu >> (((63u - x) << 3) & 31u);
+            uint32_t lit_long = (W1 & lmask) + 1u, lit_short = x + 1u;
+            uint32_t c1_len = (x & 7u) + 4u, c1_off = ((tag & 0xE0u) << 3) | (W1 & 0xFFu);
+            uint32_t c2_off = W1 & 0xFFFFu;
+            pin_v(lit_long);
+            pin_v(lit_short);
+            pin_v(c1_len);
+            pin_v(c1_off);
+            pin_v(c2_off);
+            const uint32_t lit_len = lng ? lit_long : lit_short;
+            const uint32_t len = is0 ? lit_len : (is1 ? c1_len : lit_short);
+            const uint32_t lit_hl = lng ? x - 58u : 1u;
+            const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
+            const uint32_t hl = is0 ? lit_hl : cp_hl;
+            const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
+            const uint32_t sleft = s_end - s;
+            const uint32_t lim = is0 ? sleft - hl : pd - rd_start;
+            const uint32_t key = (is0 ? len : off) - 1u;
+            const bool hbad = (hl > sleft) | (key >= lim) | (len > rd_end - pd);
+            const bool hdr = !pdone && rem == 0 && s < s_end && avail;
+            const bool badn = hdr && hbad, ok = hdr && !hbad;
+            bad = bad || badn;
+            const uint32_t sh = ok ? hl : 0u;
+            const uint32_t rem1 = ok ? len : rem, eff1 = ok ? off : eff;
+            const bool lit1 = ok ? t == 0 : islit;
+            const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
+            const uint32_t n = go ? min(rem1, lit1 ? 16u - sh : min(16u, eff1)) : 0u;
+            X.n = n;
+            X.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
+            qsrc = pd - eff1;
+            X.q = X.kind == 1 ? qsrc : (X.kind == 0 ? sh : 0u);
+            X.lit = W;
+            s += sh + (lit1 ? n : 0u);
+            rem = rem1 - n;
+            pd += n;
+            eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
+            islit = lit1;
+            s = badn ? s_end : s;
+            uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
+            pin_v(at_end);
+            if (at_end) {
+                const bool bad_len = pd != rd_end;
+                const bool more = k + 1 < r1;
+                const bool sw = !bad_len && more && nds == 2;
+                bad = bad || bad_len;
+                rem = bad_len ? rd_end - pd : rem;
+                eff = bad_len ? 16u : eff;
+                islit = islit && !bad_len;
+                pdone = pdone || (!bad_len && !more);
+                k += sw ? 1u : 0u;
+                const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
+                s = sw ? (uint32_t)(nstart - base) : s;
+                s_end = sw ? s + nd.z : s_end;
+                rd_start = sw ? pd : rd_start;
+                rd_end = sw ? pd + nd.w : rd_end;
+                nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
+            }
+        }
+        // 6. far history, the next record's descriptor, or a placeholder load
+        {
+            const bool want_desc = X.kind != 2 && nds == 0;
+            X.desc = want_desc ? 1u : 0u;
+            nds = want_desc ? 1u : nds;
+            const uint8_t* ap = X.kind == 2 ? gout + qsrc
+                                            : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
+            X.aux = ld_far(ap);
+        }
+        // 7. input prefetch into IX (lands three steps later)
+        {
+            const uint32_t a = s >> 4;
+            const bool take = cn <= lastc && cn < a + kInCh;
+            IX.v = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
+            IX.c = take ? cn : kNoChunk;
+            cn += take ? 1u : 0u;
+        }
+        // 8. land the chunk loaded three steps ago, read the next step's window
+        {
+            const bool landed = IN.c != kNoChunk;
+            if (landed) *L.in(IN.c) = IN.v;
+            whi = landed ? IN.c + 1 : whi;
+            Wa = *L.in(s >> 4);
+            Wb = *L.in((s >> 4) + 1);
+        }
+        // 9. continue while a lane still has pieces in the pipeline (handed off at step i - 2 +
+        // emitted at i + 1: three steps past its last parse)
+        const bool cont = __any(drain < 3);
+        if (lane == 0) S.ctrl[2 + (j & 1u)] = cont ? 1u : 0u;
+        pair_barrier();
+        return cont;
+    };
+    for (;;) {
+        if (!step(S0, I0, I1, 0)) break;
+        if (!step(S1, I1, I2, 1)) break;
+        if (!step(S0, I2, I3, 2)) break;
+        if (!step(S1, I3, I0, 3)) break;
+    }
+    // tail: everything the emitter wrote past the last complete flushed block (its writes are
+    // visible after the last barrier)
+    for (uint32_t q = fb; q < pd; q += 16) {
+        const uint4 v = *L.out(q);
+        if (q + 16 <= pd)
+            stu16(gout + q, v);
+        else
+            st_partial(gout + q, v, pd - q);
+    }
+    return !bad;
+}
+
+// Emitter side of one chunk: as snappy_lane step 2, for the piece handed off at the previous step.
+__device__ __forceinline__ void pair_emit(PairLds& S, uint32_t lane) {
+    const LaneLds L{S.hist + lane * 16, S.inring + lane * 16};
+    uint32_t d = 0;
+    uint4 stage = zero4();
+    pair_barrier();  // chunk start
+    for (uint32_t j = 0;; j++) {
+        const uint32_t sl = (j + 1) & 1u;
+        const uint32_t desc = S.hdesc[sl][lane];
+        const uint4 data = S.hdata[sl][lane];
+        const uint32_t n = desc & 31u, kind = (desc >> 5) & 3u, q = desc >> 8;
+        const uint32_t r = d & 15u, cs = (d >> 4) + 2u;
+        // literal / far bytes to the dead chunk chunk(d) + 2 (a ring copy's write there is harmless)
+        *L.out(cs << 4) = data;
+        const uint32_t w = (kind == 1 ? q : (cs << 4) + q) - r;
+        const uint4 wA = *L.out(w), wB = *L.out(w + 16u), wC = *L.out(w + 32u);
+        uint4 lo, hi;
+        funnel32(wA, wB, wC, w & 15u, lo, hi);
+        lo = merge_at(stage, lo, r);
+        *L.out(d) = lo;
+        *L.out(d + 16) = hi;
+        stage = sel4(r + n >= 16, hi, lo);
+        d += n;
+        pair_barrier();
+        if (!S.ctrl[2 + (j & 1u)]) break;
+    }
+}
+}  // namespace
+
+// one chunk of records per pair at a time, chunks claimed dynamically as in k_snappy_pipe
+__device__ __forceinline__ void pair_lane_range(uint64_t chunk, uint64_t per, uint64_t rpc, uint64_t n, uint32_t lane,
+                                                uint64_t& r0, uint64_t& r1) {
+    r0 = min(chunk * per + lane * rpc, n);
+    r1 = min(r0 + rpc, n);
+}
+
+__global__ void __launch_bounds__(kPairBlock) k_snappy_pair(FrameParams P) {
+    __shared__ __attribute__((aligned(16))) PairLds S;
+    ScanState* st = P.state;
+    if (!P.pair || st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
+    if (!st->any_mixed || coop_active(P, st)) return;
+    const uint32_t lane = threadIdx.x & 63u, role = threadIdx.x >> 6;
+    const uint64_t n = st->n_records;
+    const uint64_t pairs = gridDim.x;
+    constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
+    const uint64_t rpc = n >= kCpw * 64 * pairs ? n / (kCpw * 64 * pairs) : 1;
+    const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
+    uint8_t* sink = P.sink + (uint64_t)blockIdx.x * 64;
+    uint64_t chunk = blockIdx.x;
+    while (chunk < nchunks) {
+        if (role == 0) {
+            uint64_t r0, r1;
+            pair_lane_range(chunk, per, rpc, n, lane, r0, r1);
+            if (!pair_parse(P, r0, r1, S, lane, sink)) {
+                const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
+                if (at < kFailLanes) {
+                    P.fail_lanes[2 * at] = r0;
+                    P.fail_lanes[2 * at + 1] = r1;
+                }
+            }
+            if (lane == 0) S.ctrl[0] = (uint32_t)(pairs + atomicAdd(&st->pipe_next, 1u));
+        } else {
+            pair_emit(S, lane);
+        }
+        pair_barrier();
+        chunk = S.ctrl[0];
+    }
+}
+
 // rio_device_decode_batch: one launch for every lane-decoder file of the batch. The lanes of the grid
 // are split over the files by record count (whole waves per file, so the file's parameters stay
 // wave-uniform scalars), which is what fills the chip when each file alone has fewer records than
@@ -823,7 +1172,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
     uint64_t N = 0;
     for (uint32_t f = 0; f < B.n; f++)
-        if (pipe_active(B.f[f])) N += B.f[f].state->n_records;
+        if (!B.f[f].pair && pipe_active(B.f[f])) N += B.f[f].state->n_records;
     if (N == 0) return;
     // the fewest records per lane whose whole-wave shares (ceil per file) fit the grid: every wave
     // of the grid is resident at once (2 per SIMD), so a share past it would run as a second round
@@ -831,7 +1180,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     for (;;) {
         uint64_t need = 0;
         for (uint32_t f = 0; f < B.n; f++)
-            if (pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
+            if (!B.f[f].pair && pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
         if (need <= waves) break;
         rpl++;
     }
@@ -839,7 +1188,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     uint64_t w0 = 0;
     for (uint32_t f = 0; f < B.n; f++) {
         const FrameParams& P = B.f[f];
-        if (!pipe_active(P)) continue;
+        if (P.pair || !pipe_active(P)) continue;
         const uint64_t n = P.state->n_records, wf = (n + per_wave - 1) / per_wave;
         if (wg < w0 + wf) {
             const uint64_t t = ((wg - w0) << 6) | lane;
@@ -859,8 +1208,51 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     }
 }
 
+// the two-wave decoder over a batch: pairs dealt to the files by record count as above
+__global__ void __launch_bounds__(kPairBlock) k_snappy_pair_batch(FrameBatch B) {
+    __shared__ __attribute__((aligned(16))) PairLds S;
+    const uint32_t lane = threadIdx.x & 63u, role = threadIdx.x >> 6;
+    const uint64_t pairs = gridDim.x, wg = blockIdx.x;
+    uint64_t N = 0;
+    for (uint32_t f = 0; f < B.n; f++)
+        if (B.f[f].pair && pipe_active(B.f[f])) N += B.f[f].state->n_records;
+    if (N == 0) return;
+    uint64_t rpl = (N + 64 * pairs - 1) / (64 * pairs);
+    for (;;) {
+        uint64_t need = 0;
+        for (uint32_t f = 0; f < B.n; f++)
+            if (B.f[f].pair && pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
+        if (need <= pairs) break;
+        rpl++;
+    }
+    const uint64_t per = 64 * rpl;
+    uint64_t w0 = 0;
+    for (uint32_t f = 0; f < B.n; f++) {
+        const FrameParams& P = B.f[f];
+        if (!P.pair || !pipe_active(P)) continue;
+        const uint64_t n = P.state->n_records, wf = (n + per - 1) / per;
+        if (wg < w0 + wf) {
+            const uint64_t r0 = min(((wg - w0) * 64 + lane) * rpl, n), r1 = min(r0 + rpl, n);
+            if (role == 0) {
+                if (!pair_parse(P, r0, r1, S, lane, P.sink + wg * 64)) {
+                    const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
+                    if (at < kFailLanes) {
+                        P.fail_lanes[2 * at] = r0;
+                        P.fail_lanes[2 * at + 1] = r1;
+                    }
+                }
+            } else {
+                pair_emit(S, lane);
+            }
+            return;
+        }
+        w0 += wf;
+    }
+}
+
 hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
     hipLaunchKernelGGL(k_snappy_pipe_batch, dim3(kSnappyGrid), dim3(kSnappyBlock), 0, s, B);
+    if (B.n && B.f[0].pair) hipLaunchKernelGGL(k_snappy_pair_batch, dim3(kPairGrid), dim3(kPairBlock), 0, s, B);
     hipLaunchKernelGGL(k_snappy_coop_batch, dim3(kCoopGrid), dim3(64 * kCoopWaves), 0, s, B);
     return hipGetLastError();
 }
@@ -868,8 +1260,11 @@ hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
 // main = false: the caller runs the lane and wave decoders for this file itself (a batch)
 hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main) {
     // 4 waves x 20 KiB = 80 KiB per workgroup: 2 workgroups (8 waves) per CU
-    if (main)
+    if (main) {
         hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), 0, s, P);
+        // the two-wave decoder: 23 KiB per pair, seven pairs per CU
+        if (P.pair) hipLaunchKernelGGL(k_snappy_pair, dim3(kPairGrid), dim3(kPairBlock), 0, s, P);
+    }
     return hipGetLastError();
 }
 
