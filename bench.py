@@ -934,20 +934,34 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     # when input + output fit the 256 MB MALL (C1), back-to-back steps re-read a warm
     # cache. A second pass writes 1 GiB between decodes (outside the per-stage HIP events) and
     # reports the cold-cache stage times beside the headline.
-    mall_flushed = None
-    if lengths and length + nb < (512 << 20):
-        backend.set_timing(args.steps)
-        for _ in range(args.steps):
-            backend.evict()
-            backend.step()
-        backend.sync()
-        cold = backend.stage_ms()
-        backend.set_timing(1)
+    mall_flushed, cold = None, []
+    # (decided over all ranks: the reductions below are collectives every rank must join)
+    if reduce_max(1.0 if lengths and length + nb < (512 << 20) else 0.0, world) > 0:
+        if lengths:
+            backend.set_timing(args.steps)
+            for _ in range(args.steps):
+                backend.evict()
+                backend.step()
+            backend.sync()
+            cold = backend.stage_ms()
+            backend.set_timing(1)
+        cold_ms = sum(cold) if len(cold) == 4 else 0.0
+        # whole job: every rank's bytes over the slowest rank's cold step
+        cold_value, cold_step_ms, _ = job_throughput(cold_ms * 1e-3, length, 1, world)
         if len(cold) == 4:
-            cold_ms = sum(cold)
-            mall_flushed = {"ms_per_step": round(cold_ms, 4), "value": round(length / (cold_ms * 1e-3) / 2**30, 3),
+            mall_flushed = {"ms_per_step": round(cold_step_ms, 4), "value": round(cold_value, 3),
                             "unit": "GiB/s", "stages_ms": [round(x, 4) for x in cold],
                             "note": "1 GiB device write between steps; per-stage HIP events, flush excluded"}
+
+    # with the working set inside the MALL the warm loop would price cache hits as HBM;
+    # the line then reports the cold pass (MALL evicted before every step, per-stage HIP events,
+    # the eviction excluded): value, ms_per_step and the roofline; the warm wall-clock rate is kept
+    # beside it as warm_value
+    warm = None
+    if mall_flushed and len(cold) == 4:
+        warm = {"value": round(value, 3), "ms_per_step": round(ms_per_step, 4),
+                "note": "back-to-back steps, input + output resident in the 256 MB MALL (wall clock)"}
+        value, ms_per_step, stage = mall_flushed["value"], mall_flushed["ms_per_step"], cold
 
     # roofline of the dominant kernel (Snappy / copy decode): algorithmic bytes per launch =
     # input file bytes (headers + payloads read once) + decoded bytes written once
@@ -1005,6 +1019,8 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     }
     if mall_flushed:
         line["mall_flushed"] = mall_flushed
+    if warm:
+        line["warm_mall"] = warm
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec_offs = None if batch else backend.rec_offs(n)
         line["cpu_baseline"] = cpu_baseline(images, rec_offs, n_rec)
