@@ -970,14 +970,17 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     decode_ms = stage[3] if len(stage) == 4 else float("nan")
     achieved = alg_bytes / (decode_ms * 1e-3) / 1e9
     traffic = None
-    tpath = args.traffic_json
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            if tj.get("config") == args.config:
-                traffic = tj.get("decode_kernel_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    # the config's own PMC file (profiles/traffic_<config>.json), else traffic_latest.json if it is this config's
+    for tpath in ([args.traffic_json] if args.traffic_json else
+                  [os.path.join(HERE, "profiles", f"traffic_{args.config}.json"),
+                   os.path.join(HERE, "profiles", "traffic_latest.json")]):
+        if traffic is None and os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath))
+                if tj.get("config") == args.config:
+                    traffic = tj.get("decode_kernel_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
     pipe_ms = sum(stage) if stage else float("nan")
     if comp == 2 and kind == 0:
         kernel = "k_copy_records"  # ref-random records are each one literal: the copy path decodes them
@@ -1037,7 +1040,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_latest.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic file (default: profiles/traffic_<config>.json, then traffic_latest.json)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()

@@ -25,13 +25,13 @@ constexpr unsigned kSnappyBlock = 256;
 #endif
 constexpr unsigned kSnappyGrid = RIO_SNAPPY_GRID;
 constexpr uint64_t kSinkBytes = (uint64_t)kSnappyBlock / 64 * kSnappyGrid * 64;
-// k_snappy_pair: one parser + one emitter wave per workgroup, seven per CU (256 CUs); its parser
-// waves use one sink line each
+// k_snappy_pair: one parser + one emitter wave per workgroup, six per CU (256 CUs); each pair
+// uses one sink line
 #ifndef RIO_PAIR_GRID
-#define RIO_PAIR_GRID 1792
+#define RIO_PAIR_GRID 1536
 #endif
 constexpr unsigned kPairGrid = RIO_PAIR_GRID;
-static_assert(kPairGrid * 64ull <= kSinkBytes, "a sink line per parser wave");
+static_assert(kPairGrid * 64ull <= kSinkBytes, "a sink line per pair");
 
 // Framing chunk: a byte range [cs, ce) of the file; a chunk OWNS the records whose header starts
 // in its range. Written by the walk kernel, consumed by the scan / place kernels.

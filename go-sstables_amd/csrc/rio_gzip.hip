@@ -464,7 +464,7 @@ __device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t 
                 // runs of plain code lengths (symbols 0..15) as in the data loop: every offset looked
                 // up at once, the chain followed through the lanes, the lengths stored in one write
                 {
-                    const uint32_t lim = (uint32_t)min((uint64_t)B.nb, 8ull * slen - min(8ull * slen, B.consumed()));
+                    const uint32_t lim = (uint32_t)min((uint64_t)B.nb, (uint64_t)8 * slen - min((uint64_t)8 * slen, (uint64_t)B.consumed()));
                     const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
                     uint32_t o = 0, cnt = 0, eo = 0, last = prev;
                     uint64_t m = 0;
@@ -555,7 +555,7 @@ __device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t 
             // (Matches decoded from the same lookup as well measured slower: the extra uniform state
             // spills scalar registers inside the loop; C2-gzip 52.1 -> 66.0 ms.)
             {
-                const uint32_t lim = (uint32_t)min((uint64_t)B.nb, 8ull * slen - min(8ull * slen, B.consumed()));
+                const uint32_t lim = (uint32_t)min((uint64_t)B.nb, (uint64_t)8 * slen - min((uint64_t)8 * slen, (uint64_t)B.consumed()));
                 const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
                 uint32_t o = 0, cnt = 0, eo = 0;
                 uint64_t m = 0;

@@ -113,6 +113,9 @@ __device__ __forceinline__ uint4 merge_at(uint4 st, uint4 v, uint32_t r) {
 #define RIO_PARSE2 0
 #endif
 // 1: waves whose lanes hold one record each run a step without the record switch; A/B build knob
+#ifndef RIO_PAIR_DEBUG
+#define RIO_PAIR_DEBUG 0  // bounded queue waits that report a stuck pair (printf)
+#endif
 #ifndef RIO_SINGLE_REC
 #define RIO_SINGLE_REC 0
 #endif
@@ -848,61 +851,46 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
 // ------------------------------------------------------------------------------------------
 // The lane decoder split over the two waves of a workgroup (k_snappy_pair, k_snappy_pair_batch).
 //
-// Measured on C2: the one-wave decoder above is issue-bound per wave — a wave issues at
-// most one instruction per 4 cycles, 338 per step, and its 20 KiB of LDS (history + input ring)
-// leaves two waves per SIMD, so the SIMD's VALU pipe (one wave64 instruction per 2 cycles) idles
-// half the time. Here the same per-record stream is served by two waves with lane l of both on
-// record stream l:
-//   * the PARSER wave reads the input (its input ring), decodes the element headers, checks them,
-//     switches records, issues the far-history and input loads, and flushes completed 64-byte
-//     blocks of the history ring to the output arena (cooperative 4-group flush, as above);
-//   * the EMITTER wave owns nothing but the history ring: per step it takes one piece from the
-//     handoff slot, stages its literal / far bytes, funnels the source window into place and writes
-//     the two destination chunks.
-// Each wave's step is about half the instructions, and the parser needs no history LDS, so seven
-// pairs (14 waves, 23 KiB each) fit a CU where the one-wave decoder fits eight waves.
-// Step i of a chunk: the parser hands off the piece it parsed at step i-2 (its far bytes were loaded
-// then) in slot i&1 and parses the next; the emitter emits the piece handed off at step i-1. One
-// workgroup barrier per step (LDS visibility only: lgkmcnt(0), then s_barrier; vector-memory
-// operations stay in flight across it).
-// Far history: the parser flushes (its own stores, issued before its far loads in program order, as
-// in the one-wave decoder) and at step i the emitter has emitted up to the start of piece i-3, so the
-// parser's lead is three pieces (48 bytes) and kFarOff = 48 + 16 + 128 holds unchanged.
-// ------------------------------------------------------------------------------------------
+// Measured on C2: the one-wave decoder above issues at most one instruction per 4
+// cycles per wave (338 per step) and its 20 KiB of LDS (history + input ring) leaves two waves per
+// SIMD, so the SIMD's VALU pipe (one wave64 instruction per 2 cycles) idles about half the time.
+// Here lane l of two waves serves record stream l:
+//   * the PARSER wave reads the input (input ring), decodes and checks the element headers, switches
+//     records and writes one piece per step into a 4-slot LDS queue: no history, no far loads;
+//   * the EMITTER wave owns the history ring and runs the one-wave decoder's emit side unchanged: it
+//     takes piece j + 3 from the queue at step j (issuing its far-history load then, after its own
+//     flush store of the step, so kFarOff = 48 + 16 + 128 holds as before), emits piece j, flushes.
+// The two waves are decoupled: the parser may run kQ pieces past the emitter's queue reads, each side
+// waits on the other's LDS counter only when the queue is full / empty. Six pairs (26 KiB each) fit
+// a CU: twelve waves where the one-wave decoder fits eight.
 namespace {
+constexpr uint32_t kQ = 4;           // queue slots
+constexpr uint32_t kPairBlock = 128;  // parser wave 0, emitter wave 1
 struct PairLds {
     uint8_t hist[kOutCh * 1024];   // emitter history rings, [chunk][lane][16 B]
     uint8_t inring[kInCh * 1024];  // parser input rings, [chunk][lane][16 B]
-    uint4 hdata[2][64];            // handoff: a piece's literal window / far bytes
-    uint32_t hdesc[2][64];         // handoff: n | kind << 5 | (q & 255) << 8
-    uint32_t ctrl[4];              // [0] chunk of the pair, [2 + (i & 1)] continue after step i
+    uint4 qdata[kQ][64];           // a piece's literal window (16 input bytes from the tag)
+    uint2 qdesc[kQ][64];           // x = n | kind << 5 | sh << 8, y = source position (kind 1 / 2)
+    uint32_t cnt[4];               // [0] pieces produced, [1] pieces read by the emitter,
+                                   // [2] the chunk's piece count (kNoChunk until known), [3] chunk
 };
-static_assert(sizeof(PairLds) <= 23 * 1024 + 128, "seven pairs per CU");
-constexpr uint32_t kPairBlock = 128;  // parser wave 0, emitter wave 1
+static_assert(sizeof(PairLds) <= 160 * 1024 / 6, "six pairs per CU");
 
-// LDS visibility between the two waves: every LDS access of this wave completed, then the barrier.
-// (__syncthreads() would also wait for vmcnt(0): the in-flight far and input loads.)
-__device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-struct PSlot {
-    uint4 aux;      // far-history bytes (kind 2) or the next record's descriptor (desc)
-    uint4 lit;      // literal window (kind 0)
-    uint32_t n, q, kind, desc;
-};
-__device__ __forceinline__ PSlot pempty() {
-    PSlot S;
-    S.aux = zero4();
-    S.lit = zero4();
-    S.n = 0;
-    S.q = 0;
-    S.kind = 1;
-    S.desc = 0;
-    return S;
-}
 struct ISlot {
     uint4 v;     // input chunk in flight
     uint32_t c;  // its chunk index (kNoChunk: nothing)
 };
+
+// queue counters: relaxed workgroup-scope atomics (ds_read / ds_write; a plain volatile access
+// would become a flat access, which counts in vmcnt too)
+__device__ __forceinline__ uint32_t lds_ld_v(uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_ld(uint32_t* p) { return __builtin_amdgcn_readfirstlane(lds_ld_v(p)); }
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+    asm volatile("" ::: "memory");  // after the wave's data writes (LDS keeps a wave's order)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Parser side of one chunk: lane = record range [r0, r1). Returns false if a record of the range
 // does not decode (k_finish re-checks the lane's records).
@@ -910,10 +898,7 @@ __device__ __forceinline__ bool pair_parse(const FrameParams& P, uint64_t r0, ui
                                            uint32_t lane, uint8_t* sink) {
     const LaneLds L{S.hist + lane * 16, S.inring + lane * 16};
     const bool live = r0 < r1;
-    uint8_t* const out = P.out;
     const uint4 d0 = live ? P.rec_desc[r0] : zero4();
-    const uint64_t o0 = live ? P.out_off[r0] : 0;
-    uint8_t* const gout = out + o0;
     const uint64_t start0 = ((uint64_t)d0.y << 32) | d0.x;
     const uint64_t base = start0 & ~15ull;
     const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
@@ -927,51 +912,29 @@ __device__ __forceinline__ bool pair_parse(const FrameParams& P, uint64_t r0, ui
     uint32_t pd = 0, rd_start = 0, rd_end = d0.w;
     uint32_t rem = 0, eff = 0;
     bool islit = false, bad = false, pdone = !live;
+    // next record's descriptor: 0 needed, 1 in flight, 2 landed, 3 none (last record)
     uint4 nd = zero4();
     uint32_t nds = (live && r0 + 1 < r1) ? 0u : 3u;
-    // flush state: de = bytes the emitter has written (as of its previous step), fb = flushed
-    uint32_t de = 0, fb = 0, h1 = 0, h2 = 0;
-    uint8_t* obase[4];
-#pragma unroll
-    for (uint32_t jj = 0; jj < 4; jj++) {
-        const int src = (int)((16u * jj + (lane >> 2)) * 4);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
-        obase[jj] = out + (((uint64_t)hi << 32) | lo);
-    }
-    PSlot S0 = pempty(), S1 = pempty();
+    // input chunks and descriptor loads in flight: issued at step p, used at step p + 3
     ISlot I0{zero4(), kNoChunk}, I1{zero4(), kNoChunk}, I2{zero4(), kNoChunk}, I3{zero4(), kNoChunk};
-    uint32_t drain = 0, qsrc = 0;
+    uint4 D0 = zero4(), D1 = zero4(), D2 = zero4(), D3 = zero4();
+    uint32_t dm = 0;  // bit i: slot i carries a descriptor
     uint4 Wa = *L.in(s >> 4), Wb = *L.in((s >> 4) + 1);
-    S.hdesc[1][lane] = 0;  // the emitter's step 0 reads slot 1: a bubble
-    pair_barrier();        // chunk start: the emitter's ring is free, the bubble is visible
+    uint32_t rd = 0;   // the emitter's read count as last seen (wave-uniform)
+    uint32_t rdv = 0;  // its LDS read issued at the previous step
+    uint32_t p = 0;
 
-    auto step = [&](PSlot& X, ISlot& IX, const ISlot& IN, const uint32_t j) __attribute__((always_inline)) {
-        drain += pdone ? 1u : 0u;
-        // 1. X was parsed two steps ago; its far bytes / descriptor load has landed
-        nd = sel4(X.desc != 0, X.aux, nd);
-        nds = X.desc ? 2u : nds;
-        // 2. the emitter finished the piece handed off two steps ago
-        de += h2;
-        h2 = h1;
-        h1 = X.n;
-        // 3. cooperative flush of completed 64-byte blocks (bytes < de are in the ring)
-        {
-            const uint32_t o = 16u * (j & 3u) + (lane >> 2), part = lane & 3u;
-            const bool ready = de - fb >= 64;
-            const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
-            const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
-            const uint4 fv = *reinterpret_cast<const uint4*>(S.hist + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
-            st_out((ofb >> 31) ? obase[j & 3u] + pos : sink, fv);
-            fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
-        }
-        // 4. hand X off to the emitter (slot j & 1, read at its next step)
-        S.hdata[j & 1u][lane] = sel4(X.kind == 0, X.lit, X.aux);
-        S.hdesc[j & 1u][lane] = X.n | (X.kind << 5) | ((X.q & 255u) << 8);
-        // 5. parse the next piece into X (as snappy_lane step 4)
+    auto step = [&](ISlot& IX, const ISlot& IN, uint4& DX, const uint32_t j) __attribute__((always_inline)) {
+        rd = __builtin_amdgcn_readfirstlane(rdv);
+        // 1. the descriptor load of four steps ago (this slot), if any
+        const bool dl = (dm >> j) & 1u;
+        nd = sel4(dl, DX, nd);
+        nds = dl ? 2u : nds;
+        // 2. parse piece p (as snappy_lane step 4)
         const uint32_t pos = s;
+        const uint4 W = funnel16(Wa, Wb, pos & 15u);
+        uint32_t n, kind, sh, qsrc;
         {
-            const uint4 W = funnel16(Wa, Wb, pos & 15u);
             const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);
             const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
             const bool avail = min((pos + 15) >> 4, lastc) < whi;
@@ -999,16 +962,13 @@ __device__ __forceinline__ bool pair_parse(const FrameParams& P, uint64_t r0, ui
             const bool hdr = !pdone && rem == 0 && s < s_end && avail;
             const bool badn = hdr && hbad, ok = hdr && !hbad;
             bad = bad || badn;
-            const uint32_t sh = ok ? hl : 0u;
+            sh = ok ? hl : 0u;
             const uint32_t rem1 = ok ? len : rem, eff1 = ok ? off : eff;
             const bool lit1 = ok ? t == 0 : islit;
             const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
-            const uint32_t n = go ? min(rem1, lit1 ? 16u - sh : min(16u, eff1)) : 0u;
-            X.n = n;
-            X.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
+            n = go ? min(rem1, lit1 ? 16u - sh : min(16u, eff1)) : 0u;
+            kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
             qsrc = pd - eff1;
-            X.q = X.kind == 1 ? qsrc : (X.kind == 0 ? sh : 0u);
-            X.lit = W;
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
@@ -1035,92 +995,194 @@ __device__ __forceinline__ bool pair_parse(const FrameParams& P, uint64_t r0, ui
                 nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
             }
         }
-        // 6. far history, the next record's descriptor, or a placeholder load
-        {
-            const bool want_desc = X.kind != 2 && nds == 0;
-            X.desc = want_desc ? 1u : 0u;
-            nds = want_desc ? 1u : nds;
-            const uint8_t* ap = X.kind == 2 ? gout + qsrc
-                                            : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
-            X.aux = ld_far(ap);
+        // 3. queue slot p % kQ must be free: the emitter has read piece p - kQ
+        for (uint32_t spin = 0; p >= rd + kQ; spin++) {  // rare: the emitter is kQ pieces behind
+            __builtin_amdgcn_s_sleep(1);
+            rd = lds_ld(&S.cnt[1]);
+#if RIO_PAIR_DEBUG
+            if (spin == (1u << 22)) {
+                if (lane == 0)
+                    printf("pair parse stuck: block %u p %u rd %u c0 %u c2 %u r0 %llu\n", blockIdx.x, p, rd,
+                           lds_ld(&S.cnt[0]), lds_ld(&S.cnt[2]), (unsigned long long)r0);
+                rd = p;
+            }
+#endif
         }
-        // 7. input prefetch into IX (lands three steps later)
+        S.qdata[p % kQ][lane] = W;
+        S.qdesc[p % kQ][lane] = make_uint2(n | (kind << 5) | (sh << 8), kind == 2 ? qsrc : (qsrc & 0xFFu));
+        p++;
+        if (lane == 0) lds_st(&S.cnt[0], p);
+        // 4. the next record's descriptor (or a placeholder), used four steps later
+        {
+            const bool want = nds == 0;
+            nds = want ? 1u : nds;
+            dm = want ? (dm | (1u << j)) : (dm & ~(1u << j));
+            DX = *reinterpret_cast<const uint4*>(want ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
+        }
+        // 5. input prefetch into IX (lands three steps later), land IN, read the next window
         {
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn < a + kInCh;
             IX.v = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
             IX.c = take ? cn : kNoChunk;
             cn += take ? 1u : 0u;
-        }
-        // 8. land the chunk loaded three steps ago, read the next step's window
-        {
             const bool landed = IN.c != kNoChunk;
             if (landed) *L.in(IN.c) = IN.v;
             whi = landed ? IN.c + 1 : whi;
             Wa = *L.in(s >> 4);
             Wb = *L.in((s >> 4) + 1);
         }
-        // 9. continue while a lane still has pieces in the pipeline (handed off at step i - 2 +
-        // emitted at i + 1: three steps past its last parse)
-        const bool cont = __any(drain < 3);
-        if (lane == 0) S.ctrl[2 + (j & 1u)] = cont ? 1u : 0u;
-        pair_barrier();
-        return cont;
+        rdv = lds_ld_v(&S.cnt[1]);  // for the next step (lands meanwhile)
+#if RIO_PAIR_DEBUG
+        if (p == (1u << 24)) {
+            if (lane == 0) printf("pair parse runaway: block %u r0 %llu\n", blockIdx.x, (unsigned long long)r0);
+            return false;
+        }
+#endif
+        return !__all(pdone);
     };
     for (;;) {
-        if (!step(S0, I0, I1, 0)) break;
-        if (!step(S1, I1, I2, 1)) break;
-        if (!step(S0, I2, I3, 2)) break;
-        if (!step(S1, I3, I0, 3)) break;
+        if (!step(I0, I1, D0, 0)) break;
+        if (!step(I1, I2, D1, 1)) break;
+        if (!step(I2, I3, D2, 2)) break;
+        if (!step(I3, I0, D3, 3)) break;
     }
-    // tail: everything the emitter wrote past the last complete flushed block (its writes are
-    // visible after the last barrier)
-    for (uint32_t q = fb; q < pd; q += 16) {
-        const uint4 v = *L.out(q);
-        if (q + 16 <= pd)
-            stu16(gout + q, v);
-        else
-            st_partial(gout + q, v, pd - q);
-    }
+    if (lane == 0) lds_st(&S.cnt[2], p);  // every piece of the chunk is in the queue
     return !bad;
 }
 
-// Emitter side of one chunk: as snappy_lane step 2, for the piece handed off at the previous step.
-__device__ __forceinline__ void pair_emit(PairLds& S, uint32_t lane) {
+// Emitter side of one chunk (snappy_lane's emit, flush and far loads; its pieces come from the
+// queue): lane = the parser lane's record range, for the output base and the flush owners.
+__device__ __forceinline__ void pair_emit(const FrameParams& P, uint64_t r0, uint64_t r1, PairLds& S, uint32_t lane,
+                                          uint8_t* sink) {
     const LaneLds L{S.hist + lane * 16, S.inring + lane * 16};
-    uint32_t d = 0;
+    uint8_t* const out = P.out;
+    const uint64_t o0 = r0 < r1 ? P.out_off[r0] : 0;
+    uint8_t* const gout = out + o0;
+    uint8_t* obase[4];
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++) {
+        const int src = (int)((16u * jj + (lane >> 2)) * 4);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
+        obase[jj] = out + (((uint64_t)hi << 32) | lo);
+    }
+    uint32_t d = 0, fb = 0;
     uint4 stage = zero4();
-    pair_barrier();  // chunk start
-    for (uint32_t j = 0;; j++) {
-        const uint32_t sl = (j + 1) & 1u;
-        const uint32_t desc = S.hdesc[sl][lane];
-        const uint4 data = S.hdata[sl][lane];
-        const uint32_t n = desc & 31u, kind = (desc >> 5) & 3u, q = desc >> 8;
-        const uint32_t r = d & 15u, cs = (d >> 4) + 2u;
-        // literal / far bytes to the dead chunk chunk(d) + 2 (a ring copy's write there is harmless)
-        *L.out(cs << 4) = data;
-        const uint32_t w = (kind == 1 ? q : (cs << 4) + q) - r;
-        const uint4 wA = *L.out(w), wB = *L.out(w + 16u), wC = *L.out(w + 32u);
-        uint4 lo, hi;
-        funnel32(wA, wB, wC, w & 15u, lo, hi);
-        lo = merge_at(stage, lo, r);
-        *L.out(d) = lo;
-        *L.out(d + 16) = hi;
-        stage = sel4(r + n >= 16, hi, lo);
-        d += n;
-        pair_barrier();
-        if (!S.ctrl[2 + (j & 1u)]) break;
+    Slot S0 = empty_slot(), S1 = empty_slot(), S2 = empty_slot(), S3 = empty_slot();
+    uint4 wA = zero4(), wB = zero4(), wC = zero4();
+    uint32_t wF = 0, wN = 0;
+    uint32_t have = 0, fin = kNoChunk;  // pieces produced / the chunk's count, as last seen (uniform)
+    uint32_t hv = 0, fv2 = kNoChunk;     // their LDS reads issued at the previous step
+    uint32_t j = 0;                      // the piece this step emits
+
+    // take piece m into slot X (a bubble past the chunk's last piece); X.desc = its far source
+    auto take = [&](Slot& X, uint32_t m) __attribute__((always_inline)) {
+        for (uint32_t spin = 0; m >= have && m < fin; spin++) {  // the parser is behind: wait for piece m or the end
+            have = lds_ld(&S.cnt[0]);
+            fin = lds_ld(&S.cnt[2]);
+            if (m >= have && m < fin) __builtin_amdgcn_s_sleep(1);
+#if RIO_PAIR_DEBUG
+            if (spin == (1u << 22)) {
+                if (lane == 0)
+                    printf("pair emit stuck: block %u m %u have %u fin %u c1 %u r0 %llu\n", blockIdx.x, m, have, fin,
+                           lds_ld(&S.cnt[1]), (unsigned long long)r0);
+                fin = m;
+            }
+#endif
+        }
+        const bool real = m < have && m < fin;
+        const uint2 qd = S.qdesc[m % kQ][lane];
+        X.lit = S.qdata[m % kQ][lane];
+        X.n = real ? (qd.x & 31u) : 0u;
+        X.kind = real ? ((qd.x >> 5) & 3u) : 1u;
+        X.q = X.kind == 1 ? qd.y : (X.kind == 0 ? (qd.x >> 8) : 0u);
+        X.desc = qd.y;
+        if (lane == 0 && real) lds_st(&S.cnt[1], m + 1);
+    };
+    take(S0, 0);
+    take(S1, 1);
+    take(S2, 2);
+#if RIO_PAIR_DEBUG
+    if (lane == 0 && blockIdx.x == 0) printf("emit init have %u fin %u\n", have, fin);
+#endif
+    S0.aux = ld_far(S0.kind == 2 ? gout + S0.desc : sink);
+    S1.aux = ld_far(S1.kind == 2 ? gout + S1.desc : sink);
+    S2.aux = ld_far(S2.kind == 2 ? gout + S2.desc : sink);
+    {  // the first piece's window
+        const uint32_t cs = 2u;
+        *L.out(cs << 4) = sel4(S0.kind == 0, S0.lit, S0.aux);
+        wN = S0.kind == 1 ? S0.q : (cs << 4) + S0.q;
+        wF = wN & 15u;
+        wA = *L.out(wN);
+        wB = *L.out(wN + 16u);
+        wC = *L.out(wN + 32u);
+    }
+    auto step = [&](Slot& X, const Slot& N, Slot& F, const uint32_t jj) __attribute__((always_inline)) {
+        have = max(have, (uint32_t)__builtin_amdgcn_readfirstlane(hv));  // (an int argument picks min/max(double))
+        fin = min(fin, (uint32_t)__builtin_amdgcn_readfirstlane(fv2));
+        hv = lds_ld_v(&S.cnt[0]);  // for the next step
+        fv2 = lds_ld_v(&S.cnt[2]);
+        // 1. emit piece j (window read during the previous step)
+        {
+            const uint32_t r = d & 15u;
+            uint4 lo, hi;
+            funnel32(wA, wB, wC, wF, lo, hi);
+            lo = merge_at(stage, lo, r);
+            *L.out(d) = lo;
+            *L.out(d + 16) = hi;
+            stage = sel4(r + X.n >= 16, hi, lo);
+            d += X.n;
+            const uint32_t r2 = d & 15u, cs = (d >> 4) + 2u;
+            *L.out(cs << 4) = sel4(N.kind == 0, N.lit, N.aux);
+            const uint32_t w = (N.kind == 1 ? N.q : (cs << 4) + N.q) - r2;
+            wN = w;
+            wF = w & 15u;
+        }
+        // 2. cooperative flush (as snappy_lane step 3)
+        {
+            const uint32_t o = 16u * (jj & 3u) + (lane >> 2), part = lane & 3u;
+            const bool ready = d - fb >= 64;
+            const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
+            const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
+            const uint4 fv = *reinterpret_cast<const uint4*>(S.hist + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
+            wA = *L.out(wN);
+            wB = *L.out(wN + 16u);
+            wC = *L.out(wN + 32u);
+            st_out((ofb >> 31) ? obase[jj & 3u] + pos : sink, fv);
+            fb += ((lane >> 4) == (jj & 3u) && ready) ? 64u : 0u;
+        }
+        // 3. piece j + 3 from the queue into slot (j + 3) % 4 (emitted at step j - 1), its far load after
+        // this step's flush store
+#if RIO_PAIR_DEBUG
+        if (lane == 0 && j < 6 && blockIdx.x == 0) printf("emit step j %u have %u fin %u d %u fb %u\n", j, have, fin, d, fb);
+#endif
+        take(F, j + 3);
+        F.aux = ld_far(F.kind == 2 ? gout + F.desc : sink);
+        j++;
+        return j < fin;
+    };
+    for (;;) {
+        if (!step(S0, S1, S3, 0)) break;
+        if (!step(S1, S2, S0, 1)) break;
+        if (!step(S2, S3, S1, 2)) break;
+        if (!step(S3, S0, S2, 3)) break;
+    }
+#if RIO_PAIR_DEBUG
+    if (lane == 0 && blockIdx.x == 0) printf("emit done j %u have %u fin %u d %u\n", j, have, fin, d);
+#endif
+    for (uint32_t q = fb; q < d; q += 16) {
+        const uint4 v = *L.out(q);
+        if (q + 16 <= d)
+            stu16(gout + q, v);
+        else
+            st_partial(gout + q, v, d - q);
     }
 }
 }  // namespace
 
-// one chunk of records per pair at a time, chunks claimed dynamically as in k_snappy_pipe
-__device__ __forceinline__ void pair_lane_range(uint64_t chunk, uint64_t per, uint64_t rpc, uint64_t n, uint32_t lane,
-                                                uint64_t& r0, uint64_t& r1) {
-    r0 = min(chunk * per + lane * rpc, n);
-    r1 = min(r0 + rpc, n);
-}
-
+// one chunk of records per pair at a time, chunks claimed dynamically as in k_snappy_pipe; both
+// waves meet at a workgroup barrier only between chunks
 __global__ void __launch_bounds__(kPairBlock) k_snappy_pair(FrameParams P) {
     __shared__ __attribute__((aligned(16))) PairLds S;
     ScanState* st = P.state;
@@ -1132,12 +1194,17 @@ __global__ void __launch_bounds__(kPairBlock) k_snappy_pair(FrameParams P) {
     constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
     const uint64_t rpc = n >= kCpw * 64 * pairs ? n / (kCpw * 64 * pairs) : 1;
     const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
-    uint8_t* sink = P.sink + (uint64_t)blockIdx.x * 64;
+    uint8_t* sink = P.sink + (uint64_t)blockIdx.x * 64;  // placeholder line of the pair
     uint64_t chunk = blockIdx.x;
     while (chunk < nchunks) {
+        const uint64_t r0 = min(chunk * per + lane * rpc, n), r1 = min(r0 + rpc, n);
+        if (threadIdx.x == 0) {
+            S.cnt[0] = 0;
+            S.cnt[1] = 0;
+            S.cnt[2] = kNoChunk;
+        }
+        __syncthreads();
         if (role == 0) {
-            uint64_t r0, r1;
-            pair_lane_range(chunk, per, rpc, n, lane, r0, r1);
             if (!pair_parse(P, r0, r1, S, lane, sink)) {
                 const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
                 if (at < kFailLanes) {
@@ -1145,12 +1212,13 @@ __global__ void __launch_bounds__(kPairBlock) k_snappy_pair(FrameParams P) {
                     P.fail_lanes[2 * at + 1] = r1;
                 }
             }
-            if (lane == 0) S.ctrl[0] = (uint32_t)(pairs + atomicAdd(&st->pipe_next, 1u));
+            if (lane == 0) S.cnt[3] = (uint32_t)(pairs + atomicAdd(&st->pipe_next, 1u));
         } else {
-            pair_emit(S, lane);
+            pair_emit(P, r0, r1, S, lane, sink);
         }
-        pair_barrier();
-        chunk = S.ctrl[0];
+        __syncthreads();
+        chunk = S.cnt[3];
+        __syncthreads();
     }
 }
 
@@ -1233,6 +1301,12 @@ __global__ void __launch_bounds__(kPairBlock) k_snappy_pair_batch(FrameBatch B) 
         const uint64_t n = P.state->n_records, wf = (n + per - 1) / per;
         if (wg < w0 + wf) {
             const uint64_t r0 = min(((wg - w0) * 64 + lane) * rpl, n), r1 = min(r0 + rpl, n);
+            if (threadIdx.x == 0) {
+                S.cnt[0] = 0;
+                S.cnt[1] = 0;
+                S.cnt[2] = kNoChunk;
+            }
+            __syncthreads();
             if (role == 0) {
                 if (!pair_parse(P, r0, r1, S, lane, P.sink + wg * 64)) {
                     const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
@@ -1242,7 +1316,7 @@ __global__ void __launch_bounds__(kPairBlock) k_snappy_pair_batch(FrameBatch B) 
                     }
                 }
             } else {
-                pair_emit(S, lane);
+                pair_emit(P, r0, r1, S, lane, P.sink + wg * 64);
             }
             return;
         }
