@@ -94,7 +94,23 @@ struct ScanState {
                             // size (its last member's ISIZE) does not cover: k_gz_resize sizes them;
                             // lzw: some record's output is not its header's u (k_lzw_resize)
     uint32_t gz_redo;       // k_gz_resize / k_lzw_resize ran: the scan, placement and decoders run again
+    uint32_t lb_fused;      // k_walk placed every record (look-back path, FrameParams::fused): k_scan_blocks
+                            // took the totals from its last chunk and k_place only merges the chunk flags
+    uint32_t pad_lb;
 };
+
+// Decoupled look-back of the fused walk (FrameParams::fused): per chunk kLbWords 8-byte words, each
+// written once per launch by one agent-scope (write-through) store and tagged with the launch's epoch
+// in its top 24 bits, so a reader needs no fence: a word is this launch's iff its tag matches.
+//   [0..4] the chunk's own run (key, out, cnt, bytes, term | broken << 1 | term_chunk << 2)
+//   [5..8] the inclusive prefix over chunks 0..c (out, cnt, bytes, flags; key is the file's first record)
+//   [9..11] placement flags for k_place (plain stores): first flagged record, flagged count, mixed | huge << 1
+// lb_ctl[0] = the walk's wave ticket (the last wave resets it to 0), [1..4] the whole file's run
+// (the last chunk's inclusive prefix).
+constexpr uint32_t kLbWords = 16;
+constexpr uint32_t kLbValBits = 40;
+constexpr uint64_t kLbMask = (1ull << kLbValBits) - 1;
+constexpr uint32_t kLbTagMask = (1u << 24) - 1;
 
 // Result of the single-record (ReadNextAt) kernel.
 struct ReadAtResult {
@@ -130,7 +146,13 @@ struct FrameParams {
     uint64_t coop_min;
     // 1: the lane-decoder files run on the two-wave decoder (k_snappy_pair: parser + emitter wave)
     uint32_t pair;
-    uint32_t pad0;
+    // 1: k_walk places the records itself (decoupled look-back over lb); only when the decode of the
+    // same FrameParams follows in the same call (rio_device_decode[_ex|_batch])
+    uint32_t fused;
+    uint64_t* lb;         // [n_chunks * kLbWords] look-back words (see kLbWords)
+    uint64_t* lb_ctl;     // [8] ticket + file totals
+    uint32_t lb_epoch;    // this launch's tag (1 .. kLbTagMask)
+    uint32_t pad1;
     // the file header's compression type as the host knows it (RIO_COMP_UNKNOWN: every decoder is
     // launched and exits unless the file is its own); k_finish rejects a file that contradicts it
     uint32_t comp_hint;

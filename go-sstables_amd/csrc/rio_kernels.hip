@@ -381,6 +381,7 @@ __device__ void init_state(const FrameParams& P) {
     st->pipe_next = 0;
     st->gz_resize = 0;
     st->gz_redo = 0;
+    st->lb_fused = 0;
     if (P.len < RIO_FILE_HEADER_BYTES) {
         st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;
         st->version = st->compression = 0;
@@ -609,6 +610,8 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
     return mask;
 }
 
+__device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t lane, uint32_t comp, ChunkSum s);
+
 // minimum waves per SIMD for k_walk (0 = the compiler's choice, 4 waves). Round 1: 6 waves with 60 B
 // spilled to scratch beat 5 (walk 0.210 -> 0.185 ms on C2). With the packed DPP fill scans and the
 // 32-bit LEB128 packing the spills landed in the fill loop: 6 waves 0.413 ms on C3, 5 waves (96
@@ -626,7 +629,20 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
     if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
     crc32c_tab_init(crct);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
+    uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
+    if (P.fused) {
+        // look-back path: chunks go to waves in the order the waves start (a ticket), so every chunk
+        // a wave waits for belongs to a wave that is already running; the wave taking the last ticket
+        // resets the counter for the next launch
+        uint32_t t = 0;
+        if (lane == 0) {
+            t = atomicAdd(reinterpret_cast<uint32_t*>(P.lb_ctl), 1u);
+            if (t == gridDim.x * kWalkWaves - 1)
+                __hip_atomic_store(reinterpret_cast<uint32_t*>(P.lb_ctl), 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(t, 0));
+    }
     uint32_t ver, comp;
     if (c >= P.n_chunks || file_header_status(P, ver, comp) != RIO_OK) return;  // wave-uniform
     WalkLds& L = W[wv];
@@ -761,8 +777,9 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         ws = we;
     }
     // 5. serial takeover where the chain left the candidates; the chunk summary
+    ChunkSum s;
     if (lane == 0) {
-        ChunkSum s = chunk_sum_empty(entry);
+        s = chunk_sum_empty(entry);
         s.count = (uint32_t)count;
         s.bytes = bytes;
         if (mode == 2)
@@ -770,6 +787,15 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         else if (entry != kNone)
             s.exit = p;  // the chain left the chunk (or ended at the file end) cleanly
         P.chunks[c] = s;
+    }
+    if (P.fused) {
+        // the summary to every lane (wave-uniform from here on)
+        s.entry = readlane64(s.entry, 0);
+        s.exit = readlane64(s.exit, 0);
+        s.bytes = readlane64(s.bytes, 0);
+        s.count = (uint32_t)__builtin_amdgcn_readlane((int)s.count, 0);
+        s.status = __builtin_amdgcn_readlane(s.status, 0);
+        walk_publish_place(P, c, lane, comp, s);
     }
 }
 
@@ -832,6 +858,40 @@ constexpr int kScanBlock = 256;
 
 __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]);
 
+// The fused walk's result (lb_ctl[1..4], this launch's tag): if the chain through the whole file held,
+// `write` (one thread) stores what scan_top would (record and byte totals, terminal status) and every
+// block skips the scan. A broken chain (a speculative entry that did not chain) takes the scan, whose
+// sequential repair then places the records again.
+__device__ bool fused_totals(const FrameParams& P, bool write) {
+    const uint64_t* T = P.lb_ctl + 1;
+    const uint32_t tag = P.lb_epoch;
+    for (int k = 0; k < 4; k++)
+        if ((uint32_t)(T[k] >> kLbValBits) != tag) return false;
+    auto val = [&](int k) {
+        const uint64_t v = T[k] & kLbMask;
+        return v == kLbMask ? kNone : v;
+    };
+    const uint64_t fl = val(3);
+    if (fl & 2) return false;  // broken
+    if (!write) return true;
+    ScanState* st = P.state;
+    st->n_records = val(1);
+    st->total_bytes = val(2);
+    if (fl & 1) {
+        const ChunkSum s = P.chunks[fl >> 2];
+        st->status = s.status;
+        st->status_offset = s.err_off;
+        st->det0 = s.det0;
+        st->det1 = s.det1;
+    } else {
+        st->status = RIO_EOF;  // chain ended exactly at the file end
+        st->status_offset = val(0);
+    }
+    if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
+    st->lb_fused = 1;
+    return true;
+}
+
 // Level 1: inclusive scan of 256 chunk runs per block in LDS (Hillis-Steele, 8 steps). The last
 // block to finish (arrival ticket) runs level 2 over the block runs: one launch for the scan.
 __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
@@ -841,6 +901,7 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
     const uint64_t c = (uint64_t)blockIdx.x * kScanBlock + t;
     if (P.state->hdr_status != RIO_OK) return;  // block-uniform
     if (P.redo && (!P.state->gz_redo || P.state->compression != P.redo)) return;  // another codec's redo round
+    if (P.fused && !P.redo && fused_totals(P, t == 0 && blockIdx.x == 0)) return;  // the walk placed everything
     RunSum v = c < P.n_chunks ? chunk_run(P, c) : run_identity();
     int cur = 0;
     buf[cur][t] = v;
@@ -998,11 +1059,233 @@ __device__ __forceinline__ bool snappy_single_literal(const uint8_t* p, uint64_t
     return snappy_literal_hdr(p, slen, len) != 0;
 }
 
-// Placement: one wave per chunk copies its owned scratch records to their global index (64
-// records per step, out_off by a wave prefix sum: coalesced stores instead of one thread's serial
-// record loop).
-// Its prologue also does what used to be two launches: the capacity check + sentinel out_off[n]
-// (block 0) and, on the device-resident path, the zero-tail test of a magic mismatch (grid-stride).
+// A chunk's records, placed: file records [base_idx, base_idx + owned) are chunk c's scratch slots
+// [0, owned); rec_off / rec_pay / out_off / flags / rec_desc at their global index, 64 records per wave
+// step, out_off by a wave prefix sum (coalesced stores instead of one thread's serial record loop).
+// `snappy`: look for a record that is not one literal element of its whole length (the probe stops at
+// the first). What the chunk found goes back to the caller, which merges it into ScanState.
+struct PlaceFlags {
+    uint64_t first_bad;  // first record flagged at framing (kNone: none)
+    uint64_t n_bad;
+    bool mixed;          // a Snappy record that is not one literal (or the probe was off)
+    bool huge;           // a stream or record past 32-bit sizes
+};
+
+__device__ PlaceFlags place_chunk(const FrameParams& P, uint64_t c, uint64_t base_idx, uint64_t base_bytes,
+                                  uint64_t owned, bool snappy, uint32_t lane) {
+    PlaceFlags fl{kNone, 0, false, false};
+    const uint64_t* so = P.scratch_off + c * P.slots;
+    const uint64_t* sl = P.scratch_len + c * P.slots;
+    const uint64_t* sp = P.scratch_pay + c * P.slots;
+    bool mixed = false, huge = false;
+    uint64_t carry = base_bytes;
+    // scratch of the next 64 records loaded before this step's stores: on CDNA vmcnt retires loads
+    // and stores in issue order, so a load issued after the stores would wait for them
+    uint64_t l_n = 0, ro_n = 0, pay_n = 0;
+    if (lane < owned) {
+        l_n = sl[lane];
+        ro_n = so[lane];
+        pay_n = sp[lane];
+    }
+    for (uint64_t k0 = 0; k0 < owned; k0 += 64) {
+        const uint64_t k = k0 + lane;
+        const bool v = k < owned;
+        const uint64_t l = l_n, ro = ro_n, pay = pay_n, len = v ? l & kLenMask : 0;
+        if (k + 64 < owned) {
+            l_n = sl[k + 64];
+            ro_n = so[k + 64];
+            pay_n = sp[k + 64];
+        }
+        uint64_t wsum;
+        const uint64_t excl = wave_excl_scan64(len, lane, wsum);
+        bool bad = false;
+        if (v) {
+            const uint64_t i = base_idx + k;
+            const uint64_t start = ro + (pay & 0xFF), slen = pay >> 8;
+            P.rec_off[i] = ro;
+            P.rec_pay[i] = pay;
+            P.out_off[i] = carry + excl;
+            const uint8_t fg = ((l & kNilBit) ? RIO_FLAG_NIL : 0) | ((l & kBadBit) ? RIO_FLAG_CORRUPT : 0) |
+                               ((l & kEofBit) ? RIO_FLAG_EOF : 0);
+            P.flags[i] = fg;
+            bad = (fg & (RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) != 0;  // failed at framing (stream length 0)
+            P.rec_desc[i] = make_uint4((uint32_t)start, (uint32_t)(start >> 32), (uint32_t)slen, (uint32_t)len);
+            huge = huge || (slen | len) > 0xFFFFFFFFull;
+            // a snappy stream that is exactly one literal element of the record's whole length
+            // (what golang/snappy emits for incompressible input) decodes as a copy
+            if (snappy && fg == 0) mixed |= !snappy_single_literal(P.file + start, slen, len);
+        }
+        const uint64_t bm = __ballot(bad);
+        if (bm) {
+            fl.n_bad += (uint64_t)__popcll(bm);
+            if (fl.first_bad == kNone) fl.first_bad = base_idx + k0 + (uint64_t)__builtin_ctzll(bm);
+        }
+        carry += wsum;
+        snappy = snappy && !__any(mixed);
+        mixed = mixed || !snappy;  // keep the wave's verdict
+    }
+    fl.mixed = __any(mixed);
+    fl.huge = __any(huge);
+    return fl;
+}
+
+// a chunk's flags into the file's state (one lane)
+__device__ __forceinline__ void merge_place_flags(const FrameParams& P, const PlaceFlags& f) {
+    ScanState* st = P.state;
+    if (f.first_bad != kNone) atomicMin((unsigned long long*)&st->first_bad, (unsigned long long)f.first_bad);
+    if (f.n_bad) atomicAdd((unsigned long long*)&st->n_bad, (unsigned long long)f.n_bad);
+    if (f.huge) atomicOr(&st->huge_streams, 1u);
+    // every writer stores the same 1: a plain store, not an atomic (17 k same-address atomics from
+    // the chunk waves of a 1 M-record file serialized at L2 and cost 0.35 ms)
+    if (f.mixed && st->compression == RIO_COMP_SNAPPY) st->any_mixed = 1u;
+}
+
+// ---- decoupled look-back (FrameParams::fused) -------------------------------------------------
+__device__ __forceinline__ uint64_t lb_word(uint32_t tag, uint64_t v) {
+    return ((uint64_t)tag << kLbValBits) | (v == kNone ? kLbMask : (v & kLbMask));
+}
+__device__ __forceinline__ uint64_t lb_val(uint64_t w) {
+    const uint64_t v = w & kLbMask;
+    return v == kLbMask ? kNone : v;
+}
+__device__ __forceinline__ bool lb_tagged(uint64_t w, uint32_t tag) { return (uint32_t)(w >> kLbValBits) == tag; }
+// agent-scope relaxed atomics: global_store / global_load with sc1 (write-through, L1 bypassed), so a
+// word another XCD stored is seen without a fence (MI355X_MICROARCH.md, inter-workgroup visibility)
+__device__ __forceinline__ void lb_st(uint64_t* p, uint64_t w) {
+    __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_ld(uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_flags(const RunSum& r) {
+    return (uint64_t)r.term | ((uint64_t)r.broken << 1) | (r.term_chunk << 2);
+}
+__device__ __forceinline__ void lb_unflag(RunSum& r, uint64_t f) {
+    r.term = (uint32_t)(f & 1);
+    r.broken = (uint32_t)((f >> 1) & 1);
+    r.term_chunk = f >> 2;
+}
+
+// bounded waits: a predecessor that never publishes (it cannot happen; a bug would hang the GPU) turns
+// into a broken chain after ~1 s, and the two-launch scan then frames the file
+#ifndef RIO_LB_SPIN_MAX
+#define RIO_LB_SPIN_MAX (1u << 22)
+#endif
+
+// Chunk c of the fused walk: publish its run, find the exclusive prefix over chunks 0..c-1 (the
+// nearest predecessor's inclusive prefix, composed with the runs of the chunks between, which lanes
+// read 64 at a time), publish the inclusive prefix, and place the chunk's records if the chain enters
+// it at its speculative entry; the last chunk publishes the file's run for k_scan_blocks.
+__device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t lane, uint32_t comp, ChunkSum s) {
+    const uint32_t tag = P.lb_epoch;
+    uint64_t* const me = P.lb + c * kLbWords;
+    RunSum A;  // this chunk's run (chunk_run)
+    A.key = s.entry;
+    A.out = s.exit;
+    A.cnt = s.count;
+    A.bytes = s.bytes;
+    A.ce = chunk_end(P, c);
+    A.term = s.status != RIO_OK;
+    A.broken = 0;
+    A.term_chunk = c;
+    {
+        const uint64_t v = lane == 0 ? A.key : lane == 1 ? A.out : lane == 2 ? A.cnt : lane == 3 ? A.bytes : lb_flags(A);
+        if (lane < 5) lb_st(me + lane, lb_word(tag, v));
+    }
+    RunSum E = run_identity();  // exclusive prefix
+    if (c > 0) {
+        RunSum acc = run_identity();  // runs of the chunks right of the current window, composed
+        uint64_t hi = c;              // window: chunks hi - 64 .. hi - 1 (lane l: chunk hi - 1 - l)
+        uint32_t spins = 0;
+        for (;;) {
+            const bool live = hi >= (uint64_t)lane + 1;
+            const uint64_t j = hi - 1 - lane;
+            uint64_t w[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) w[k] = 0;
+            bool hasA = false, hasP = !live;  // before chunk 0: the empty prefix
+            if (live) {
+                uint64_t* q = P.lb + j * kLbWords;
+#pragma unroll
+                for (int k = 0; k < 9; k++) w[k] = lb_ld(q + k);
+                hasA = lb_tagged(w[0], tag) && lb_tagged(w[1], tag) && lb_tagged(w[2], tag) && lb_tagged(w[3], tag) &&
+                       lb_tagged(w[4], tag);
+                hasP = lb_tagged(w[5], tag) && lb_tagged(w[6], tag) && lb_tagged(w[7], tag) && lb_tagged(w[8], tag);
+            }
+            const uint64_t pm = __ballot(hasP), am = __ballot(hasA);
+            const uint32_t kp = lane_ffs(pm);  // nearest lane with a prefix (64: none in the window)
+            const uint64_t need = kp >= 64 ? ~0ull : ((1ull << kp) - 1);
+            if ((am & need) != need) {  // a chunk between has not published its run yet
+                if (++spins >= RIO_LB_SPIN_MAX) {
+                    E.ce = A.ce;
+                    E.key = RIO_FILE_HEADER_BYTES;
+                    E.broken = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+                continue;
+            }
+            RunSum X = run_identity();
+            if (kp < 64 && hi >= (uint64_t)kp + 1) {  // lane kp's inclusive prefix (not the empty one)
+                const uint64_t jp = hi - 1 - kp;
+                X.key = RIO_FILE_HEADER_BYTES;
+                X.out = lb_val(readlane64(w[5], kp));
+                X.cnt = lb_val(readlane64(w[6], kp));
+                X.bytes = lb_val(readlane64(w[7], kp));
+                X.ce = chunk_end(P, jp);
+                lb_unflag(X, lb_val(readlane64(w[8], kp)));
+            }
+            for (int l = (int)(kp < 64 ? kp : 64) - 1; l >= 0; l--) {
+                RunSum Y;
+                Y.key = lb_val(readlane64(w[0], (uint32_t)l));
+                Y.out = lb_val(readlane64(w[1], (uint32_t)l));
+                Y.cnt = lb_val(readlane64(w[2], (uint32_t)l));
+                Y.bytes = lb_val(readlane64(w[3], (uint32_t)l));
+                Y.ce = chunk_end(P, hi - 1 - (uint64_t)l);
+                lb_unflag(Y, lb_val(readlane64(w[4], (uint32_t)l)));
+                X = combine(X, Y);
+            }
+            acc = combine(X, acc);
+            if (kp < 64) break;
+            hi -= 64;
+        }
+        if (!E.broken) E = acc;
+    }
+    const RunSum I = c > 0 ? combine(E, A) : A;  // inclusive prefix (chunk 0's run is keyed at 8)
+    {
+        const uint64_t v = lane == 5 ? I.out : lane == 6 ? I.cnt : lane == 7 ? I.bytes : lb_flags(I);
+        if (lane >= 5 && lane < 9) lb_st(me + lane, lb_word(tag, v));
+    }
+    // ownership as k_place decides it: the chain (unbroken, not terminated) enters chunk c at its entry
+    ChunkPlace pl;
+    pl.base_idx = E.cnt;
+    pl.base_bytes = E.bytes;
+    pl.owned = 0;
+    if (c == 0)
+        pl.owned = s.count;
+    else if (!E.broken && !E.term && s.entry != kNone && E.out == s.entry)
+        pl.owned = s.count;
+    if (lane == 0) P.place[c] = pl;
+    PlaceFlags f{kNone, 0, false, false};
+    if (pl.owned && pl.base_idx + pl.owned <= P.rec_cap) {
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's scratch stores before it reads them back
+        f = place_chunk(P, c, pl.base_idx, pl.base_bytes, pl.owned, comp == RIO_COMP_SNAPPY, lane);
+    }
+    if (lane == 0) {  // for k_place (next launch): plain stores
+        me[9] = f.first_bad;
+        me[10] = f.n_bad;
+        me[11] = (f.mixed ? 1u : 0u) | (f.huge ? 2u : 0u);
+    }
+    if (c + 1 == P.n_chunks) {  // the file's run
+        const uint64_t v = lane == 0 ? I.out : lane == 1 ? I.cnt : lane == 2 ? I.bytes : lb_flags(I);
+        if (lane < 4) lb_st(P.lb_ctl + 1 + lane, lb_word(tag, v));
+    }
+}
+
+// Placement: one wave per chunk (place_chunk). Its prologue also does what used to be two launches:
+// the capacity check + sentinel out_off[n] (block 0) and, on the device-resident path, the zero-tail
+// test of a magic mismatch (grid-stride). When the walk already placed the records (look-back path,
+// ScanState::lb_fused), a wave only merges its chunk's flags.
 __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -1023,6 +1306,13 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
         if (__any(nz != 0) && lane == 0) atomicOr(&st->zero_nonzero, 1u);
     }
     if (c >= P.n_chunks) return;  // wave-uniform
+    if (st->lb_fused && !P.redo) {
+        if (lane == 0) {
+            const uint64_t* w = P.lb + c * kLbWords;
+            merge_place_flags(P, PlaceFlags{w[9], w[10], (w[11] & 1) != 0, (w[11] & 2) != 0});
+        }
+        return;
+    }
     ChunkPlace pl;
     if (st->slow) {
         pl = P.place[c];
@@ -1047,59 +1337,10 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     }
     if (pl.owned == 0) return;
     if (pl.base_idx + pl.owned > P.rec_cap || st->n_records > P.rec_cap) return;
-    const uint64_t* so = P.scratch_off + c * P.slots;
-    const uint64_t* sl = P.scratch_len + c * P.slots;
-    const uint64_t* sp = P.scratch_pay + c * P.slots;
     // once any wave has found a mixed record the file takes k_snappy_pipe: later waves skip the probe
-    // (and within a wave: the probe stops once one of its lanes has found a mixed record)
-    bool snappy = st->compression == RIO_COMP_SNAPPY && !*(volatile const uint32_t*)&st->any_mixed;
-    bool mixed = false;
-    uint64_t carry = pl.base_bytes;
-    // scratch of the next 64 records loaded before this step's stores: on CDNA vmcnt retires loads
-    // and stores in issue order, so a load issued after the stores would wait for them
-    uint64_t l_n = 0, ro_n = 0, pay_n = 0;
-    if (lane < pl.owned) {
-        l_n = sl[lane];
-        ro_n = so[lane];
-        pay_n = sp[lane];
-    }
-    for (uint64_t k0 = 0; k0 < pl.owned; k0 += 64) {
-        const uint64_t k = k0 + lane;
-        const bool v = k < pl.owned;
-        const uint64_t l = l_n, ro = ro_n, pay = pay_n, len = v ? l & kLenMask : 0;
-        if (k + 64 < pl.owned) {
-            l_n = sl[k + 64];
-            ro_n = so[k + 64];
-            pay_n = sp[k + 64];
-        }
-        uint64_t wsum;
-        const uint64_t excl = wave_excl_scan64(len, lane, wsum);
-        if (v) {
-            const uint64_t i = pl.base_idx + k;
-            const uint64_t start = ro + (pay & 0xFF), slen = pay >> 8;
-            P.rec_off[i] = ro;
-            P.rec_pay[i] = pay;
-            P.out_off[i] = carry + excl;
-            const uint8_t fl = ((l & kNilBit) ? RIO_FLAG_NIL : 0) | ((l & kBadBit) ? RIO_FLAG_CORRUPT : 0) |
-                               ((l & kEofBit) ? RIO_FLAG_EOF : 0);
-            P.flags[i] = fl;
-            if (fl & (RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) {  // failed at framing (stream length 0)
-                atomicMin((unsigned long long*)&P.state->first_bad, (unsigned long long)i);
-                atomicAdd((unsigned long long*)&P.state->n_bad, 1ull);
-            }
-            P.rec_desc[i] = make_uint4((uint32_t)start, (uint32_t)(start >> 32), (uint32_t)slen, (uint32_t)len);
-            if ((slen | len) > 0xFFFFFFFFull) atomicOr(&P.state->huge_streams, 1u);
-            // a snappy stream that is exactly one literal element of the record's whole length
-            // (what golang/snappy emits for incompressible input) decodes as a copy
-            if (snappy && fl == 0) mixed |= !snappy_single_literal(P.file + start, slen, len);
-        }
-        carry += wsum;
-        snappy = snappy && !__any(mixed);
-        mixed = mixed || !snappy;  // keep the wave's verdict for the store below
-    }
-    // every writer stores the same 1: a plain store, not an atomic (17 k same-address atomics from
-    // the chunk waves of a 1 M-record file serialized at L2 and cost 0.35 ms)
-    if (st->compression == RIO_COMP_SNAPPY && __any(mixed) && lane == 0) P.state->any_mixed = 1u;
+    const bool snappy = st->compression == RIO_COMP_SNAPPY && !*(volatile const uint32_t*)&st->any_mixed;
+    const PlaceFlags f = place_chunk(P, c, pl.base_idx, pl.base_bytes, pl.owned, snappy, lane);
+    if (lane == 0) merge_place_flags(P, f);
 }
 
 __global__ void __launch_bounds__(256) k_zero(FrameParams P) {

@@ -999,6 +999,7 @@ __device__ __forceinline__ bool pair_parse(const FrameParams& P, uint64_t r0, ui
         for (uint32_t spin = 0; p >= rd + kQ; spin++) {  // rare: the emitter is kQ pieces behind
             __builtin_amdgcn_s_sleep(1);
             rd = lds_ld(&S.cnt[1]);
+            (void)spin;
 #if RIO_PAIR_DEBUG
             if (spin == (1u << 22)) {
                 if (lane == 0)
@@ -1082,6 +1083,7 @@ __device__ __forceinline__ void pair_emit(const FrameParams& P, uint64_t r0, uin
             have = lds_ld(&S.cnt[0]);
             fin = lds_ld(&S.cnt[2]);
             if (m >= have && m < fin) __builtin_amdgcn_s_sleep(1);
+            (void)spin;
 #if RIO_PAIR_DEBUG
             if (spin == (1u << 22)) {
                 if (lane == 0)

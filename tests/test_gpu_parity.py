@@ -61,15 +61,20 @@ def test_repairs_happen_and_stay_exact():
     assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), "embedded")
 
 
+@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("chunk", [64, 256, 1024, 4096, 65536])
-def test_chunk_size_independent(chunk, monkeypatch):
-    """The result does not depend on the framing chunk size (speculation granularity)."""
+def test_chunk_size_independent(chunk, fused, monkeypatch):
+    """The result does not depend on the framing chunk size (speculation granularity), with the walk
+    placing the records through its look-back (RIO_FUSED=1, the default: at 64-byte chunks the files
+    have thousands of chunks, so look-back windows of 64 and broken speculations are crossed) or the
+    two-launch scan and placement (RIO_FUSED=0)."""
     import ctypes
 
     from recordio import _lib as L
     from recordio.device import DeviceDecoder, to_device_file
 
     monkeypatch.setenv("RIO_CHUNK_BYTES", str(chunk))
+    monkeypatch.setenv("RIO_FUSED", str(fused))
     h = ctypes.c_void_p()
     assert L.lib().rio_ctx_create(0, ctypes.byref(h)) == 0
     try:
