@@ -171,7 +171,7 @@ struct rio_ctx {
     uint64_t chunk_bytes = 32768;
     uint64_t coop_min = ~0ull >> 8;
     uint32_t pair = 0;  // Snappy lane-decoder files on k_snappy_pair (RIO_SNAPPY_PAIR)
-    uint32_t fused = 1;  // device decodes place the records in the walk (RIO_FUSED=0: the two-launch scan)
+    uint32_t fused = 0;  // RIO_FUSED=1: device decodes place the records in the walk (look-back)
     hipEvent_t* next_events() {
         if (ev.empty()) return nullptr;
         return ev[ev_cursor++ % ev.size()].data();
@@ -299,7 +299,8 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
     c->coop_min = env_u64("RIO_COOP_MIN", ~0ull >> 8);  // k_snappy_coop: wide files only
     c->pair = (uint32_t)env_u64("RIO_SNAPPY_PAIR", 0);  // two-wave lane decoder
-    c->fused = (uint32_t)env_u64("RIO_FUSED", 1);       // look-back placement in the walk
+    // look-back placement in the walk: opt-in until it has run on the GPU
+    c->fused = (uint32_t)env_u64("RIO_FUSED", 0);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RIO_ERR_HIP;

@@ -65,9 +65,9 @@ def test_repairs_happen_and_stay_exact():
 @pytest.mark.parametrize("chunk", [64, 256, 1024, 4096, 65536])
 def test_chunk_size_independent(chunk, fused, monkeypatch):
     """The result does not depend on the framing chunk size (speculation granularity), with the walk
-    placing the records through its look-back (RIO_FUSED=1, the default: at 64-byte chunks the files
-    have thousands of chunks, so look-back windows of 64 and broken speculations are crossed) or the
-    two-launch scan and placement (RIO_FUSED=0)."""
+    placing the records through its look-back (RIO_FUSED=1: at 64-byte chunks the files have thousands
+    of chunks, so look-back windows of 64 and broken speculations are crossed) or the two-launch scan
+    and placement (RIO_FUSED=0, the default)."""
     import ctypes
 
     from recordio import _lib as L
