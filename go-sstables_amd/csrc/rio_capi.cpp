@@ -244,26 +244,28 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     HIP_TRY(A.info.ensure(sizeof(rio_file_info)));
     HIP_TRY(ctx->sink.ensure(kSinkBytes));
     HIP_TRY(A.fail_lanes.ensure(2 * kFailLanes * sizeof(uint64_t)));
-    {
+    P.fused = 0;
+    if (ctx->fused) {
         // look-back words (fused walk): every launch tags its words with a new epoch, so a word from an
         // earlier launch never matches; fresh buffers, and every kLbTagMask launches, are zeroed first
-        // (tag 0 is never used) with the host waiting, so no launch sees the old bytes
+        // (tag 0 is never used) once the previous call is done, with the host waiting, so no launch sees
+        // the old bytes
         void* lb0 = A.lb.p;
         void* ctl0 = A.lb_ctl.p;
         HIP_TRY(A.lb.ensure(nc * kLbWords * sizeof(uint64_t)));
         HIP_TRY(A.lb_ctl.ensure(8 * sizeof(uint64_t)));
         if (A.lb.p != lb0 || A.lb_ctl.p != ctl0 || A.lb_epoch >= kLbTagMask) A.lb_epoch = 0;
         if (A.lb_epoch == 0) {
+            if (ctx->order_valid) HIP_TRY(hipEventSynchronize(ctx->order_ev));
             HIP_TRY(hipMemsetAsync(A.lb.p, 0, A.lb.cap, ctx->stream));
             HIP_TRY(hipMemsetAsync(A.lb_ctl.p, 0, A.lb_ctl.cap, ctx->stream));
             HIP_TRY(hipStreamSynchronize(ctx->stream));
         }
         A.lb_epoch++;
+        P.lb = A.lb.as<uint64_t>();
+        P.lb_ctl = A.lb_ctl.as<uint64_t>();
+        P.lb_epoch = A.lb_epoch;
     }
-    P.lb = A.lb.as<uint64_t>();
-    P.lb_ctl = A.lb_ctl.as<uint64_t>();
-    P.lb_epoch = A.lb_epoch;
-    P.fused = 0;
     P.sink = ctx->sink.as<uint8_t>();
     P.fail_lanes = A.fail_lanes.as<uint64_t>();
     P.scratch_off = A.scratch_off.as<uint64_t>();
@@ -402,7 +404,7 @@ extern "C" int rio_ctx_reserve(rio_ctx* ctx, uint64_t max_file_len, uint64_t max
 // the walk places the records (look-back) when the decode follows in the same call and every value
 // fits the look-back words' 40 bits
 static uint32_t fused_ok(const rio_ctx* ctx, const FrameParams& P) {
-    return ctx->fused && P.len < kLbMask && P.out_cap < kLbMask && P.rec_cap < kLbMask ? 1u : 0u;
+    return ctx->fused && P.lb && P.len < kLbMask && P.out_cap < kLbMask && P.rec_cap < kLbMask ? 1u : 0u;
 }
 
 extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
