@@ -1174,9 +1174,10 @@ static int ensure_on_device(rio_reader* r) {
 // record bytes of a kernel-path result: valid until this thread's next ReadNextAt / SeekNext
 static thread_local std::vector<uint8_t> tl_rec;
 
-// the single-record kernels (ReadNextAt at `offset`, or SeekNext scanning from it)
+// the single-record kernels (ReadNextAt at `offset`, or SeekNext scanning from it); *res_out gets the
+// kernel's result (a gzip / lzw record it located but did not expand: payload_off, len)
 static int readat_kernel(rio_reader* r, uint64_t offset, bool seek, uint64_t seek_len, uint64_t* ro_out,
-                         const uint8_t** data, uint64_t* len, int* is_nil) {
+                         const uint8_t** data, uint64_t* len, int* is_nil, ReadAtResult* res_out = nullptr) {
     std::lock_guard<std::mutex> g(r->mu);
     if (!r->open || r->closed) return RIO_ERR_STATE;
     std::lock_guard<std::mutex> cg(r->ctx->mu);
@@ -1187,6 +1188,7 @@ static int readat_kernel(rio_reader* r, uint64_t offset, bool seek, uint64_t see
     rc = read_at_impl(r->ctx, r->dfile.as<uint8_t>(), r->size, offset, seek, seek_len, &res, seek ? &ro : nullptr);
     if (rc) return rc;
     if (ro_out) *ro_out = ro;
+    if (res_out) *res_out = res;
     tl_det.d0 = res.det0;
     tl_det.d1 = res.det1;
     if (res.status != RIO_OK) return res.status;
@@ -1195,6 +1197,45 @@ static int readat_kernel(rio_reader* r, uint64_t offset, bool seek, uint64_t see
     tl_rec.resize(res.len + 1);
     if (!res.nil && res.len) HIP_TRY(hipMemcpy(tl_rec.data(), r->ctx->readat_out.p, res.len, hipMemcpyDeviceToHost));
     if (data) *data = tl_rec.data();
+    return RIO_OK;
+}
+
+// A gzip / lzw record the whole-file decode never reached (MMapReader.ReadNextAt decodes any record
+// start, mmap_reader.go:130-203, e.g. one after a header that fails its CRC, where FileReader stops):
+// the single-record kernel located it (res: payload_off, len = payload bytes), and it is decoded here
+// as a file of its own (the 8-byte file header, then the record's header and payload) through the
+// whole-file path on the reader's context: the same inflate / lzw kernels, Go's multistream and size
+// rules included. ReadNextAt's result for it: the record, or the codec's error class.
+static thread_local std::vector<uint8_t> tl_x_out, tl_x_flags;
+static thread_local std::vector<uint64_t> tl_x_off, tl_x_rec;
+static int readat_expand(rio_reader* r, uint64_t rec, const ReadAtResult& res, const uint8_t** data, uint64_t* len,
+                         int* is_nil) {
+    const uint64_t end = res.payload_off + res.len;
+    if (!r->map || res.nil || res.len == 0 || res.payload_off <= rec || end > r->size) return RIO_ERR_UNSUPPORTED;
+    std::vector<uint8_t> img(RIO_FILE_HEADER_BYTES + (end - rec));
+    memcpy(img.data(), r->map, RIO_FILE_HEADER_BYTES);
+    memcpy(img.data() + RIO_FILE_HEADER_BYTES, r->map + rec, end - rec);
+    std::lock_guard<std::mutex> g(r->mu);
+    if (!r->open || r->closed) return RIO_ERR_STATE;
+    std::lock_guard<std::mutex> cg(r->ctx->mu);
+    rio_file_info fi{};
+    int rc = rio_frame(r->ctx, img.data(), img.size(), &fi);
+    if (rc) return rc;
+    if (fi.n_records == 0) return RIO_ERR_UNSUPPORTED;  // (the kernel framed it: not reached)
+    const uint64_t n = fi.n_records;
+    tl_x_out.resize(fi.total_out_bytes + 1);
+    tl_x_off.resize(n + 1);
+    tl_x_rec.resize(n);
+    tl_x_flags.resize(n);
+    rc = rio_decode(r->ctx, tl_x_out.data(), fi.total_out_bytes, tl_x_off.data(), tl_x_rec.data(), tl_x_flags.data(), n,
+                    &fi);
+    if (rc) return rc;
+    if (fi.n_records == 0 || fi.status == RIO_ERR_UNSUPPORTED) return RIO_ERR_UNSUPPORTED;
+    if (tl_x_flags[0] & RIO_FLAG_CORRUPT) return RIO_ERR_DECOMPRESS;
+    if (tl_x_flags[0] & RIO_FLAG_EOF) return RIO_EOF_CODEC;
+    if (is_nil) *is_nil = 0;
+    if (len) *len = tl_x_off[1] - tl_x_off[0];
+    if (data) *data = tl_x_out.data() + tl_x_off[0];
     return RIO_OK;
 }
 
@@ -1215,7 +1256,11 @@ extern "C" int rio_reader_read_next_at(rio_reader* r, uint64_t offset, const uin
     const ReadAtIndex* x = readat_index(r);
     const uint64_t i = x->find(offset);
     if (i < x->n) return x->record(i, data, len, is_nil);
-    return readat_kernel(r, offset, false, 0, nullptr, data, len, is_nil);
+    ReadAtResult res{};
+    const int rc = readat_kernel(r, offset, false, 0, nullptr, data, len, is_nil, &res);
+    const bool expand = r->compression == RIO_COMP_GZIP || r->compression == RIO_COMP_LZW;
+    if (rc == RIO_ERR_UNSUPPORTED && expand) return readat_expand(r, offset, res, data, len, is_nil);
+    return rc;
 }
 
 extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* rec_offset, const uint8_t** data,
@@ -1241,19 +1286,27 @@ extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* re
     }
     for (;;) {
         uint64_t ro = 0;
-        const int rc = readat_kernel(r, s, true, seek_len, &ro, data, len, is_nil);
+        ReadAtResult res{};
+        const int rc = readat_kernel(r, s, true, seek_len, &ro, data, len, is_nil, &res);
         if (rec_offset) *rec_offset = ro;
         tl_det.off = rc == RIO_ERR_INVALID_OFFSET ? offset : ro;
         // gzip / lzw: the kernel stops at a trial whose payload needs expanding; a record start is served
-        // from the decoded index (an io.EOF-class one continues the scan), anything else is handed back
+        // from the decoded index, any other record is expanded on its own (readat_expand); an io.EOF-class
+        // trial (an empty gzip payload) continues the scan as mmap_reader.go:105-114 does
         const bool expand = r->compression == RIO_COMP_GZIP || r->compression == RIO_COMP_LZW;
-        const uint64_t i = rc == RIO_ERR_UNSUPPORTED && expand ? x->find(ro) : x->n;
-        if (i == x->n) return rc;
-        if (x->flags[i] & RIO_FLAG_EOF) {
+        if (rc != RIO_ERR_UNSUPPORTED || !expand) return rc;
+        const uint64_t i = x->find(ro);
+        int rx;
+        if (i < x->n) {
+            rx = x->record(i, data, len, is_nil);
+        } else {
+            rx = readat_expand(r, ro, res, data, len, is_nil);
+        }
+        if (rx == RIO_EOF_CODEC) {
             s = ro + 3;
             continue;
         }
-        return x->record(i, data, len, is_nil);
+        return rx;
     }
 }
 
