@@ -55,7 +55,10 @@ hipError_t launch_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t*
                           ReadAtResult* res, hipStream_t s);
 int build_seek_map(const uint8_t* f, uint64_t len, const uint64_t* rec_off, const uint8_t* flags, uint64_t n,
                    std::vector<uint64_t>& P, std::vector<uint64_t>& R, hipStream_t s);
-constexpr uint64_t kSeekOther = ~0ull >> 1;  // rio_kernels.hip
+hipError_t launch_index_search_view(const uint8_t* out, const uint64_t* out_off, const uint8_t* flags, uint64_t n,
+                                    const uint64_t* P, uint64_t K, const uint64_t* R, uint64_t len, const uint8_t* keys,
+                                    const uint64_t* key_off, uint64_t nq, const uint32_t* perm, rio_index_hit* hits,
+                                    hipStream_t s);
 hipError_t launch_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64_t seek_len, uint8_t* out,
                             uint64_t out_cap, ReadAtResult* res, uint64_t* rec_off, hipStream_t s);
 }  // namespace rio
@@ -1277,7 +1280,7 @@ extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* re
     // marker byte, so with seekLen 3 every marker ends the scan in io.EOF (k_seek_next reproduces it)
     if (seek_len >= 4 && s <= r->size && x->n) {
         const uint64_t k = (uint64_t)(std::lower_bound(x->P.begin(), x->P.end(), s) - x->P.begin());
-        if (k < x->P.size() && x->R[k] != kSeekOther) {
+        if (k < x->P.size() && x->R[k] < x->n) {  // else the single-record kernel answers (kSeekOther / io.EOF walks)
             const uint64_t i = x->R[k];
             if (rec_offset) *rec_offset = x->rec_off[i];
             tl_det.off = x->rec_off[i];
@@ -1500,7 +1503,57 @@ struct rio_index {
     rio_ctx* ctx = nullptr;
     uint64_t len = 0;
     DevBuf file, keys, key_off, hits;
+    // a compressed index.rio: its decoded records and SeekNext map (k_index_search_view)
+    bool view = false;
+    uint64_t n = 0, K = 0;
+    DevBuf v_out, v_off, v_rec, v_flags, v_P, v_R;
 };
+
+// The view of a compressed index (DiskKeyIndex over rProto.NewMMapProtoReaderWithPath, which decompresses
+// every record it reads, sstables/disk_key_index.go:173): the FileReader sequence of records (rio_frame +
+// rio_decode on the index's context) and the SeekNext map over the file (build_seek_map), all resident.
+static int index_build_view(rio_index* x, const uint8_t* file, uint64_t len) {
+    rio_ctx* ctx = x->ctx;
+    std::lock_guard<std::mutex> cg(ctx->mu);  // reader handles sharing the context take it around device use
+    rio_file_info fi{};
+    int rc = rio_frame(ctx, file, len, &fi);
+    if (rc) return rc;
+    if (fi.status == RIO_ERR_VERSION || fi.status == RIO_ERR_COMPRESSION_TYPE || fi.status == RIO_ERR_UNSUPPORTED ||
+        fi.status == RIO_ERR_SHORT_FILE_HEADER)
+        return RIO_OK;  // no view: the kernel reports the header's status per query
+    const uint64_t n = fi.n_records, nb = fi.total_out_bytes;
+    std::vector<uint8_t> out(nb + 1), flags(n + 1);
+    std::vector<uint64_t> off(n + 1), rec(n + 1);
+    rc = rio_decode(ctx, out.data(), nb, off.data(), rec.data(), flags.data(), n, &fi);
+    if (rc) return rc;
+    const uint64_t m = std::min<uint64_t>(fi.n_records, n);
+    HIP_TRY(x->v_out.ensure(nb + 16));
+    HIP_TRY(x->v_off.ensure((m + 1) * 8));
+    HIP_TRY(x->v_rec.ensure((m + 1) * 8));
+    HIP_TRY(x->v_flags.ensure(m + 8));
+    if (nb) HIP_TRY(hipMemcpyAsync(x->v_out.p, out.data(), nb, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(x->v_off.p, off.data(), (m + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (m) {
+        HIP_TRY(hipMemcpyAsync(x->v_rec.p, rec.data(), m * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(x->v_flags.p, flags.data(), m, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    std::vector<uint64_t> P, R;
+    if (build_seek_map(x->file.as<uint8_t>(), len, x->v_rec.as<uint64_t>(), x->v_flags.as<uint8_t>(), m, P, R,
+                       ctx->stream))
+        return RIO_ERR_HIP;
+    HIP_TRY(x->v_P.ensure(P.size() * 8 + 8));
+    HIP_TRY(x->v_R.ensure(R.size() * 8 + 8));
+    if (!P.empty()) {
+        HIP_TRY(hipMemcpyAsync(x->v_P.p, P.data(), P.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(x->v_R.p, R.data(), R.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    x->n = m;
+    x->K = P.size();
+    x->view = true;
+    return RIO_OK;
+}
 
 extern "C" int rio_index_open(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_index** out) {
     if (!ctx || !out || (!file && len)) return RIO_ERR_ARG;
@@ -1513,8 +1566,13 @@ extern "C" int rio_index_open(rio_ctx* ctx, const uint8_t* file, uint64_t len, r
     if (!rc) rc = h2d_staged(ctx, x->file.p, file, len);
     if (!rc && hipMemsetAsync(x->file.as<uint8_t>() + len, 0, RIO_DEVICE_PAD, ctx->stream) != hipSuccess) rc = RIO_ERR_HIP;
     if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = RIO_ERR_HIP;
+    if (!rc && len >= RIO_FILE_HEADER_BYTES) {
+        const uint32_t v = file[0] | (uint32_t)file[1] << 8 | (uint32_t)file[2] << 16 | (uint32_t)file[3] << 24;
+        const uint32_t c = file[4] | (uint32_t)file[5] << 8 | (uint32_t)file[6] << 16 | (uint32_t)file[7] << 24;
+        if (v >= RIO_VERSION3 && v <= RIO_VERSION4 && c != RIO_COMP_NONE && c <= RIO_COMP_LZW) rc = index_build_view(x, file, len);
+    }
     if (rc) {
-        x->file.release();
+        for (DevBuf* b : {&x->file, &x->v_out, &x->v_off, &x->v_rec, &x->v_flags, &x->v_P, &x->v_R}) b->release();
         delete x;
         return rc;
     }
@@ -1536,9 +1594,15 @@ extern "C" int rio_index_search(rio_index* x, const uint8_t* keys, const uint64_
     int rc = kb ? h2d_staged(ctx, x->keys.p, keys, kb) : RIO_OK;
     if (!rc) rc = h2d_staged(ctx, x->key_off.p, reinterpret_cast<const uint8_t*>(key_off), (n + 1) * 8);
     if (rc) return rc;
-    rc = rio_device_index_search(ctx, x->file.as<uint8_t>(), x->len, 4096, x->keys.as<uint8_t>(),
-                                 x->key_off.as<uint64_t>(), n, x->hits.as<rio_index_hit>(), nullptr);
-    if (rc) return rc;
+    if (x->view) {
+        HIP_TRY(launch_index_search_view(x->v_out.as<uint8_t>(), x->v_off.as<uint64_t>(), x->v_flags.as<uint8_t>(), x->n,
+                                         x->v_P.as<uint64_t>(), x->K, x->v_R.as<uint64_t>(), x->len, x->keys.as<uint8_t>(),
+                                         x->key_off.as<uint64_t>(), n, nullptr, x->hits.as<rio_index_hit>(), ctx->stream));
+    } else {
+        rc = rio_device_index_search(ctx, x->file.as<uint8_t>(), x->len, 4096, x->keys.as<uint8_t>(),
+                                     x->key_off.as<uint64_t>(), n, x->hits.as<rio_index_hit>(), nullptr);
+        if (rc) return rc;
+    }
     return d2h_staged(ctx, reinterpret_cast<uint8_t*>(hits), x->hits.p, n * sizeof(rio_index_hit));
 }
 
@@ -1546,10 +1610,9 @@ extern "C" void rio_index_free(rio_index* x) {
     if (!x) return;
     hipSetDevice(x->ctx->device);
     hipStreamSynchronize(x->ctx->stream);
-    x->file.release();
-    x->keys.release();
-    x->key_off.release();
-    x->hits.release();
+    for (DevBuf* b : {&x->file, &x->keys, &x->key_off, &x->hits, &x->v_out, &x->v_off, &x->v_rec, &x->v_flags, &x->v_P,
+                      &x->v_R})
+        b->release();
     delete x;
 }
 

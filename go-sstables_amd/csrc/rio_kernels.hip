@@ -1666,14 +1666,15 @@ __global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64
 // of >= 4 bytes the walk does not depend on where windows start (a marker cut by a window end is
 // re-read from its start). So the answer from offset s is fixed by the first 0x91 at or after s:
 // P = every 0x91 position in file order, R[k] = the walk's end from P[k] — a record j of the decoded
-// sequence (its trial is record j, answered from the decoded arena) or kSeekOther (a trial outside
-// the sequence that ends the walk, a partial marker at the file end, or a walk that runs off the
-// last 0x91: the single-record kernel answers those). Built once per reader:
+// sequence (its trial is record j, answered from the decoded arena), kSeekEof (the walk passes the
+// last 0x91 and the scan reads to the file end: io.EOF) or kSeekOther (a trial outside the sequence
+// that ends the walk, or a partial marker at the file end: the single-record kernel answers those). Built once per reader:
 //   k_count91 / k_scan_segs / k_list91: P (a wave per 4 KiB segment, ballot-free lane prefix);
 //   k_seek_step: each position's own step (terminal, or the index of the next 0x91 visited);
 //   k_seek_jump: pointer jumping to each walk's end (log2 of the longest walk rounds).
 // ------------------------------------------------------------------------------------------
 constexpr uint64_t kSeekOther = ~0ull >> 1;
+constexpr uint64_t kSeekEof = kSeekOther - 1;  // the walk passed the last 0x91 without a trial ending it: io.EOF
 constexpr uint64_t kSeekTerm = 1ull << 63;
 constexpr uint32_t kSegBytes = 4096;
 
@@ -1806,7 +1807,7 @@ __global__ void __launch_bounds__(256) k_seek_step(const uint8_t* f, uint64_t le
         }
         if (c) {
             const uint64_t nk = lower_u64(P, K, c);
-            out = nk < K ? nk : (kSeekTerm | kSeekOther);  // no 0x91 left: the walk reaches the file end
+            out = nk < K ? nk : (kSeekTerm | kSeekEof);  // no 0x91 left: the scan reads to the file end
         }
         step[k] = out;
     }
@@ -1958,6 +1959,85 @@ __global__ void __launch_bounds__(256) k_index_search(
         out.status = e;
         hits[q] = out;
     }
+}
+
+// DiskKeyIndex lookups on a compressed index.rio (rio_index_open builds the view): the same binarySearch
+// per query lane, each probe findAt(h) answered from the decoded records and the SeekNext map instead
+// of the raw file: the first 0x91 at or after h fixes SeekNext's answer (windows of 4096 bytes), which
+// is record R[k] (its IndexEntry parsed from the decoded arena), io.EOF (no 0x91 left, or a walk that
+// runs past the last one), the record's codec error, or a trial outside the decoded sequence (handed
+// back: RIO_ERR_UNSUPPORTED for that query).
+__device__ __forceinline__ int index_view_find_at(const uint8_t* out, const uint64_t* out_off, const uint8_t* flags,
+                                                  uint64_t n, const uint64_t* P, uint64_t K, const uint64_t* R,
+                                                  uint64_t h, uint64_t& ko, uint64_t& kl, uint64_t& vo, uint64_t& cs) {
+    const uint64_t k = lower_u64(P, K, h);
+    if (k >= K) return RIO_EOF;
+    const uint64_t r = R[k];
+    if (r == kSeekEof) return RIO_EOF;
+    if (r >= n) return RIO_ERR_UNSUPPORTED;
+    if (flags[r] & RIO_FLAG_CORRUPT) return RIO_ERR_DECOMPRESS;
+    if (flags[r] & RIO_FLAG_EOF) return RIO_EOF_CODEC;  // (the map walks past those)
+    const uint64_t base = out_off[r], pl = out_off[r + 1] - base;  // a nil record: no bytes
+    if (!pb_index_entry(out + base, pl, ko, kl, vo, cs)) return RIO_ERR_PROTO;
+    ko += base;
+    return RIO_OK;
+}
+
+__device__ __forceinline__ int bytes_compare_mem(const uint8_t* a, uint64_t an, const uint8_t* b, uint64_t bn) {
+    const uint64_t m = an < bn ? an : bn;
+    for (uint64_t k = 0; k < m; k++)
+        if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+    return an < bn ? -1 : (an > bn ? 1 : 0);
+}
+
+__global__ void __launch_bounds__(256) k_index_search_view(const uint8_t* out, const uint64_t* out_off,
+                                                           const uint8_t* flags, uint64_t n, const uint64_t* P,
+                                                           uint64_t K, const uint64_t* R, uint64_t len,
+                                                           const uint8_t* keys, const uint64_t* key_off, uint64_t nq,
+                                                           const uint32_t* perm, rio_index_hit* hits) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t qq = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; qq < nq; qq += stride) {
+        const uint64_t q = perm ? perm[qq] : qq;
+        rio_index_hit o{};
+        const uint8_t* key = keys + key_off[q];
+        const uint64_t klen = key_off[q + 1] - key_off[q];
+        uint64_t ko = 0, kl = 0, vo = 0, cs = 0, i = 0, j = len;
+        int e = RIO_OK;
+        while (i < j) {
+            const uint64_t h = (i + j) >> 1;
+            e = index_view_find_at(out, out_off, flags, n, P, K, R, h, ko, kl, vo, cs);
+            if (e) break;
+            if (bytes_compare_mem(out + ko, kl, key, klen) < 0) i = h + 1; else j = h;
+        }
+        if (e == RIO_OK) {
+            e = index_view_find_at(out, out_off, flags, n, P, K, R, i, ko, kl, vo, cs);
+            if (e == RIO_OK) {
+                o.offset = i;
+                o.found = i < len && bytes_compare_mem(out + ko, kl, key, klen) == 0;
+                if (o.found) {
+                    o.value_offset = vo;
+                    o.checksum = cs;
+                }
+            }
+        }
+        if (eof_class(e)) {  // binarySearch: an io.EOF probe means "not found" at offset size
+            e = RIO_OK;
+            o.offset = len;
+        }
+        o.status = e;
+        hits[q] = o;
+    }
+}
+
+hipError_t launch_index_search_view(const uint8_t* out, const uint64_t* out_off, const uint8_t* flags, uint64_t n,
+                                    const uint64_t* P, uint64_t K, const uint64_t* R, uint64_t len, const uint8_t* keys,
+                                    const uint64_t* key_off, uint64_t nq, const uint32_t* perm, rio_index_hit* hits,
+                                    hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    const uint64_t blocks = (nq + 255) / 256;
+    hipLaunchKernelGGL(k_index_search_view, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s, out,
+                       out_off, flags, n, P, K, R, len, keys, key_off, nq, perm, hits);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------

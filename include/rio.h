@@ -292,7 +292,8 @@ int rio_encode_file(rio_ctx* ctx, const uint8_t* records, const uint64_t* rec_of
  * probe hit io.EOF; later lookups on the same Go object then see that entry: see DESIGN.md §8).
  *   status  RIO_OK (no error; `found` tells Get / Contains), else findAt's error: SeekNext's
  *           non-EOF error (e.g. RIO_ERR_UNEXPECTED_EOF) or RIO_ERR_PROTO. RIO_ERR_UNSUPPORTED for a
- *           compressed or v1/v2 index (keep the reference index).
+ *           v1/v2 index, and from rio_device_index_search for a compressed one (keep the reference
+ *           index); the rio_index handle answers compressed indexes from their decoded view.
  *   offset  binarySearch's offset (IteratorStartingAt starts there; size when an io.EOF probe ended it)
  *   value_offset / checksum  IndexVal when found. */
 typedef struct rio_index_hit {
@@ -308,7 +309,9 @@ int rio_device_index_search(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, u
                             const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n, rio_index_hit* d_hits,
                             void* stream);
 /* host-memory handle (the cgo DiskIndexLoader.Load / Get binding): the index file stays resident in
- * HBM; each search copies the keys in and the hits out (synchronises). */
+ * HBM; each search copies the keys in and the hits out (synchronises). A compressed index.rio is
+ * decoded once at open (records + the SeekNext map over the file) and searched from that view
+ * (disk_key_index.go:173 reads it through an MMapReader, which decompresses every record). */
 typedef struct rio_index rio_index;
 int rio_index_open(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_index** out);
 int rio_index_search(rio_index* idx, const uint8_t* keys, const uint64_t* key_off, uint64_t n, rio_index_hit* hits);

@@ -189,3 +189,42 @@ def test_large_batch_sorted_path_matches_oracle():
         r = rng.random()
         qs.append(k if r < 0.5 else (k[:8] + bytes([rng.getrandbits(8)]) if r < 0.8 else k[:rng.randint(0, len(k))]))
     check(idx, qs)
+
+
+def handle_hits(idx_bytes, queries):
+    """rio_index_open / rio_index_search (the cgo DiskIndexLoader binding's calls) on a host image."""
+    h = ctypes.c_void_p()
+    assert L.lib().rio_index_open(L.default_ctx(0), idx_bytes, len(idx_bytes), ctypes.byref(h)) == 0
+    try:
+        off = np.zeros(len(queries) + 1, dtype=np.uint64)
+        np.cumsum([len(q) for q in queries], out=off[1:])
+        blob = b"".join(queries) or b"\0"
+        hits = (L.IndexHit * len(queries))()
+        assert L.lib().rio_index_search(h, blob, off.ctypes.data, len(queries), hits) == 0
+        return [(x.status, x.offset, bool(x.found), x.value_offset, x.checksum) for x in hits]
+    finally:
+        L.lib().rio_index_free(h)
+
+
+@pytest.mark.pending
+@pytest.mark.parametrize("comp", [1, 2, 3])
+def test_compressed_index_through_the_decoded_view(comp):
+    """A gzip / snappy / lzw index.rio (rProto.NewMMapProtoReaderWithPath decompresses every record,
+    disk_key_index.go:173): the handle decodes the index once and answers every probe from its records
+    and SeekNext map; hits equal the oracle's binarySearch over the compressed file, adversarial keys
+    (fake headers and 0x91 bytes inside entries) and nil records included."""
+    rng = random.Random(20 + comp)
+    keys = sorted({bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 40))) for _ in range(1500)})
+    keys = [k + (b"\x91\x8d\x4c" if i % 7 == 1 else b"") for i, k in enumerate(keys)]
+    keys = sorted(set(keys))
+    for nil_every in (0, 11):
+        idx = index_image(entries_for(keys, nil_every), comp)
+        qs = queries_for(keys, rng, 100)
+        got = handle_hits(idx, qs)
+        for q, g in zip(qs, got):
+            o = orc.disk_index_search(idx, q, 4096)
+            if o[0] != 0:
+                assert g[0] == o[0], (comp, q, g, o)
+            else:
+                assert g == o, (comp, q, g, o)
+        assert sum(g[2] for g in got[:len(keys)]) > len(keys) // 2
