@@ -275,45 +275,109 @@ corrupt:
     return RIO_ERR_DECOMPRESS;
 }
 
-/* GzipCompressor.DecompressWithBuf (gzip_compression.go:54-69): gzip.NewReader (multistream)
- * + ReadFrom. zlib restatement; parity pinned only by the _comp1 fixture. */
+/* GzipCompressor.DecompressWithBuf (gzip_compression.go:54-69): gzip.NewReader + bytes.Buffer.ReadFrom,
+ * i.e. Go's compress/gzip Reader, multistream (go 1.25 stdlib gunzip.go; not vendored). Restated:
+ *   member header (readHeader): ID1 ID2 = 1f 8b, CM = 8, else ErrHeader; FLG's reserved bits are
+ *   ignored; FEXTRA: 2-byte XLEN and its bytes; FNAME, FCOMMENT: readString, which reads into a
+ *   512-byte buffer and fails with ErrHeader when the 512th byte is not the NUL; FHCRC: the low 16 bits
+ *   of the CRC-32 of every header byte before it (strings with their NUL); a short header is
+ *   io.ErrUnexpectedEOF (noEOF);
+ *   body: DEFLATE (compress/flate; here zlib's raw inflate);
+ *   trailer: CRC-32 and ISIZE (mod 2^32) of the member's output, else ErrChecksum; short: ErrUnexpectedEOF;
+ *   after a trailer: the end of the payload ends the record (readHeader's io.EOF), anything else is the
+ *   next member's header. An empty payload is gzip.NewReader's bare io.EOF.
+ * zlib's own gzip wrapper differs from Go on the header (it rejects reserved FLG bits and accepts any
+ * name length), so only the DEFLATE body is zlib's here. Pinned by the _comp1 fixture (Go-written). */
+static uLong crc_upd(uLong c, const uint8_t* p, uint64_t n) { return crc32(c, p, (uInt)n); }
+
+static int gz_member_header(const uint8_t* s, uint64_t n, uint64_t* hl) {
+    if (n < 10 || s[0] != 0x1f || s[1] != 0x8b || s[2] != 8) return RIO_ERR_DECOMPRESS;
+    const uint32_t flg = s[3];
+    uLong crc = crc_upd(crc32(0L, Z_NULL, 0), s, 10);
+    uint64_t p = 10;
+    if (flg & 4) { /* FEXTRA */
+        if (n - p < 2) return RIO_ERR_DECOMPRESS;
+        const uint64_t xl = (uint64_t)s[p] | (uint64_t)s[p + 1] << 8;
+        crc = crc_upd(crc, s + p, 2);
+        p += 2;
+        if (n - p < xl) return RIO_ERR_DECOMPRESS;
+        crc = crc_upd(crc, s + p, xl);
+        p += xl;
+    }
+    for (int f = 0; f < 2; f++) { /* FNAME, then FCOMMENT */
+        if (!(flg & (f ? 16u : 8u))) continue;
+        uint64_t i = 0;
+        for (;;) {
+            if (i >= 512) return RIO_ERR_DECOMPRESS; /* readString: ErrHeader */
+            if (p + i >= n) return RIO_ERR_DECOMPRESS;
+            if (s[p + i] == 0) break;
+            i++;
+        }
+        crc = crc_upd(crc, s + p, i + 1);
+        p += i + 1;
+    }
+    if (flg & 2) { /* FHCRC */
+        if (n - p < 2) return RIO_ERR_DECOMPRESS;
+        if (((uint32_t)s[p] | (uint32_t)s[p + 1] << 8) != (uint32_t)(crc & 0xFFFFu)) return RIO_ERR_DECOMPRESS;
+        p += 2;
+    }
+    *hl = p;
+    return RIO_OK;
+}
+
 static int gzip_decode(const uint8_t* src, uint64_t n, uint8_t** out, uint64_t* out_len) {
     *out = NULL;
     *out_len = 0;
     /* gzip.NewReader(empty) returns a bare io.EOF (gzip_compression.go:56-59), which ReadNext
      * passes through unwrapped (file_reader.go:118-121) and ReadNextAt wraps once: io.EOF class */
     if (n == 0) return RIO_EOF_CODEC;
-    uint64_t cap = n * 4 + 64, used = 0;
+    uint64_t cap = n * 4 + 64, used = 0, pos = 0;
     uint8_t* dst = (uint8_t*)malloc(cap);
-    z_stream z;
-    memset(&z, 0, sizeof z);
-    if (inflateInit2(&z, 16 + 15) != Z_OK) { free(dst); return RIO_ERR_DECOMPRESS; }
-    z.next_in = (Bytef*)src;
-    z.avail_in = (uInt)n;
-    for (;;) {
-        if (used == cap) {
-            cap *= 2;
-            dst = (uint8_t*)realloc(dst, cap);
+    for (;;) { /* one member */
+        uint64_t hl = 0;
+        if (gz_member_header(src + pos, n - pos, &hl)) goto bad;
+        pos += hl;
+        z_stream z;
+        memset(&z, 0, sizeof z);
+        if (inflateInit2(&z, -15) != Z_OK) goto bad;
+        z.next_in = (Bytef*)(src + pos);
+        z.avail_in = (uInt)(n - pos);
+        const uint64_t m0 = used;
+        int rc;
+        for (;;) {
+            if (used == cap) {
+                cap *= 2;
+                dst = (uint8_t*)realloc(dst, cap);
+            }
+            z.next_out = dst + used;
+            z.avail_out = (uInt)(cap - used);
+            rc = inflate(&z, Z_NO_FLUSH);
+            used = cap - z.avail_out;
+            if (rc == Z_STREAM_END) break;
+            if (rc == Z_OK) continue;
+            if (rc == Z_BUF_ERROR && z.avail_out == 0) continue;
+            break;
         }
-        z.next_out = dst + used;
-        z.avail_out = (uInt)(cap - used);
-        int rc = inflate(&z, Z_NO_FLUSH);
-        used = cap - z.avail_out;
-        if (rc == Z_STREAM_END) {
-            if (z.avail_in == 0) break;
-            inflateReset(&z); /* next gzip member (multistream) */
-            continue;
-        }
-        if (rc == Z_OK) continue;
-        if (rc == Z_BUF_ERROR && z.avail_out == 0) continue;
+        const uint64_t rest = z.avail_in;
         inflateEnd(&z);
-        free(dst);
-        return RIO_ERR_DECOMPRESS;
+        if (rc != Z_STREAM_END) goto bad;
+        pos = n - rest;
+        if (n - pos < 8) goto bad; /* trailer: io.ErrUnexpectedEOF */
+        const uint8_t* t = src + pos;
+        const uint32_t want_crc = (uint32_t)t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
+        const uint32_t want_sz = (uint32_t)t[4] | (uint32_t)t[5] << 8 | (uint32_t)t[6] << 16 | (uint32_t)t[7] << 24;
+        if ((uint32_t)crc_upd(crc32(0L, Z_NULL, 0), dst + m0, used - m0) != want_crc ||
+            (uint32_t)(used - m0) != want_sz)
+            goto bad; /* ErrChecksum */
+        pos += 8;
+        if (pos == n) break; /* readHeader's io.EOF: the stream ends cleanly */
     }
-    inflateEnd(&z);
     *out = dst;
     *out_len = used;
     return RIO_OK;
+bad:
+    free(dst);
+    return RIO_ERR_DECOMPRESS;
 }
 
 

@@ -360,6 +360,28 @@ def gzip_cases():
     return cases
 
 
+def gzip_go_header_cases():
+    """(name, image, record index, Go accepts it) gzip headers on which zlib's wrapper and Go's
+    compress/gzip readHeader disagree (gunzip.go): Go ignores FLG's reserved bits (zlib rejects them),
+    and readString fails with ErrHeader once a name or comment reaches 512 bytes without its NUL
+    (zlib takes any length). Record 3 of each file carries the header."""
+    text = text_records(8, 12)
+    cases = []
+
+    def one(name, hdr, ok):
+        recs = [(len(r), gzip_member(r)) for r in text]
+        recs[3] = (len(text[3]), gzip_member(text[3], header=hdr))
+        cases.append((name, gz_file(recs), 3, ok))
+
+    one("gz_flg_reserved_bits", gzip_header(0xE0), True)
+    one("gz_flg_reserved_with_name", gzip_header(0x20 | 8, name=b"n"), True)
+    one("gz_name_511", gzip_header(8, name=b"a" * 511), True)
+    one("gz_name_512", gzip_header(8, name=b"a" * 512), False)
+    one("gz_comment_511_hcrc", gzip_header(16 | 2, comment=b"c" * 511), True)
+    one("gz_comment_600", gzip_header(16, comment=b"c" * 600), False)
+    return cases
+
+
 # ---------------------------------------------------------------------------------------------
 # lzw-compressed files (compType 3, LzwCompressor: Go compress/lzw, LSB, litWidth 8)
 # ---------------------------------------------------------------------------------------------

@@ -119,3 +119,13 @@ def test_gzip_multi_member_batch():
         g = dict(info, out=b.out[:nb].cpu().numpy(), out_off=b.out_off[:n + 1].cpu().numpy(),
                  rec_off=b.rec_off[:n].cpu().numpy(), flags=b.flags[:n].cpu().numpy())
         assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), f"batch {k}")
+
+
+@pytest.mark.pending
+@pytest.mark.parametrize("name,image,k,go_ok", corpus.gzip_go_header_cases(), ids=lambda v: v if isinstance(v, str) else "")
+def test_gzip_go_header_rules(name, image, k, go_ok):
+    """Member headers on which Go's readHeader and zlib's wrapper disagree (reserved FLG bits, names
+    and comments of 512+ bytes): the device and the Go-faithful oracle agree record by record."""
+    g = gpu_decode_arrays(image)
+    assert_same_as_oracle(g, orc.file_reader_decode_arrays(image), name)
+    assert bool(g["flags"][k] & 2) == (not go_ok), name

@@ -72,3 +72,17 @@ def test_gzip_empty_payload_is_eof_class():
     o = orc.file_reader_decode_arrays(_records("gz_empty_payload"))
     assert o["status"] == STATUS["EOF"] and o["n_records"] == 20
     assert o["flags"][7] == 4 and o["out_off"][8] == o["out_off"][7]
+
+
+@pytest.mark.parametrize("name,image,k,go_ok", corpus.gzip_go_header_cases(), ids=lambda v: v if isinstance(v, str) else "")
+def test_oracle_follows_go_gzip_header_rules(name, image, k, go_ok):
+    """The oracle reads member headers as Go's readHeader does (gunzip.go), not as zlib's wrapper:
+    reserved FLG bits are ignored, a name or comment of 512 bytes or more without its NUL is ErrHeader."""
+    o = orc.file_reader_decode(image)
+    assert o["n_records"] == 8, name
+    rec = o["records"][k]
+    if go_ok:
+        assert not isinstance(rec, orc.BadRecord) and rec == corpus.text_records(8, 12)[k], name
+    else:
+        assert isinstance(rec, orc.BadRecord), name
+    assert all(not isinstance(r, orc.BadRecord) for i, r in enumerate(o["records"]) if i != k), name
