@@ -1186,7 +1186,9 @@ __device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t la
     A.bytes = s.bytes;
     A.ce = chunk_end(P, c);
     A.term = s.status != RIO_OK;
-    A.broken = 0;
+    // sizes the 40-bit words cannot carry (a header may announce far more output than the file holds)
+    // break the chain: the two-launch scan, in 64 bits, then frames the file
+    A.broken = A.bytes >= (kLbMask >> 1) ? 1u : 0u;
     A.term_chunk = c;
     {
         const uint64_t v = lane == 0 ? A.key : lane == 1 ? A.out : lane == 2 ? A.cnt : lane == 3 ? A.bytes : lb_flags(A);
@@ -1251,7 +1253,8 @@ __device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t la
         }
         if (!E.broken) E = acc;
     }
-    const RunSum I = c > 0 ? combine(E, A) : A;  // inclusive prefix (chunk 0's run is keyed at 8)
+    RunSum I = c > 0 ? combine(E, A) : A;  // inclusive prefix (chunk 0's run is keyed at 8)
+    if (I.bytes >= (kLbMask >> 1)) I.broken = 1;
     {
         const uint64_t v = lane == 5 ? I.out : lane == 6 ? I.cnt : lane == 7 ? I.bytes : lb_flags(I);
         if (lane >= 5 && lane < 9) lb_st(me + lane, lb_word(tag, v));
