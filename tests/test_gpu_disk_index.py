@@ -206,7 +206,6 @@ def handle_hits(idx_bytes, queries):
         L.lib().rio_index_free(h)
 
 
-@pytest.mark.pending
 @pytest.mark.parametrize("comp", [1, 2, 3])
 def test_compressed_index_through_the_decoded_view(comp):
     """A gzip / snappy / lzw index.rio (rProto.NewMMapProtoReaderWithPath decompresses every record,

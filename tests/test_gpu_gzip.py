@@ -121,7 +121,6 @@ def test_gzip_multi_member_batch():
         assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), f"batch {k}")
 
 
-@pytest.mark.pending
 @pytest.mark.parametrize("name,image,k,go_ok", corpus.gzip_go_header_cases(), ids=lambda v: v if isinstance(v, str) else "")
 def test_gzip_go_header_rules(name, image, k, go_ok):
     """Member headers on which Go's readHeader and zlib's wrapper disagree (reserved FLG bits, names

@@ -61,7 +61,7 @@ def test_repairs_happen_and_stay_exact():
     assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), "embedded")
 
 
-@pytest.mark.parametrize("fused", [pytest.param(1, marks=pytest.mark.pending), 0])
+@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("chunk", [64, 256, 1024, 4096, 65536])
 def test_chunk_size_independent(chunk, fused, monkeypatch):
     """The result does not depend on the framing chunk size (speculation granularity), with the walk

@@ -15,7 +15,7 @@ import corpus
 import oracle_py as orc
 from conftest import STATUS
 
-pytestmark = [pytest.mark.gpu, pytest.mark.pending]
+pytestmark = pytest.mark.gpu
 
 
 def _records(n, seed):
