@@ -25,13 +25,6 @@ constexpr unsigned kSnappyBlock = 256;
 #endif
 constexpr unsigned kSnappyGrid = RIO_SNAPPY_GRID;
 constexpr uint64_t kSinkBytes = (uint64_t)kSnappyBlock / 64 * kSnappyGrid * 64;
-// k_snappy_pair: one parser + one emitter wave per workgroup, six per CU (256 CUs); each pair
-// uses one sink line
-#ifndef RIO_PAIR_GRID
-#define RIO_PAIR_GRID 1536
-#endif
-constexpr unsigned kPairGrid = RIO_PAIR_GRID;
-static_assert(kPairGrid * 64ull <= kSinkBytes, "a sink line per pair");
 
 // Framing chunk: a byte range [cs, ce) of the file; a chunk OWNS the records whose header starts
 // in its range. Written by the walk kernel, consumed by the scan / place kernels.
@@ -144,8 +137,6 @@ struct FrameParams {
     // Snappy: files whose mean decoded record is at least this many bytes (and files past 32-bit
     // lane positions) take the wave-per-record decoder k_snappy_coop instead of k_snappy_pipe
     uint64_t coop_min;
-    // 1: the lane-decoder files run on the two-wave decoder (k_snappy_pair: parser + emitter wave)
-    uint32_t pair;
     // 1: k_walk places the records itself (decoupled look-back over lb); only when the decode of the
     // same FrameParams follows in the same call (rio_device_decode[_ex|_batch])
     uint32_t fused;

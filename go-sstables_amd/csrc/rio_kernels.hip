@@ -1218,13 +1218,22 @@ __device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t la
             const uint32_t kp = lane_ffs(pm);  // nearest lane with a prefix (64: none in the window)
             const uint64_t need = kp >= 64 ? ~0ull : ((1ull << kp) - 1);
             if ((am & need) != need) {  // a chunk between has not published its run yet
-                if (++spins >= RIO_LB_SPIN_MAX) {
+                // wait for it with five loads per poll (lanes 0-4 read its run words), not the window's
+                // 576: thousands of waves re-reading whole windows saturated the memory system and
+                // starved the walks they were waiting for (C2 at 4406 chunks: 18 s per decode)
+                const uint64_t* q = P.lb + (hi - 1 - lane_ffs(need & ~am)) * kLbWords;
+                bool there = false;
+                while (!there && spins < RIO_LB_SPIN_MAX) {
+                    __builtin_amdgcn_s_sleep(8);
+                    spins++;
+                    there = __all(lane >= 5 || lb_tagged(lb_ld(const_cast<uint64_t*>(q) + lane), tag));
+                }
+                if (spins >= RIO_LB_SPIN_MAX) {
                     E.ce = A.ce;
                     E.key = RIO_FILE_HEADER_BYTES;
                     E.broken = 1;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(8);
                 continue;
             }
             RunSum X = run_identity();

@@ -108,17 +108,6 @@ __device__ __forceinline__ uint4 merge_at(uint4 st, uint4 v, uint32_t r) {
 #ifndef RIO_NT
 #define RIO_NT 1
 #endif
-// 1: the element header decoded through one value-field width (fewer selects); A/B build knob
-#ifndef RIO_PARSE2
-#define RIO_PARSE2 0
-#endif
-// 1: waves whose lanes hold one record each run a step without the record switch; A/B build knob
-#ifndef RIO_PAIR_DEBUG
-#define RIO_PAIR_DEBUG 0  // bounded queue waits that report a stuck pair (printf)
-#endif
-#ifndef RIO_SINGLE_REC
-#define RIO_SINGLE_REC 0
-#endif
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
 }
@@ -288,19 +277,6 @@ __device__ __forceinline__ bool snappy_lane_t(const FrameParams& P, uint64_t r0,
             const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
             const bool avail = min((pos + 15) >> 4, lastc) < whi;
             const bool is0 = t == 0, is1 = t == 1;
-#if RIO_PARSE2
-            // One value field after the tag, of wf bits: a literal with x >= 60 carries x - 59 length
-            // bytes, copy-1 one offset byte (the high 3 offset bits are in the tag), copy-2 two, copy-4
-            // four; so hl = 1 + wf / 8 and the field is the low wf bits of W1 for every form.
-            const bool lng = x >= 60;
-            uint32_t wf = is0 ? (lng ? 8u * x - 472u : 0u) : (4u << t);
-            pin_v(wf);
-            const uint32_t shf = (32u - wf) & 31u;
-            const uint32_t fld = (W1 << shf) >> shf;  // wf = 0 (short literal): unused
-            const uint32_t hl = 1u + (wf >> 3);
-            const uint32_t len = (is0 && lng ? fld : (is1 ? (x & 7u) + 3u : x)) + 1u;
-            const uint32_t off = is1 ? (((tag & 0xE0u) << 3) | fld) : fld;
-#else
             const bool is2 = t == 2;
             // literal: x < 60 -> length x + 1; x in [60, 63] -> x - 59 little-endian length bytes follow
             const bool lng = x >= 60;
@@ -321,7 +297,6 @@ __device__ __forceinline__ bool snappy_lane_t(const FrameParams& P, uint64_t r0,
             const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
             const uint32_t hl = is0 ? lit_hl : cp_hl;
             const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
-#endif
             // golang/snappy bounds, per record: header bytes present; literal source room or copy
             // offset in [1, bytes produced] (length / offset 0 wrap to the maximum key); output room
             const uint32_t sleft = s_end - s;
@@ -439,9 +414,6 @@ __device__ __forceinline__ bool snappy_lane_t(const FrameParams& P, uint64_t r0,
 
 __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint8_t* wi,
                                             uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
-#if RIO_SINGLE_REC
-    if (__all(r1 - r0 <= 1)) return snappy_lane_t<false>(P, r0, r1, wl, wi, lane, sink, bad_rec);
-#endif
     return snappy_lane_t<true>(P, r0, r1, wl, wi, lane, sink, bad_rec);
 }
 
@@ -812,7 +784,6 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
     if (!st->any_mixed) return;  // every record is one literal: k_copy_records copies them
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (P.pair && !coop_active(P, st)) return;  // k_snappy_pair decodes the file
     if (coop_active(P, st)) {  // large records / past 32-bit positions: the wave-per-record decoder
         coop_file(P, *reinterpret_cast<CoopLds*>(hist[wave]), lane, (uint64_t)blockIdx.x * (kSnappyBlock / 64) + wave,
                   (uint64_t)gridDim.x * (kSnappyBlock / 64));
@@ -848,382 +819,6 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// The lane decoder split over the two waves of a workgroup (k_snappy_pair, k_snappy_pair_batch).
-//
-// Measured on C2: the one-wave decoder above issues at most one instruction per 4
-// cycles per wave (338 per step) and its 20 KiB of LDS (history + input ring) leaves two waves per
-// SIMD, so the SIMD's VALU pipe (one wave64 instruction per 2 cycles) idles about half the time.
-// Here lane l of two waves serves record stream l:
-//   * the PARSER wave reads the input (input ring), decodes and checks the element headers, switches
-//     records and writes one piece per step into a 4-slot LDS queue: no history, no far loads;
-//   * the EMITTER wave owns the history ring and runs the one-wave decoder's emit side unchanged: it
-//     takes piece j + 3 from the queue at step j (issuing its far-history load then, after its own
-//     flush store of the step, so kFarOff = 48 + 16 + 128 holds as before), emits piece j, flushes.
-// The two waves are decoupled: the parser may run kQ pieces past the emitter's queue reads, each side
-// waits on the other's LDS counter only when the queue is full / empty. Six pairs (26 KiB each) fit
-// a CU: twelve waves where the one-wave decoder fits eight.
-namespace {
-constexpr uint32_t kQ = 4;           // queue slots
-constexpr uint32_t kPairBlock = 128;  // parser wave 0, emitter wave 1
-struct PairLds {
-    uint8_t hist[kOutCh * 1024];   // emitter history rings, [chunk][lane][16 B]
-    uint8_t inring[kInCh * 1024];  // parser input rings, [chunk][lane][16 B]
-    uint4 qdata[kQ][64];           // a piece's literal window (16 input bytes from the tag)
-    uint2 qdesc[kQ][64];           // x = n | kind << 5 | sh << 8, y = source position (kind 1 / 2)
-    uint32_t cnt[4];               // [0] pieces produced, [1] pieces read by the emitter,
-                                   // [2] the chunk's piece count (kNoChunk until known), [3] chunk
-};
-static_assert(sizeof(PairLds) <= 160 * 1024 / 6, "six pairs per CU");
-
-struct ISlot {
-    uint4 v;     // input chunk in flight
-    uint32_t c;  // its chunk index (kNoChunk: nothing)
-};
-
-// queue counters: relaxed workgroup-scope atomics (ds_read / ds_write; a plain volatile access
-// would become a flat access, which counts in vmcnt too)
-__device__ __forceinline__ uint32_t lds_ld_v(uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t lds_ld(uint32_t* p) { return __builtin_amdgcn_readfirstlane(lds_ld_v(p)); }
-__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
-    asm volatile("" ::: "memory");  // after the wave's data writes (LDS keeps a wave's order)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Parser side of one chunk: lane = record range [r0, r1). Returns false if a record of the range
-// does not decode (k_finish re-checks the lane's records).
-__device__ __forceinline__ bool pair_parse(const FrameParams& P, uint64_t r0, uint64_t r1, PairLds& S,
-                                           uint32_t lane, uint8_t* sink) {
-    const LaneLds L{S.hist + lane * 16, S.inring + lane * 16};
-    const bool live = r0 < r1;
-    const uint4 d0 = live ? P.rec_desc[r0] : zero4();
-    const uint64_t start0 = ((uint64_t)d0.y << 32) | d0.x;
-    const uint64_t base = start0 & ~15ull;
-    const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
-    const uint32_t lastc = live && base < P.len ? (uint32_t)min((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
-    uint32_t whi = live ? min(kInCh, lastc + 1) : 0u;
-    for (uint32_t c = 0; c < whi; c++) *L.in(c) = sa[c];
-    uint32_t cn = live ? whi : 0xFFFFFFFFu;
-
-    uint64_t k = r0;
-    uint32_t s = (uint32_t)(start0 - base), s_end = s + d0.z;
-    uint32_t pd = 0, rd_start = 0, rd_end = d0.w;
-    uint32_t rem = 0, eff = 0;
-    bool islit = false, bad = false, pdone = !live;
-    // next record's descriptor: 0 needed, 1 in flight, 2 landed, 3 none (last record)
-    uint4 nd = zero4();
-    uint32_t nds = (live && r0 + 1 < r1) ? 0u : 3u;
-    // input chunks and descriptor loads in flight: issued at step p, used at step p + 3
-    ISlot I0{zero4(), kNoChunk}, I1{zero4(), kNoChunk}, I2{zero4(), kNoChunk}, I3{zero4(), kNoChunk};
-    uint4 D0 = zero4(), D1 = zero4(), D2 = zero4(), D3 = zero4();
-    uint32_t dm = 0;  // bit i: slot i carries a descriptor
-    uint4 Wa = *L.in(s >> 4), Wb = *L.in((s >> 4) + 1);
-    uint32_t rd = 0;   // the emitter's read count as last seen (wave-uniform)
-    uint32_t rdv = 0;  // its LDS read issued at the previous step
-    uint32_t p = 0;
-
-    auto step = [&](ISlot& IX, const ISlot& IN, uint4& DX, const uint32_t j) __attribute__((always_inline)) {
-        rd = __builtin_amdgcn_readfirstlane(rdv);
-        // 1. the descriptor load of four steps ago (this slot), if any
-        const bool dl = (dm >> j) & 1u;
-        nd = sel4(dl, DX, nd);
-        nds = dl ? 2u : nds;
-        // 2. parse piece p (as snappy_lane step 4)
-        const uint32_t pos = s;
-        const uint4 W = funnel16(Wa, Wb, pos & 15u);
-        uint32_t n, kind, sh, qsrc;
-        {
-            const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);
-            const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
-            const bool avail = min((pos + 15) >> 4, lastc) < whi;
-            const bool is0 = t == 0, is1 = t == 1, is2 = t == 2;
-            const bool lng = x >= 60;
-            const uint32_t lmask = 0xFFFFFFFFu >> (((63u - x) << 3) & 31u);
-            uint32_t lit_long = (W1 & lmask) + 1u, lit_short = x + 1u;
-            uint32_t c1_len = (x & 7u) + 4u, c1_off = ((tag & 0xE0u) << 3) | (W1 & 0xFFu);
-            uint32_t c2_off = W1 & 0xFFFFu;
-            pin_v(lit_long);
-            pin_v(lit_short);
-            pin_v(c1_len);
-            pin_v(c1_off);
-            pin_v(c2_off);
-            const uint32_t lit_len = lng ? lit_long : lit_short;
-            const uint32_t len = is0 ? lit_len : (is1 ? c1_len : lit_short);
-            const uint32_t lit_hl = lng ? x - 58u : 1u;
-            const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
-            const uint32_t hl = is0 ? lit_hl : cp_hl;
-            const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
-            const uint32_t sleft = s_end - s;
-            const uint32_t lim = is0 ? sleft - hl : pd - rd_start;
-            const uint32_t key = (is0 ? len : off) - 1u;
-            const bool hbad = (hl > sleft) | (key >= lim) | (len > rd_end - pd);
-            const bool hdr = !pdone && rem == 0 && s < s_end && avail;
-            const bool badn = hdr && hbad, ok = hdr && !hbad;
-            bad = bad || badn;
-            sh = ok ? hl : 0u;
-            const uint32_t rem1 = ok ? len : rem, eff1 = ok ? off : eff;
-            const bool lit1 = ok ? t == 0 : islit;
-            const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
-            n = go ? min(rem1, lit1 ? 16u - sh : min(16u, eff1)) : 0u;
-            kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
-            qsrc = pd - eff1;
-            s += sh + (lit1 ? n : 0u);
-            rem = rem1 - n;
-            pd += n;
-            eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
-            islit = lit1;
-            s = badn ? s_end : s;
-            uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
-            pin_v(at_end);
-            if (at_end) {
-                const bool bad_len = pd != rd_end;
-                const bool more = k + 1 < r1;
-                const bool sw = !bad_len && more && nds == 2;
-                bad = bad || bad_len;
-                rem = bad_len ? rd_end - pd : rem;
-                eff = bad_len ? 16u : eff;
-                islit = islit && !bad_len;
-                pdone = pdone || (!bad_len && !more);
-                k += sw ? 1u : 0u;
-                const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
-                s = sw ? (uint32_t)(nstart - base) : s;
-                s_end = sw ? s + nd.z : s_end;
-                rd_start = sw ? pd : rd_start;
-                rd_end = sw ? pd + nd.w : rd_end;
-                nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
-            }
-        }
-        // 3. queue slot p % kQ must be free: the emitter has read piece p - kQ
-        for (uint32_t spin = 0; p >= rd + kQ; spin++) {  // rare: the emitter is kQ pieces behind
-            __builtin_amdgcn_s_sleep(1);
-            rd = lds_ld(&S.cnt[1]);
-            (void)spin;
-#if RIO_PAIR_DEBUG
-            if (spin == (1u << 22)) {
-                if (lane == 0)
-                    printf("pair parse stuck: block %u p %u rd %u c0 %u c2 %u r0 %llu\n", blockIdx.x, p, rd,
-                           lds_ld(&S.cnt[0]), lds_ld(&S.cnt[2]), (unsigned long long)r0);
-                rd = p;
-            }
-#endif
-        }
-        S.qdata[p % kQ][lane] = W;
-        S.qdesc[p % kQ][lane] = make_uint2(n | (kind << 5) | (sh << 8), kind == 2 ? qsrc : (qsrc & 0xFFu));
-        p++;
-        if (lane == 0) lds_st(&S.cnt[0], p);
-        // 4. the next record's descriptor (or a placeholder), used four steps later
-        {
-            const bool want = nds == 0;
-            nds = want ? 1u : nds;
-            dm = want ? (dm | (1u << j)) : (dm & ~(1u << j));
-            DX = *reinterpret_cast<const uint4*>(want ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
-        }
-        // 5. input prefetch into IX (lands three steps later), land IN, read the next window
-        {
-            const uint32_t a = s >> 4;
-            const bool take = cn <= lastc && cn < a + kInCh;
-            IX.v = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
-            IX.c = take ? cn : kNoChunk;
-            cn += take ? 1u : 0u;
-            const bool landed = IN.c != kNoChunk;
-            if (landed) *L.in(IN.c) = IN.v;
-            whi = landed ? IN.c + 1 : whi;
-            Wa = *L.in(s >> 4);
-            Wb = *L.in((s >> 4) + 1);
-        }
-        rdv = lds_ld_v(&S.cnt[1]);  // for the next step (lands meanwhile)
-#if RIO_PAIR_DEBUG
-        if (p == (1u << 24)) {
-            if (lane == 0) printf("pair parse runaway: block %u r0 %llu\n", blockIdx.x, (unsigned long long)r0);
-            return false;
-        }
-#endif
-        return !__all(pdone);
-    };
-    for (;;) {
-        if (!step(I0, I1, D0, 0)) break;
-        if (!step(I1, I2, D1, 1)) break;
-        if (!step(I2, I3, D2, 2)) break;
-        if (!step(I3, I0, D3, 3)) break;
-    }
-    if (lane == 0) lds_st(&S.cnt[2], p);  // every piece of the chunk is in the queue
-    return !bad;
-}
-
-// Emitter side of one chunk (snappy_lane's emit, flush and far loads; its pieces come from the
-// queue): lane = the parser lane's record range, for the output base and the flush owners.
-__device__ __forceinline__ void pair_emit(const FrameParams& P, uint64_t r0, uint64_t r1, PairLds& S, uint32_t lane,
-                                          uint8_t* sink) {
-    const LaneLds L{S.hist + lane * 16, S.inring + lane * 16};
-    uint8_t* const out = P.out;
-    const uint64_t o0 = r0 < r1 ? P.out_off[r0] : 0;
-    uint8_t* const gout = out + o0;
-    uint8_t* obase[4];
-#pragma unroll
-    for (uint32_t jj = 0; jj < 4; jj++) {
-        const int src = (int)((16u * jj + (lane >> 2)) * 4);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
-        obase[jj] = out + (((uint64_t)hi << 32) | lo);
-    }
-    uint32_t d = 0, fb = 0;
-    uint4 stage = zero4();
-    Slot S0 = empty_slot(), S1 = empty_slot(), S2 = empty_slot(), S3 = empty_slot();
-    uint4 wA = zero4(), wB = zero4(), wC = zero4();
-    uint32_t wF = 0, wN = 0;
-    uint32_t have = 0, fin = kNoChunk;  // pieces produced / the chunk's count, as last seen (uniform)
-    uint32_t hv = 0, fv2 = kNoChunk;     // their LDS reads issued at the previous step
-    uint32_t j = 0;                      // the piece this step emits
-
-    // take piece m into slot X (a bubble past the chunk's last piece); X.desc = its far source
-    auto take = [&](Slot& X, uint32_t m) __attribute__((always_inline)) {
-        for (uint32_t spin = 0; m >= have && m < fin; spin++) {  // the parser is behind: wait for piece m or the end
-            have = lds_ld(&S.cnt[0]);
-            fin = lds_ld(&S.cnt[2]);
-            if (m >= have && m < fin) __builtin_amdgcn_s_sleep(1);
-            (void)spin;
-#if RIO_PAIR_DEBUG
-            if (spin == (1u << 22)) {
-                if (lane == 0)
-                    printf("pair emit stuck: block %u m %u have %u fin %u c1 %u r0 %llu\n", blockIdx.x, m, have, fin,
-                           lds_ld(&S.cnt[1]), (unsigned long long)r0);
-                fin = m;
-            }
-#endif
-        }
-        const bool real = m < have && m < fin;
-        const uint2 qd = S.qdesc[m % kQ][lane];
-        X.lit = S.qdata[m % kQ][lane];
-        X.n = real ? (qd.x & 31u) : 0u;
-        X.kind = real ? ((qd.x >> 5) & 3u) : 1u;
-        X.q = X.kind == 1 ? qd.y : (X.kind == 0 ? (qd.x >> 8) : 0u);
-        X.desc = qd.y;
-        if (lane == 0 && real) lds_st(&S.cnt[1], m + 1);
-    };
-    take(S0, 0);
-    take(S1, 1);
-    take(S2, 2);
-#if RIO_PAIR_DEBUG
-    if (lane == 0 && blockIdx.x == 0) printf("emit init have %u fin %u\n", have, fin);
-#endif
-    S0.aux = ld_far(S0.kind == 2 ? gout + S0.desc : sink);
-    S1.aux = ld_far(S1.kind == 2 ? gout + S1.desc : sink);
-    S2.aux = ld_far(S2.kind == 2 ? gout + S2.desc : sink);
-    {  // the first piece's window
-        const uint32_t cs = 2u;
-        *L.out(cs << 4) = sel4(S0.kind == 0, S0.lit, S0.aux);
-        wN = S0.kind == 1 ? S0.q : (cs << 4) + S0.q;
-        wF = wN & 15u;
-        wA = *L.out(wN);
-        wB = *L.out(wN + 16u);
-        wC = *L.out(wN + 32u);
-    }
-    auto step = [&](Slot& X, const Slot& N, Slot& F, const uint32_t jj) __attribute__((always_inline)) {
-        have = max(have, (uint32_t)__builtin_amdgcn_readfirstlane(hv));  // (an int argument picks min/max(double))
-        fin = min(fin, (uint32_t)__builtin_amdgcn_readfirstlane(fv2));
-        hv = lds_ld_v(&S.cnt[0]);  // for the next step
-        fv2 = lds_ld_v(&S.cnt[2]);
-        // 1. emit piece j (window read during the previous step)
-        {
-            const uint32_t r = d & 15u;
-            uint4 lo, hi;
-            funnel32(wA, wB, wC, wF, lo, hi);
-            lo = merge_at(stage, lo, r);
-            *L.out(d) = lo;
-            *L.out(d + 16) = hi;
-            stage = sel4(r + X.n >= 16, hi, lo);
-            d += X.n;
-            const uint32_t r2 = d & 15u, cs = (d >> 4) + 2u;
-            *L.out(cs << 4) = sel4(N.kind == 0, N.lit, N.aux);
-            const uint32_t w = (N.kind == 1 ? N.q : (cs << 4) + N.q) - r2;
-            wN = w;
-            wF = w & 15u;
-        }
-        // 2. cooperative flush (as snappy_lane step 3)
-        {
-            const uint32_t o = 16u * (jj & 3u) + (lane >> 2), part = lane & 3u;
-            const bool ready = d - fb >= 64;
-            const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
-            const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
-            const uint4 fv = *reinterpret_cast<const uint4*>(S.hist + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
-            wA = *L.out(wN);
-            wB = *L.out(wN + 16u);
-            wC = *L.out(wN + 32u);
-            st_out((ofb >> 31) ? obase[jj & 3u] + pos : sink, fv);
-            fb += ((lane >> 4) == (jj & 3u) && ready) ? 64u : 0u;
-        }
-        // 3. piece j + 3 from the queue into slot (j + 3) % 4 (emitted at step j - 1), its far load after
-        // this step's flush store
-#if RIO_PAIR_DEBUG
-        if (lane == 0 && j < 6 && blockIdx.x == 0) printf("emit step j %u have %u fin %u d %u fb %u\n", j, have, fin, d, fb);
-#endif
-        take(F, j + 3);
-        F.aux = ld_far(F.kind == 2 ? gout + F.desc : sink);
-        j++;
-        return j < fin;
-    };
-    for (;;) {
-        if (!step(S0, S1, S3, 0)) break;
-        if (!step(S1, S2, S0, 1)) break;
-        if (!step(S2, S3, S1, 2)) break;
-        if (!step(S3, S0, S2, 3)) break;
-    }
-#if RIO_PAIR_DEBUG
-    if (lane == 0 && blockIdx.x == 0) printf("emit done j %u have %u fin %u d %u\n", j, have, fin, d);
-#endif
-    for (uint32_t q = fb; q < d; q += 16) {
-        const uint4 v = *L.out(q);
-        if (q + 16 <= d)
-            stu16(gout + q, v);
-        else
-            st_partial(gout + q, v, d - q);
-    }
-}
-}  // namespace
-
-// one chunk of records per pair at a time, chunks claimed dynamically as in k_snappy_pipe; both
-// waves meet at a workgroup barrier only between chunks
-__global__ void __launch_bounds__(kPairBlock) k_snappy_pair(FrameParams P) {
-    __shared__ __attribute__((aligned(16))) PairLds S;
-    ScanState* st = P.state;
-    if (!P.pair || st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
-    if (!st->any_mixed || coop_active(P, st)) return;
-    const uint32_t lane = threadIdx.x & 63u, role = threadIdx.x >> 6;
-    const uint64_t n = st->n_records;
-    const uint64_t pairs = gridDim.x;
-    constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
-    const uint64_t rpc = n >= kCpw * 64 * pairs ? n / (kCpw * 64 * pairs) : 1;
-    const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
-    uint8_t* sink = P.sink + (uint64_t)blockIdx.x * 64;  // placeholder line of the pair
-    uint64_t chunk = blockIdx.x;
-    while (chunk < nchunks) {
-        const uint64_t r0 = min(chunk * per + lane * rpc, n), r1 = min(r0 + rpc, n);
-        if (threadIdx.x == 0) {
-            S.cnt[0] = 0;
-            S.cnt[1] = 0;
-            S.cnt[2] = kNoChunk;
-        }
-        __syncthreads();
-        if (role == 0) {
-            if (!pair_parse(P, r0, r1, S, lane, sink)) {
-                const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
-                if (at < kFailLanes) {
-                    P.fail_lanes[2 * at] = r0;
-                    P.fail_lanes[2 * at + 1] = r1;
-                }
-            }
-            if (lane == 0) S.cnt[3] = (uint32_t)(pairs + atomicAdd(&st->pipe_next, 1u));
-        } else {
-            pair_emit(P, r0, r1, S, lane, sink);
-        }
-        __syncthreads();
-        chunk = S.cnt[3];
-        __syncthreads();
-    }
-}
-
 // rio_device_decode_batch: one launch for every lane-decoder file of the batch. The lanes of the grid
 // are split over the files by record count (whole waves per file, so the file's parameters stay
 // wave-uniform scalars), which is what fills the chip when each file alone has fewer records than
@@ -1242,7 +837,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
     uint64_t N = 0;
     for (uint32_t f = 0; f < B.n; f++)
-        if (!B.f[f].pair && pipe_active(B.f[f])) N += B.f[f].state->n_records;
+        if (pipe_active(B.f[f])) N += B.f[f].state->n_records;
     if (N == 0) return;
     // the fewest records per lane whose whole-wave shares (ceil per file) fit the grid: every wave
     // of the grid is resident at once (2 per SIMD), so a share past it would run as a second round
@@ -1250,7 +845,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     for (;;) {
         uint64_t need = 0;
         for (uint32_t f = 0; f < B.n; f++)
-            if (!B.f[f].pair && pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
+            if (pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
         if (need <= waves) break;
         rpl++;
     }
@@ -1258,7 +853,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     uint64_t w0 = 0;
     for (uint32_t f = 0; f < B.n; f++) {
         const FrameParams& P = B.f[f];
-        if (P.pair || !pipe_active(P)) continue;
+        if (!pipe_active(P)) continue;
         const uint64_t n = P.state->n_records, wf = (n + per_wave - 1) / per_wave;
         if (wg < w0 + wf) {
             const uint64_t t = ((wg - w0) << 6) | lane;
@@ -1278,57 +873,8 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
     }
 }
 
-// the two-wave decoder over a batch: pairs dealt to the files by record count as above
-__global__ void __launch_bounds__(kPairBlock) k_snappy_pair_batch(FrameBatch B) {
-    __shared__ __attribute__((aligned(16))) PairLds S;
-    const uint32_t lane = threadIdx.x & 63u, role = threadIdx.x >> 6;
-    const uint64_t pairs = gridDim.x, wg = blockIdx.x;
-    uint64_t N = 0;
-    for (uint32_t f = 0; f < B.n; f++)
-        if (B.f[f].pair && pipe_active(B.f[f])) N += B.f[f].state->n_records;
-    if (N == 0) return;
-    uint64_t rpl = (N + 64 * pairs - 1) / (64 * pairs);
-    for (;;) {
-        uint64_t need = 0;
-        for (uint32_t f = 0; f < B.n; f++)
-            if (B.f[f].pair && pipe_active(B.f[f])) need += (B.f[f].state->n_records + 64 * rpl - 1) / (64 * rpl);
-        if (need <= pairs) break;
-        rpl++;
-    }
-    const uint64_t per = 64 * rpl;
-    uint64_t w0 = 0;
-    for (uint32_t f = 0; f < B.n; f++) {
-        const FrameParams& P = B.f[f];
-        if (!P.pair || !pipe_active(P)) continue;
-        const uint64_t n = P.state->n_records, wf = (n + per - 1) / per;
-        if (wg < w0 + wf) {
-            const uint64_t r0 = min(((wg - w0) * 64 + lane) * rpl, n), r1 = min(r0 + rpl, n);
-            if (threadIdx.x == 0) {
-                S.cnt[0] = 0;
-                S.cnt[1] = 0;
-                S.cnt[2] = kNoChunk;
-            }
-            __syncthreads();
-            if (role == 0) {
-                if (!pair_parse(P, r0, r1, S, lane, P.sink + wg * 64)) {
-                    const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
-                    if (at < kFailLanes) {
-                        P.fail_lanes[2 * at] = r0;
-                        P.fail_lanes[2 * at + 1] = r1;
-                    }
-                }
-            } else {
-                pair_emit(P, r0, r1, S, lane, P.sink + wg * 64);
-            }
-            return;
-        }
-        w0 += wf;
-    }
-}
-
 hipError_t launch_snappy_batch(const FrameBatch& B, hipStream_t s) {
     hipLaunchKernelGGL(k_snappy_pipe_batch, dim3(kSnappyGrid), dim3(kSnappyBlock), 0, s, B);
-    if (B.n && B.f[0].pair) hipLaunchKernelGGL(k_snappy_pair_batch, dim3(kPairGrid), dim3(kPairBlock), 0, s, B);
     hipLaunchKernelGGL(k_snappy_coop_batch, dim3(kCoopGrid), dim3(64 * kCoopWaves), 0, s, B);
     return hipGetLastError();
 }
@@ -1338,8 +884,6 @@ hipError_t launch_snappy_decode(const FrameParams& P, hipStream_t s, bool main) 
     // 4 waves x 20 KiB = 80 KiB per workgroup: 2 workgroups (8 waves) per CU
     if (main) {
         hipLaunchKernelGGL(k_snappy_pipe, dim3(kSnappyGrid), dim3(kSnappyBlock), 0, s, P);
-        // the two-wave decoder: 23 KiB per pair, seven pairs per CU
-        if (P.pair) hipLaunchKernelGGL(k_snappy_pair, dim3(kPairGrid), dim3(kPairBlock), 0, s, P);
     }
     return hipGetLastError();
 }
