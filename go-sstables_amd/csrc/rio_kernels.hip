@@ -1236,26 +1236,45 @@ __device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t la
                 }
                 continue;
             }
-            RunSum X = run_identity();
-            if (kp < 64 && hi >= (uint64_t)kp + 1) {  // lane kp's inclusive prefix (not the empty one)
-                const uint64_t jp = hi - 1 - kp;
-                X.key = RIO_FILE_HEADER_BYTES;
-                X.out = lb_val(readlane64(w[5], kp));
-                X.cnt = lb_val(readlane64(w[6], kp));
-                X.bytes = lb_val(readlane64(w[7], kp));
-                X.ce = chunk_end(P, jp);
-                lb_unflag(X, lb_val(readlane64(w[8], kp)));
+            // lane kp's inclusive prefix (not the empty one), then the runs of lanes kp-1 .. 0 (later
+            // chunks at lower lanes), composed as a tree over the lanes: step k combines lane l + k's
+            // product (earlier chunks) with lane l's, so lane 0 ends with the window's composite
+            RunSum V = run_identity();
+            if (live && lane < kp) {
+                V.key = lb_val(w[0]);
+                V.out = lb_val(w[1]);
+                V.cnt = lb_val(w[2]);
+                V.bytes = lb_val(w[3]);
+                V.ce = chunk_end(P, j);
+                lb_unflag(V, lb_val(w[4]));
+            } else if (live && lane == kp) {
+                V.key = RIO_FILE_HEADER_BYTES;
+                V.out = lb_val(w[5]);
+                V.cnt = lb_val(w[6]);
+                V.bytes = lb_val(w[7]);
+                V.ce = chunk_end(P, j);
+                lb_unflag(V, lb_val(w[8]));
             }
-            for (int l = (int)(kp < 64 ? kp : 64) - 1; l >= 0; l--) {
-                RunSum Y;
-                Y.key = lb_val(readlane64(w[0], (uint32_t)l));
-                Y.out = lb_val(readlane64(w[1], (uint32_t)l));
-                Y.cnt = lb_val(readlane64(w[2], (uint32_t)l));
-                Y.bytes = lb_val(readlane64(w[3], (uint32_t)l));
-                Y.ce = chunk_end(P, hi - 1 - (uint64_t)l);
-                lb_unflag(Y, lb_val(readlane64(w[4], (uint32_t)l)));
-                X = combine(X, Y);
+#pragma unroll
+            for (uint32_t k = 1; k < 64; k <<= 1) {
+                RunSum U;
+                U.key = __shfl_down(V.key, k, 64);
+                U.out = __shfl_down(V.out, k, 64);
+                U.cnt = __shfl_down(V.cnt, k, 64);
+                U.bytes = __shfl_down(V.bytes, k, 64);
+                U.ce = __shfl_down(V.ce, k, 64);
+                const uint64_t f = __shfl_down(lb_flags(V), k, 64);
+                lb_unflag(U, f);
+                if (lane + k >= 64) U = run_identity();
+                V = combine(U, V);
             }
+            RunSum X;
+            X.key = readlane64(V.key, 0);
+            X.out = readlane64(V.out, 0);
+            X.cnt = readlane64(V.cnt, 0);
+            X.bytes = readlane64(V.bytes, 0);
+            X.ce = readlane64(V.ce, 0);
+            lb_unflag(X, readlane64(lb_flags(V), 0));
             acc = combine(X, acc);
             if (kp < 64) break;
             hi -= 64;

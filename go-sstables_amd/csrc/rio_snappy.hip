@@ -2,7 +2,7 @@
 // decode.go + decode_other.go; called per record by FileReader.ReadNext, file_reader.go:115-125).
 //
 // k_snappy_pipe: one lane per record (SIMT across consecutive records), software-pipelined so that
-// no lane ever waits on a memory load issued in the same iteration.
+// no lane ever waits on a memory load issued in the same iteration (snappy_lane, below).
 //
 //   * The record is emitted as a sequence of pieces of <= 16 bytes. A PARSER runs kD pieces ahead
 //     of the EMITTER; pieces travel through kD register slots.
@@ -13,16 +13,18 @@
 //     in issue order, so a uniform schedule is what lets the compiler wait for exactly the loads
 //     issued kD iterations earlier instead of draining the queue whenever some lane of the wave
 //     touched memory.
-//   * The flush is cooperative (see snappy_wave): 64 contiguous bytes of 16 records per wave
-//     store. Lane-private 16-byte stores to 64 records run at ~1.5 TB/s on MI355X, the 16-record
-//     form at ~4.2 TB/s (scripts/mem_probe.hip); loads do not care (5.5 vs 6.0 TB/s).
-//   * History: the last 256 decoded bytes of each record live in an LDS ring; copies reaching
-//     further back (offset > kFarOff) are loaded from the output arena at PARSE time, kD
-//     iterations before use — the flush schedule guarantees those bytes were stored already
-//     (flush lag < 128 bytes, parser lead <= 16*(kD-1) bytes: kFarOff >= 16*(kD-1) + 16 + 128).
+//   * The flush is cooperative: 64 contiguous bytes of 16 records per wave store. Lane-private
+//     16-byte stores to 64 records run at ~1.5 TB/s on MI355X, the 16-record form at ~4.2 TB/s
+//     (scripts/mem_probe.hip); loads do not care (5.5 vs 6.0 TB/s).
+//   * History: the last 256 decoded bytes of each record live in LDS; copies reaching further back
+//     (offset > kFarOff) are loaded from the output arena at PARSE time, kD iterations before use —
+//     the flush schedule guarantees those bytes were stored already (flush lag < 128 bytes, parser
+//     lead <= 16*(kD-1) bytes: kFarOff >= 16*(kD-1) + 16 + 128).
 //   * Input: aligned 16-byte chunks loaded kD iterations ahead land in a 64-byte LDS ring.
-//   * LDS image per wave is chunk-interleaved ([chunk][lane][16 B]): every 16-byte access by a
-//     wave touches each bank once, whatever positions the lanes are at.
+//   * LDS images are dword columns (round 3): row k of lane l is one dword, and all of a lane's rows
+//     sit in its own bank, so every per-lane dword access of a wave is conflict-free; the address
+//     selects the dword and a piece needs only a byte shift (v_alignbyte_b32), placed
+//     destination-aligned (see snappy_lane).
 // Wave-per-record decoder (coop_*, k_snappy_coop_batch): files or arenas past 32-bit positions and
 // streams >= 4 GiB; 64-bit addressing, one 64-byte output window per round with lane = byte.
 // Files whose every record is a single literal (k_place sets ScanState::any_mixed otherwise) are
@@ -35,7 +37,6 @@
 namespace rio {
 
 namespace {
-constexpr uint32_t kOutCh = 16;                  // history ring: 16 chunks = 256 bytes per lane
 constexpr uint32_t kInCh = 4;                    // input ring: 4 chunks = 64 bytes per lane
 constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 // chunks per wave: the balance against the per-chunk drain and setup (A/B on MI355X, records per lane
@@ -47,22 +48,7 @@ constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 constexpr uint32_t kFarOff = 16 * (kD - 1) + 16 + 128;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
 static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128, "far history must be flushed before the parser reads it");
-// v9: a ring copy's source window starts >= 16 * (chunk(d) - kFarOff / 16), and ring chunk chunk(d) + 2
-// (= chunk(d) - 14 mod 16) serves as the staging chunk of literal / far bytes: it must be dead
-static_assert(kOutCh == 16 && kFarOff <= 16 * 13, "staging chunk must hold no live history");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
-
-// bytes [r, r + 16) of the 32-byte little-endian concatenation (a, b), r in [0, 16): dword
-// selection by r >> 2 (two select levels) + v_alignbyte_b32 for the byte shift
-__device__ __forceinline__ uint4 funnel16(uint4 a, uint4 b, uint32_t r) {
-    const uint32_t sh = r & 3u;
-    const bool h1 = (r & 4u) != 0, h2 = (r & 8u) != 0;
-    const uint32_t p0 = h1 ? a.y : a.x, p1 = h1 ? a.z : a.y, p2 = h1 ? a.w : a.z, p3 = h1 ? b.x : a.w,
-                   p4 = h1 ? b.y : b.x, p5 = h1 ? b.z : b.y, p6 = h1 ? b.w : b.z;
-    const uint32_t e0 = h2 ? p2 : p0, e1 = h2 ? p3 : p1, e2 = h2 ? p4 : p2, e3 = h2 ? p5 : p3, e4 = h2 ? p6 : p4;
-    return make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
-                      __builtin_amdgcn_alignbyte(e3, e2, sh), __builtin_amdgcn_alignbyte(e4, e3, sh));
-}
 
 // materialize x in a VGPR here: the selects that use it can no longer be turned into branches that
 // compute x on one side only (an empty asm with a register constraint; no instruction is emitted)
@@ -70,35 +56,6 @@ __device__ __forceinline__ void pin_v(uint32_t& x) { asm volatile("" : "+v"(x));
 
 __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
     return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
-}
-
-// bytes [f, f + 16) and [f + 16, f + 32) of the 48-byte little-endian concatenation (A, B, C),
-// f in [0, 16): one dword-select network shared by both halves, then v_alignbyte_b32
-__device__ __forceinline__ void funnel32(uint4 A, uint4 B, uint4 C, uint32_t f, uint4& L, uint4& H) {
-    const uint32_t sh = f & 3u;
-    const bool h1 = (f & 4u) != 0, h2 = (f & 8u) != 0;
-    // written out (no arrays): an indexed form is lowered to a private-memory table lookup
-    uint32_t p0 = h1 ? A.y : A.x, p1 = h1 ? A.z : A.y, p2 = h1 ? A.w : A.z, p3 = h1 ? B.x : A.w,
-             p4 = h1 ? B.y : B.x, p5 = h1 ? B.z : B.y, p6 = h1 ? B.w : B.z, p7 = h1 ? C.x : B.w,
-             p8 = h1 ? C.y : C.x, p9 = h1 ? C.z : C.y, p10 = h1 ? C.w : C.z;
-    pin_v(p0), pin_v(p1), pin_v(p2), pin_v(p3), pin_v(p4), pin_v(p5), pin_v(p6), pin_v(p7), pin_v(p8), pin_v(p9),
-        pin_v(p10);
-    const uint32_t e0 = h2 ? p2 : p0, e1 = h2 ? p3 : p1, e2 = h2 ? p4 : p2, e3 = h2 ? p5 : p3, e4 = h2 ? p6 : p4,
-                   e5 = h2 ? p7 : p5, e6 = h2 ? p8 : p6, e7 = h2 ? p9 : p7, e8 = h2 ? p10 : p8;
-    L = make_uint4(__builtin_amdgcn_alignbyte(e1, e0, sh), __builtin_amdgcn_alignbyte(e2, e1, sh),
-                   __builtin_amdgcn_alignbyte(e3, e2, sh), __builtin_amdgcn_alignbyte(e4, e3, sh));
-    H = make_uint4(__builtin_amdgcn_alignbyte(e5, e4, sh), __builtin_amdgcn_alignbyte(e6, e5, sh),
-                   __builtin_amdgcn_alignbyte(e7, e6, sh), __builtin_amdgcn_alignbyte(e8, e7, sh));
-}
-
-// bytes [0, r) from `st`, [r, 16) from `v` (r in [0, 16)): two 64-bit masks, then bit selects
-__device__ __forceinline__ uint4 merge_at(uint4 st, uint4 v, uint32_t r) {
-    const uint32_t s8 = 8u * r;
-    const uint64_t all = ~0ull;
-    const uint64_t mlo = s8 >= 64 ? 0ull : (all << s8), mhi = s8 >= 64 ? (all << ((s8 - 64) & 63)) : all;
-    const uint32_t m0 = (uint32_t)mlo, m1 = (uint32_t)(mlo >> 32), m2 = (uint32_t)mhi, m3 = (uint32_t)(mhi >> 32);
-    return make_uint4((v.x & m0) | (st.x & ~m0), (v.y & m1) | (st.y & ~m1), (v.z & m2) | (st.z & ~m2),
-                      (v.w & m3) | (st.w & ~m3));
 }
 
 // cache policy (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads. Default 1: the
@@ -112,309 +69,11 @@ __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
 }
 __device__ __forceinline__ uint4 ld_far(const uint8_t* p) { return (RIO_NT & 2) ? ldu16_nt(p) : ldu16(p); }
-
-// per-lane view of the wave's chunk-interleaved LDS images. History and input ring are separate
-// __shared__ objects, so the compiler knows they never alias and may issue the parser's input-ring
-// reads while the emitter's history writes are still queued.
-struct LaneLds {
-    uint8_t* h;  // wave history image + lane * 16
-    uint8_t* i;  // wave input-ring image + lane * 16
-    __device__ uint4* out(uint32_t pos) const { return reinterpret_cast<uint4*>(h + ((pos >> 4) & (kOutCh - 1)) * 1024); }
-    __device__ uint4* in(uint32_t c) const { return reinterpret_cast<uint4*>(i + (c & (kInCh - 1)) * 1024); }
-};
-
-// one pipeline slot: a parsed piece plus the two loads issued with it
-struct Slot {
-    uint4 in;       // input chunk in_c (load in flight; sink bytes when in_c == kNoChunk)
-    uint4 aux;      // far-history bytes (kind 2) or the next record's descriptor (desc): in flight
-    uint4 lit;      // literal bytes (kind == 0)
-    uint32_t in_c;  // chunk index of `in`
-    uint32_t n;     // piece length, 0 = bubble
-    uint32_t q;     // source output position (kind 1)
-    uint32_t kind;  // 0 literal, 1 ring copy, 2 far copy
-    uint32_t desc;  // aux carries the next record's descriptor
-};
-__device__ __forceinline__ Slot empty_slot() {
-    Slot S;
-    S.in = zero4();
-    S.in_c = kNoChunk;
-    S.aux = zero4();
-    S.lit = zero4();
-    S.n = 0;
-    S.q = 0;
-    S.kind = 1;
-    S.desc = 0;
-    return S;
-}
 }  // namespace
 
 // Files the 32-bit lane-stream positions cannot cover take the wave-per-record decoder.
 __device__ __forceinline__ bool snappy_wide(const FrameParams& P, const ScanState* st) {
     return st->huge_streams || P.len >= 0xFFFFFF00ull || st->total_bytes >= 0xFFFFFF00ull;
-}
-
-// Decode the contiguous record range [r0, r1) of this lane as ONE stream: consecutive records are
-// contiguous in the output arena and separated only by their headers in the file, so the lane's
-// pipeline never drains between records; positions are relative to the lane's aligned input base
-// and to its output base out_off[r0]. Copy offsets stay record-relative (golang/snappy bounds per
-// record); the next record's descriptor travels in the far-load slot of a step without a far copy.
-// The loop runs until every lane of the wave is done: finished lanes keep stepping as bubbles because
-// the flush is cooperative — at step j the 16 lanes 16*(j%4) .. +15 are "owners" and every quad of
-// lanes writes one owner's next complete 64-byte block (16 B per lane, 64 contiguous bytes of one
-// stream): a wave store touches 16 streams instead of 64, which the L2 absorbs ~3x faster.
-// Returns false with *bad_rec = the failing record if a record does not decode.
-// kMulti = false: every lane of the wave has at most one record (C2's chunks), so the record switch
-// and the next-descriptor fetch are compiled out of the step.
-template <bool kMulti>
-__device__ __forceinline__ bool snappy_lane_t(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint8_t* wi,
-                                              uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
-    const LaneLds L{wl + lane * 16, wi + lane * 16};
-    const bool live = r0 < r1;
-    uint8_t* const out = P.out;
-    const uint4 d0 = live ? P.rec_desc[r0] : zero4();
-    const uint64_t o0 = live ? P.out_off[r0] : 0;  // lane output base (arena offset)
-    uint8_t* const gout = out + o0;
-    const uint64_t start0 = ((uint64_t)d0.y << 32) | d0.x;
-    const uint64_t base = start0 & ~15ull;  // lane input base (file offset, 16-B aligned)
-    const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
-    // chunks the prefetcher may read: up to the file end (+pad), never more than the lane needs
-    const uint32_t lastc = live && base < P.len ? (uint32_t)min((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
-    // prime the input ring with chunks [0, 4)
-    uint32_t whi = live ? min(kInCh, lastc + 1) : 0u;  // chunks [0, whi) have landed
-    for (uint32_t c = 0; c < whi; c++) *L.in(c) = sa[c];
-    uint32_t cn = live ? whi : 0xFFFFFFFFu;  // next chunk to load (never for an idle lane)
-
-    // record state: current record k, its input [s, s_end) and output [rd_start, rd_end)
-    uint64_t k = r0;
-    uint32_t s = (uint32_t)(start0 - base), s_end = s + d0.z;
-    uint32_t pd = 0, rd_start = 0, rd_end = d0.w;
-    uint32_t rem = 0, eff = 0;
-    bool islit = false, bad = false, pdone = !live;
-    // next record's descriptor: 0 needed, 1 in flight, 2 landed, 3 none (last record)
-    uint4 nd = zero4();
-    uint32_t nds = (live && r0 + 1 < r1) ? 0u : 3u;
-    // emitter state: d = bytes emitted, fb = flushed bytes (multiple of 64)
-    uint32_t d = 0, fb = 0;
-    uint4 stage = zero4();
-
-    // output base of the owner each lane flushes for at step j (owner = 16 (j % 4) + lane / 4): the
-    // owners never change, so their bases are exchanged once instead of every step
-    uint8_t* obase[4];
-#pragma unroll
-    for (uint32_t jj = 0; jj < 4; jj++) {
-        const int src = (int)((16u * jj + (lane >> 2)) * 4);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
-        obase[jj] = out + (((uint64_t)hi << 32) | lo);
-    }
-
-    Slot S0 = empty_slot(), S1 = empty_slot(), S2 = empty_slot(), S3 = empty_slot();
-    uint32_t drain = 0, qsrc = 0;
-    // v9: the next emit's source window (three ring chunks) and its funnel shift
-    uint4 wA = zero4(), wB = zero4(), wC = zero4();
-    uint32_t wF = 0, wN = 0;
-    // the parser's input window [s, s + 16), read one step ahead (end of the previous step) so that
-    // its LDS latency hides behind the emit and flush
-    // (the two raw chunks travel; the funnel runs where the parser needs the bytes)
-    uint4 Wa = *L.in(s >> 4), Wb = *L.in((s >> 4) + 1);
-
-    auto step = [&](Slot& S, const Slot& N, const uint32_t j) __attribute__((always_inline)) {
-        drain += pdone ? 1u : 0u;
-        // 1. the next record's descriptor, if this slot fetched it
-        if constexpr (kMulti) {
-            nd = sel4(S.desc != 0, S.aux, nd);
-            nds = S.desc ? 2u : nds;
-        }
-        const uint32_t pos = s;
-
-        // 2. emit the piece parsed kD iterations ago (a bubble appends nothing)
-        // Destination-aligned: a literal's or far copy's 16 bytes are first stored to the dead ring
-        // chunk chunk(d) + 2, so every piece is "bytes [w, w + 32) of the ring, w = source - r" with
-        // r = d & 15: one funnel over three ring chunks yields the destination chunk and its
-        // successor already aligned; bytes below r come from the staged head, bytes past the piece
-        // are garbage that later pieces overwrite (never flushed: flushes take complete blocks < d).
-        {
-            const uint32_t r = d & 15u;
-            uint4 lo, hi;
-            funnel32(wA, wB, wC, wF, lo, hi);  // this piece's window, read during the previous step
-            lo = merge_at(stage, lo, r);
-            *L.out(d) = lo;
-            *L.out(d + 16) = hi;
-            stage = sel4(r + S.n >= 16, hi, lo);
-            d += S.n;
-            // The NEXT slot: d does not move before its emit, so its staging chunk and source window
-            // are known now. Stage its literal / far bytes, then read its window: the reads' latency
-            // hides behind this step's flush and parse instead of sitting on the emit chain.
-            const uint32_t r2 = d & 15u, cs = (d >> 4) + 2u;
-            *L.out(cs << 4) = sel4(N.kind == 0, N.lit, N.aux);
-            const uint32_t w = (N.kind == 1 ? N.q : (cs << 4) + N.q) - r2;
-            wN = w;
-            wF = w & 15u;
-        }
-
-        // 3. cooperative flush: lane writes 16 bytes of owner o's next 64-byte block if complete
-        {
-            const uint32_t o = 16u * (j & 3u) + (lane >> 2), part = lane & 3u;
-            const bool ready = d - fb >= 64;
-            const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(o * 4), (int)(fb | (ready ? 0x80000000u : 0u)));
-            const uint32_t pos = (ofb & 0x7FFFFFFFu) + 16u * part;
-            const uint4 fv = *reinterpret_cast<const uint4*>(wl + ((pos >> 4) & (kOutCh - 1)) * 1024 + o * 16);
-            // the next emit's window after the flush data: the store waits for fv only, the window
-            // reads stay in flight through the store and the parse
-            wA = *L.out(wN);
-            wB = *L.out(wN + 16u);
-            wC = *L.out(wN + 32u);
-            st_out((ofb >> 31) ? obase[j & 3u] + pos : sink, fv);
-            fb += ((lane >> 4) == (j & 3u) && ready) ? 64u : 0u;
-        }
-
-        // 4. parse the next piece into this slot (selects only: lanes diverge in data, not flow)
-        {
-            const uint4 W = funnel16(Wa, Wb, pos & 15u);  // input bytes [s, s + 16)
-            // element header at s (golang/snappy decode_other.go tag forms): every form is computed
-            // and combined with selects, so divergent tags cost no exec-mask branches
-            const uint32_t W1 = __builtin_amdgcn_alignbyte(W.y, W.x, 1);  // the 4 bytes after the tag
-            const uint32_t tag = W.x & 0xFFu, t = tag & 3u, x = tag >> 2;
-            const bool avail = min((pos + 15) >> 4, lastc) < whi;
-            const bool is0 = t == 0, is1 = t == 1;
-            const bool is2 = t == 2;
-            // literal: x < 60 -> length x + 1; x in [60, 63] -> x - 59 little-endian length bytes follow
-            const bool lng = x >= 60;
-            const uint32_t lmask = 0xFFFFFFFFu >> (((63u - x) << 3) & 31u);
-            // every alternative computed unconditionally, then selected: the compiler otherwise
-            // turned these nested ternaries into exec-mask branches (3 per step)
-            uint32_t lit_long = (W1 & lmask) + 1u, lit_short = x + 1u;
-            uint32_t c1_len = (x & 7u) + 4u, c1_off = ((tag & 0xE0u) << 3) | (W1 & 0xFFu);
-            uint32_t c2_off = W1 & 0xFFFFu;
-            pin_v(lit_long);
-            pin_v(lit_short);
-            pin_v(c1_len);
-            pin_v(c1_off);
-            pin_v(c2_off);
-            const uint32_t lit_len = lng ? lit_long : lit_short;
-            const uint32_t len = is0 ? lit_len : (is1 ? c1_len : lit_short);
-            const uint32_t lit_hl = lng ? x - 58u : 1u;
-            const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
-            const uint32_t hl = is0 ? lit_hl : cp_hl;
-            const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
-            // golang/snappy bounds, per record: header bytes present; literal source room or copy
-            // offset in [1, bytes produced] (length / offset 0 wrap to the maximum key); output room
-            const uint32_t sleft = s_end - s;
-            const uint32_t lim = is0 ? sleft - hl : pd - rd_start;
-            const uint32_t key = (is0 ? len : off) - 1u;
-            const bool hbad = (hl > sleft) | (key >= lim) | (len > rd_end - pd);
-            const bool hdr = !pdone && rem == 0 && s < s_end && avail;
-            const bool badn = hdr && hbad, ok = hdr && !hbad;
-            bad = bad || badn;
-            const uint32_t sh = ok ? hl : 0u;
-            const uint32_t rem1 = ok ? len : rem, eff1 = ok ? off : eff;
-            const bool lit1 = ok ? t == 0 : islit;
-            // a literal piece takes the window bytes after the header; a copy piece reaches back
-            // at most `eff` bytes (overlapping copies double their reach: a multiple of the offset)
-            const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
-            const uint32_t n = go ? min(rem1, lit1 ? 16u - sh : min(16u, eff1)) : 0u;
-            S.n = n;
-            S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
-            qsrc = pd - eff1;
-            // the literal starts sh bytes into W; the emitter's funnel absorbs that shift (S.q = sh),
-            // a far copy's bytes sit at the start of the staging chunk (S.q = 0)
-            S.q = S.kind == 1 ? qsrc : (S.kind == 0 ? sh : 0u);
-            S.lit = W;
-            s += sh + (lit1 ? n : 0u);
-            rem = rem1 - n;
-            pd += n;
-            eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
-            islit = lit1;
-            // a record that does not decode is not the end of the lane: its remaining input is skipped
-            // and the rest of its announced output is filled (16-byte ring pieces of unspecified
-            // bytes), then the next record starts; k_finish re-checks the lane and flags it
-            s = badn ? s_end : s;
-            // record boundary: stream consumed -> the record must be complete; switch to the next
-            // (its descriptor landed) or finish the range
-            // (a real branch: a lane ends a record every ~130 steps, so most steps of a wave skip it;
-            // it holds no memory operation, so the wave's memory schedule stays uniform)
-            // one condition in a VGPR, one branch: written with && the compiler nested three
-            // branches (and their exec-mask merges) into every step
-            uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
-            pin_v(at_end);
-            if (at_end) {
-                const bool bad_len = pd != rd_end;  // snappy: d != len(dst) => ErrCorrupt
-                bad = bad || bad_len;
-                // fill (rd_end > pd: output room is checked per element)
-                rem = bad_len ? rd_end - pd : rem;
-                eff = bad_len ? 16u : eff;
-                islit = islit && !bad_len;
-                if constexpr (kMulti) {
-                    const bool more = k + 1 < r1;
-                    const bool sw = !bad_len && more && nds == 2;
-                    pdone = pdone || (!bad_len && !more);
-                    k += sw ? 1u : 0u;
-                    const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
-                    s = sw ? (uint32_t)(nstart - base) : s;
-                    s_end = sw ? s + nd.z : s_end;
-                    rd_start = sw ? pd : rd_start;
-                    rd_end = sw ? pd + nd.w : rd_end;
-                    nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
-                } else {
-                    pdone = pdone || !bad_len;
-                }
-            }
-        }
-        // far history (flushed: see header), or the next record's descriptor, or a placeholder load
-        {
-            const bool want_desc = kMulti && S.kind != 2 && nds == 0;
-            S.desc = want_desc ? 1u : 0u;
-            nds = want_desc ? 1u : nds;
-            const uint8_t* ap = S.kind == 2 ? gout + qsrc
-                                            : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
-            S.aux = ld_far(ap);
-        }
-
-        // 5. input prefetch: the next chunk if the ring has room for it when it lands
-        {
-            const uint32_t a = s >> 4;
-            const bool take = cn <= lastc && cn < a + kInCh;
-            S.in = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
-            S.in_c = take ? cn : kNoChunk;
-            cn += take ? 1u : 0u;
-        }
-
-        // 6. land the next slot's input chunk (loaded kD - 1 iterations ago), then read the next
-        // step's parser window
-        {
-            const bool landed = N.in_c != kNoChunk;
-            if (landed) *L.in(N.in_c) = N.in;
-            whi = landed ? N.in_c + 1 : whi;
-            Wa = *L.in(s >> 4);
-            Wb = *L.in((s >> 4) + 1);
-        }
-    };
-
-    // one exit per kD steps, taken by the whole wave: every path around the loop issues the same
-    // memory operations, so the compiler's wait counts stay exact
-    static_assert(kD == 4, "unrolled for four slots");
-    do {
-        step(S0, S1, 0);
-        step(S1, S2, 1);
-        step(S2, S3, 2);
-        step(S3, S0, 3);
-    } while (__any(drain < kD));
-    // the stream's tail (< 128 bytes), lane by lane; written even after a failure: the bytes of
-    // the records before the failing one must be complete
-    for (uint32_t q = fb; q < d; q += 16) {
-        const uint4 v = *L.out(q);
-        if (q + 16 <= d)
-            stu16(gout + q, v);
-        else
-            st_partial(gout + q, v, d - q);
-    }
-    *bad_rec = r0;
-    return !bad;
-}
-
-__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* wl, uint8_t* wi,
-                                            uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
-    return snappy_lane_t<true>(P, r0, r1, wl, wi, lane, sink, bad_rec);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -458,8 +117,6 @@ struct CoopLds {
     uint8_t slot[64];                     // element starts in the current output window
     uint8_t ring[kCoopRing];              // decoded history of the current record
 };
-// k_snappy_pipe runs the wave decoder in the wave's history image
-static_assert(sizeof(CoopLds) <= kOutCh * 1024, "wave decoder LDS must fit a history image");
 
 __device__ __forceinline__ bool coop_active(const FrameParams& P, const ScanState* st) {
     if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY || !st->any_mixed)
@@ -767,6 +424,362 @@ __device__ __forceinline__ void coop_file(const FrameParams& P, CoopLds& S, uint
 }
 }  // namespace
 
+// ------------------------------------------------------------------------------------------
+// snappy_lane: the lane decoder (round 3: dword-column LDS images). Each step of a lane emits the
+// piece its parser produced kD steps earlier, takes part in the cooperative flush, parses the next
+// piece, issues its far-history (or next descriptor) load and its input prefetch. Byte placement:
+//   * Row k of a lane's history / input image is one dword; a lane's rows are 1 KiB apart and all
+//     in its own bank, so any per-lane dword access of a wave is conflict-free, wherever the lanes
+//     are. The LDS address selects the dword; only the byte shift inside it is VALU work
+//     (v_alignbyte_b32). Round 2's [chunk][lane][16 B] image needed a select network over three
+//     16-byte chunks per piece (funnel32: 44 VALU) and a second one for the parser (funnel16).
+//   * A piece is placed destination-aligned: with r = d & 3, the four dwords of output bytes
+//     [d - r, d - r + 16) are written (pieces are capped at 16 - r bytes), the r bytes below d
+//     merged from the row as it stands (one v_bfi_b32). The source rows [q - r, q - r + 20) are
+//     read as five dwords and shifted by (q - r) & 3.
+//   * Literal bytes are read at parse time from the input image at the literal's own position
+//     (five rows, shift (s - r) & 3) and travel in the slot; far-copy bytes are loaded from the
+//     arena already destination-aligned (16 bytes at q - r), so they need no shift.
+// The four waves' rows are interleaved: row k of wave w, lane l is the dword at k * 1024 + w * 256
+// + 4 l of its image. The history image (64 rows, 64 KiB) starts at byte kColI of the workgroup's
+// LDS and its local addresses are 16-bit: the next row is one v_pk_add_u16 (the ring wraps with the
+// address); the input image (16 rows) is the first 16 KiB.
+// Measured on MI355X against round 2's decoder (same pipeline, one box, 308-test parity subset
+// green): static VALU per step 268 -> 217, executed VALU per C2 launch 4.95e8 -> 3.98e8 (PMC),
+// decode C2 1.19 -> 1.13 ms, C3 0.86 -> 0.80, C4 13.9 -> 13.6 (gpurun_out/r3k).
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr uint32_t kColRows = 64;                  // history rows per lane: 256 bytes
+constexpr uint32_t kColInRows = 16;                // input rows per lane: 64 bytes = kInCh chunks
+constexpr uint32_t kColWaves = kSnappyBlock / 64;
+constexpr uint32_t kColRow = kColWaves * 256;      // bytes per row of the four waves (1 KiB)
+constexpr uint32_t kColH = kColRows * kColRow;     // history image (64 KiB: 16-bit local addresses)
+constexpr uint32_t kColI = kColInRows * kColRow;   // input image (16 KiB)
+constexpr uint32_t kColLds = kColH + kColI;
+constexpr uint32_t kCoopSlice = kColH / kColWaves; // a wave's contiguous slice for the wave decoder
+static_assert(kColH == 65536, "history addresses wrap at 16 bits");
+static_assert(kColInRows == 4 * kInCh, "input image holds the input ring's chunks");
+static_assert(sizeof(CoopLds) <= kCoopSlice, "wave decoder LDS must fit a history slice");
+// live history: ring-copy sources reach kFarOff + 3 bytes below the destination, the emit writes
+// the 16 bytes from d - r; the flush reads complete blocks at most 127 bytes below d
+static_assert(kFarOff + 3 + 16 + 4 <= kColRows * 4, "history image must hold the copy reach");
+
+struct ColSlot {
+    uint4 in;        // input chunk in_c (load in flight)
+    uint4 aux;       // far-copy bytes [q - r, q - r + 16) or the next record's descriptor (in flight)
+    uint32_t x0, x1, x2, x3, x4;  // literal: input rows from (src - r) & ~3 (read at parse)
+    uint32_t in_c;
+    uint32_t n;      // piece length, 0 = bubble
+    uint32_t kind;   // 0 literal, 1 ring copy, 2 far copy, 3 far copy loaded from q (see the emit)
+    uint32_t q;      // ring copy: source output position; literal: byte shift of x0..x4
+    uint32_t desc;   // aux carries the next record's descriptor
+};
+__device__ __forceinline__ ColSlot col_empty_slot() {
+    ColSlot S;
+    S.in = zero4();
+    S.aux = zero4();
+    S.x0 = S.x1 = S.x2 = S.x3 = S.x4 = 0;
+    S.in_c = kNoChunk;
+    S.n = 0;
+    S.kind = 1;
+    S.q = 0;
+    S.desc = 0;
+    return S;
+}
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t col_ld(const uint8_t* L, uint32_t a) {
+    return *reinterpret_cast<const uint32_t*>(L + a);
+}
+__device__ __forceinline__ void col_st(uint8_t* L, uint32_t a, uint32_t v) { *reinterpret_cast<uint32_t*>(L + a) = v; }
+
+// history / input dword at a local address (the history image follows the input image)
+__device__ __forceinline__ uint32_t col_hld(const uint8_t* L, uint32_t a) { return col_ld(L + kColI, a); }
+__device__ __forceinline__ void col_hst(uint8_t* L, uint32_t a, uint32_t v) { col_st(L + kColI, a, v); }
+
+// Decode the record range [r0, r1) of this lane as one stream (as snappy_lane_t). L is the
+// workgroup's LDS base (input image, then history image).
+__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* L,
+                                                uint32_t wave, uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
+    const uint32_t wl = wave * 256u + lane * 4u;  // row 0 of this lane (both images)
+    // history / input row of a byte position (mod the ring), and the next row with wrap
+    auto hrow = [&](uint32_t b) __attribute__((always_inline)) { return ((b << 8) & (kColH - kColRow)) | wl; };
+    // v_pk_add_u16: the low half wraps at 64 KiB, the high half (0) stays 0
+    auto hnext = [&](uint32_t a) __attribute__((always_inline)) {
+        const u16x2 v = __builtin_bit_cast(u16x2, a) + u16x2{(uint16_t)kColRow, 0};
+        return __builtin_bit_cast(uint32_t, v);
+    };
+    auto irow = [&](uint32_t b) __attribute__((always_inline)) { return ((b << 8) & (kColI - kColRow)) | wl; };
+    auto inext = [&](uint32_t a) __attribute__((always_inline)) { return (a + kColRow) & (kColI - 1u); };
+
+    const bool live = r0 < r1;
+    uint8_t* const out = P.out;
+    const uint4 d0 = live ? P.rec_desc[r0] : zero4();
+    const uint64_t o0 = live ? P.out_off[r0] : 0;
+    uint8_t* const gout = out + o0;
+    // a far copy's 16 bytes are loaded from q - r: below the arena for a source in its first
+    // bytes (only the lane of a file's first record can meet this: kind 3)
+    const bool low_base = o0 < 3;
+    const uint8_t* const gout_m3 = gout - 3;  // never dereferenced below out: see low_base
+    const uint64_t start0 = ((uint64_t)d0.y << 32) | d0.x;
+    const uint64_t base = start0 & ~15ull;
+    const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
+    const uint32_t lastc = live && base < P.len ? (uint32_t)min((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
+    // prime the input image with chunks [0, 4)
+    uint32_t whi = live ? min(kInCh, lastc + 1) : 0u;
+    for (uint32_t c = 0; c < whi; c++) {
+        const uint4 v = sa[c];
+        const uint32_t a = wl | (c << 12);
+        col_st(L, a, v.x);
+        col_st(L, a + kColRow, v.y);
+        col_st(L, a + 2 * kColRow, v.z);
+        col_st(L, a + 3 * kColRow, v.w);
+    }
+    uint32_t cn = live ? whi : 0xFFFFFFFFu;
+
+    uint64_t k = r0;
+    uint32_t s = (uint32_t)(start0 - base), s_end = s + d0.z;
+    uint32_t pd = 0, rd_start = 0, rd_end = d0.w;
+    uint32_t rem = 0, eff = 0;
+    bool islit = false, bad = false, pdone = !live;
+    uint4 nd = zero4();
+    uint32_t nds = (live && r0 + 1 < r1) ? 0u : 3u;
+    uint32_t d = 0, fb = 0;
+
+    uint8_t* obase[4];
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++) {
+        const int src = (int)((16u * jj + (lane >> 2)) * 4);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
+        obase[jj] = out + (((uint64_t)hi << 32) | lo);
+    }
+
+    ColSlot S0 = col_empty_slot(), S1 = col_empty_slot(), S2 = col_empty_slot(), S3 = col_empty_slot();
+    uint32_t drain = 0, qsrc = 0;
+    // the next emit's source rows (ring copy) and shift, and the row holding bytes [d & ~3, d)
+    uint32_t wL0 = 0, wL1 = 0, wL2 = 0, wL3 = 0, wL4 = 0, wSh = 0, wP = 0;
+    uint32_t aD = hrow(0);  // history row of d
+    // the parser's window: rows s >> 2 and (s >> 2) + 1, read one step ahead
+    uint32_t Wa, Wb;
+    {
+        const uint32_t a = irow(s);
+        Wa = col_ld(L, a);
+        Wb = col_ld(L, inext(a));
+    }
+
+    auto step = [&](ColSlot& S, const ColSlot& N, const uint32_t j) __attribute__((always_inline)) {
+        drain += pdone ? 1u : 0u;
+        nd = sel4(S.desc != 0, S.aux, nd);
+        nds = S.desc ? 2u : nds;
+        const uint32_t pos = s;
+
+        // 2. flush owner exchange first (its LDS round trip overlaps the emit): this step's owners
+        // are lanes 16 (j % 4) .. + 15; a block is ready once the emit below completes it
+        const uint32_t fo = 16u * (j & 3u) + (lane >> 2), fpart = lane & 3u;
+        const uint32_t dn = d + S.n;
+        const bool fready = dn - fb >= 64;
+        const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fo * 4), (int)(fb | (fready ? 0x80000000u : 0u)));
+
+        // 3. emit the piece parsed kD steps ago: destination dwords of bytes [d - r, d - r + 16)
+        {
+            const bool ring = S.kind == 1;
+            uint32_t X0 = ring ? wL0 : S.x0, X1 = ring ? wL1 : S.x1, X2 = ring ? wL2 : S.x2, X3 = ring ? wL3 : S.x3,
+                     X4 = ring ? wL4 : S.x4;
+            const uint32_t sh = ring ? wSh : S.q;
+            uint32_t D0 = __builtin_amdgcn_alignbyte(X1, X0, sh), D1 = __builtin_amdgcn_alignbyte(X2, X1, sh),
+                     D2 = __builtin_amdgcn_alignbyte(X3, X2, sh), D3 = __builtin_amdgcn_alignbyte(X4, X3, sh);
+            const bool far = S.kind == 2;
+            D0 = far ? S.aux.x : D0;
+            D1 = far ? S.aux.y : D1;
+            D2 = far ? S.aux.z : D2;
+            D3 = far ? S.aux.w : D3;
+            // kind 3 (rare: a far source in the first bytes of the arena, lane of the file's first
+            // record): aux holds bytes [q, q + 16), shifted up by r here
+            if (__builtin_expect(__any(S.kind == 3), 0)) {
+                if (S.kind == 3) {
+                    const uint32_t u = 4u - (d & 3u);
+                    D0 = __builtin_amdgcn_alignbyte(S.aux.x, 0u, u);
+                    D1 = __builtin_amdgcn_alignbyte(S.aux.y, S.aux.x, u);
+                    D2 = __builtin_amdgcn_alignbyte(S.aux.z, S.aux.y, u);
+                    D3 = __builtin_amdgcn_alignbyte(S.aux.w, S.aux.z, u);
+                }
+            }
+            // bytes below d keep the row's content (v_bfi_b32); the shift uses the low 5 bits: 8 (d & 3)
+            const uint32_t hm = 0xFFFFFFFFu << ((d << 3) & 31u);
+            D0 = (D0 & hm) | (wP & ~hm);
+            const uint32_t a1 = hnext(aD), a2 = hnext(a1), a3 = hnext(a2);
+            col_hst(L, aD, D0);
+            col_hst(L, a1, D1);
+            col_hst(L, a2, D2);
+            col_hst(L, a3, D3);
+            d = dn;
+        }
+
+        // 4. cooperative flush: lane writes 16 bytes of owner fo's next 64-byte block if complete
+        // (rows fpos >> 2 .. + 3 of column fo: 16-byte aligned, no wrap inside); its reads go before
+        // the next emit's source reads, so the store waits for them only
+        {
+            const uint32_t fpos = (ofb & 0x7FFFFFFFu) + 16u * fpart;
+            const uint32_t fa = ((fpos << 8) & (kColH - kColRow)) | (wave * 256u + fo * 4u);
+            const uint4 fv = make_uint4(col_hld(L, fa), col_hld(L, fa + kColRow), col_hld(L, fa + 2 * kColRow),
+                                        col_hld(L, fa + 3 * kColRow));
+            // the NEXT slot: its destination row, and (ring copy) its five source rows
+            const uint32_t r2 = d & 3u;
+            aD = hrow(d);
+            wP = col_hld(L, aD);
+            const uint32_t src = N.q - r2;
+            wSh = src;  // alignbyte takes the low 2 bits
+            const uint32_t b0 = hrow(src), b1 = hnext(b0), b2 = hnext(b1), b3 = hnext(b2), b4 = hnext(b3);
+            wL0 = col_hld(L, b0);
+            wL1 = col_hld(L, b1);
+            wL2 = col_hld(L, b2);
+            wL3 = col_hld(L, b3);
+            wL4 = col_hld(L, b4);
+            st_out((ofb >> 31) ? obase[j & 3u] + fpos : sink, fv);
+            fb += ((lane >> 4) == (j & 3u) && fready) ? 64u : 0u;
+        }
+
+        // 4. parse the next piece into this slot
+        {
+            // v_alignbyte_b32 and the shifts use the low bits of their shift operand only
+            const uint32_t W0 = __builtin_amdgcn_alignbyte(Wb, Wa, pos);  // bytes s .. s + 3
+            const uint32_t W1 = __builtin_amdgcn_alignbyte(Wb >> ((pos << 3) & 31u), W0, 1u);  // s + 1 .. s + 4
+            const uint32_t tag = W0 & 0xFFu, t = tag & 3u, x = tag >> 2;
+            const bool avail = min((pos + 15) >> 4, lastc) < whi;
+            const bool is0 = t == 0, is1 = t == 1;
+            const bool is2 = t == 2;
+            const bool lng = x >= 60;
+            const uint32_t lmask = 0xFFFFFFFFu >> (((63u - x) << 3) & 31u);
+            uint32_t lit_long = (W1 & lmask) + 1u, lit_short = x + 1u;
+            uint32_t c1_len = (x & 7u) + 4u, c1_off = ((tag & 0xE0u) << 3) | (W1 & 0xFFu);
+            uint32_t c2_off = W1 & 0xFFFFu;
+            pin_v(lit_long);
+            pin_v(lit_short);
+            pin_v(c1_len);
+            pin_v(c1_off);
+            pin_v(c2_off);
+            const uint32_t lit_len = lng ? lit_long : lit_short;
+            const uint32_t len = is0 ? lit_len : (is1 ? c1_len : lit_short);
+            const uint32_t lit_hl = lng ? x - 58u : 1u;
+            const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
+            const uint32_t hl = is0 ? lit_hl : cp_hl;
+            const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
+            const uint32_t sleft = s_end - s;
+            const uint32_t lim = is0 ? sleft - hl : pd - rd_start;
+            const uint32_t key = (is0 ? len : off) - 1u;
+            const bool hbad = (hl > sleft) | (key >= lim) | (len > rd_end - pd);
+            const bool hdr = !pdone && rem == 0 && s < s_end && avail;
+            const bool badn = hdr && hbad, ok = hdr && !hbad;
+            bad = bad || badn;
+            const uint32_t sh = ok ? hl : 0u;
+            const uint32_t rem1 = ok ? len : rem, eff1 = ok ? off : eff;
+            const bool lit1 = ok ? t == 0 : islit;
+            const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
+            // destination-aligned pieces: at most 16 - r bytes (r = pd & 3); a literal's bytes also
+            // stay inside the window [s, s + 16) the availability check covers
+            const uint32_t r = pd & 3u;
+            const uint32_t cap = 16u - max(lit1 ? sh : 0u, r);
+            const uint32_t n = go ? min(rem1, lit1 ? cap : min(cap, eff1)) : 0u;
+            S.n = n;
+            S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
+            qsrc = pd - eff1;
+            // literal rows from (s + sh - r) & ~3 (the bytes below s + sh are masked at the emit)
+            const uint32_t ls = s + sh - r;
+            const uint32_t c0 = irow(ls), c1 = inext(c0), c2 = inext(c1), c3 = inext(c2), c4 = inext(c3);
+            S.x0 = col_ld(L, c0);
+            S.x1 = col_ld(L, c1);
+            S.x2 = col_ld(L, c2);
+            S.x3 = col_ld(L, c3);
+            S.x4 = col_ld(L, c4);
+            S.q = S.kind == 1 ? qsrc : ls;  // literal: the shift (low 2 bits) of x0..x4
+            s += sh + (lit1 ? n : 0u);
+            rem = rem1 - n;
+            pd += n;
+            eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
+            islit = lit1;
+            s = badn ? s_end : s;
+            uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
+            pin_v(at_end);
+            if (at_end) {
+                const bool bad_len = pd != rd_end;
+                bad = bad || bad_len;
+                rem = bad_len ? rd_end - pd : rem;
+                eff = bad_len ? 16u : eff;
+                islit = islit && !bad_len;
+                const bool more = k + 1 < r1;
+                const bool sw = !bad_len && more && nds == 2;
+                pdone = pdone || (!bad_len && !more);
+                k += sw ? 1u : 0u;
+                const uint64_t nstart = ((uint64_t)nd.y << 32) | nd.x;
+                s = sw ? (uint32_t)(nstart - base) : s;
+                s_end = sw ? s + nd.z : s_end;
+                rd_start = sw ? pd : rd_start;
+                rd_end = sw ? pd + nd.w : rd_end;
+                nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
+            }
+        }
+        // far history (destination-aligned: from q - r), or the next record's descriptor, or a placeholder
+        {
+            const bool want_desc = S.kind != 2 && nds == 0;
+            S.desc = want_desc ? 1u : 0u;
+            nds = want_desc ? 1u : nds;
+            const uint32_t r = (pd - S.n) & 3u;  // the piece's destination alignment
+            // 16 bytes from q - r would start below the arena: load from q, shift at the emit (kind 3)
+            const bool below = low_base && S.kind == 2 && qsrc < r;
+            S.kind = below ? 3u : S.kind;
+            const uint8_t* ap = S.kind >= 2 ? gout_m3 + (qsrc + 3u - (below ? 0u : r))
+                                            : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
+            S.aux = ld_far(ap);
+        }
+
+        // 5. input prefetch
+        {
+            const uint32_t a = s >> 4;
+            const bool take = cn <= lastc && cn < a + kInCh;
+            S.in = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
+            S.in_c = take ? cn : kNoChunk;
+            cn += take ? 1u : 0u;
+        }
+
+        // 6. land the next slot's input chunk, then read the next step's parser window
+        {
+            const bool landed = N.in_c != kNoChunk;
+            if (landed) {
+                const uint32_t a = wl | ((N.in_c & (kInCh - 1)) << 12);
+                col_st(L, a, N.in.x);
+                col_st(L, a + kColRow, N.in.y);
+                col_st(L, a + 2 * kColRow, N.in.z);
+                col_st(L, a + 3 * kColRow, N.in.w);
+            }
+            whi = landed ? N.in_c + 1 : whi;
+            const uint32_t a = irow(s);
+            Wa = col_ld(L, a);
+            Wb = col_ld(L, inext(a));
+        }
+    };
+
+    static_assert(kD == 4, "unrolled for four slots");
+    do {
+        step(S0, S1, 0);
+        step(S1, S2, 1);
+        step(S2, S3, 2);
+        step(S3, S0, 3);
+    } while (__any(drain < kD));
+    // the stream's tail (< 128 bytes) from the lane's own rows
+    for (uint32_t q = fb; q < d; q += 16) {
+        const uint32_t a = hrow(q);
+        const uint4 v = make_uint4(col_hld(L, a), col_hld(L, hnext(a)), col_hld(L, hnext(hnext(a))),
+                                   col_hld(L, hnext(hnext(hnext(a)))));
+        if (q + 16 <= d)
+            stu16(gout + q, v);
+        else
+            st_partial(gout + q, v, d - q);
+    }
+    *bad_rec = r0;
+    return !bad;
+}
+}  // namespace
+
 // rio_device_decode_batch: the files one after the other, every wave of the grid on each (a wave
 // that finishes its share of file f goes on to file f + 1 at once: no grid-wide step)
 __global__ void __launch_bounds__(64 * kCoopWaves) k_snappy_coop_batch(FrameBatch B) {
@@ -775,48 +788,6 @@ __global__ void __launch_bounds__(64 * kCoopWaves) k_snappy_coop_batch(FrameBatc
     for (uint32_t f = 0; f < B.n; f++)
         coop_file(B.f[f], lds[wv], threadIdx.x & 63u, (uint64_t)blockIdx.x * kCoopWaves + wv,
                   (uint64_t)gridDim.x * kCoopWaves);
-}
-
-__global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
-    __shared__ __attribute__((aligned(16))) uint8_t hist[kSnappyBlock / 64][kOutCh * 1024];
-    __shared__ __attribute__((aligned(16))) uint8_t inring[kSnappyBlock / 64][kInCh * 1024];
-    ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
-    if (!st->any_mixed) return;  // every record is one literal: k_copy_records copies them
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (coop_active(P, st)) {  // large records / past 32-bit positions: the wave-per-record decoder
-        coop_file(P, *reinterpret_cast<CoopLds*>(hist[wave]), lane, (uint64_t)blockIdx.x * (kSnappyBlock / 64) + wave,
-                  (uint64_t)gridDim.x * (kSnappyBlock / 64));
-        return;
-    }
-    const uint64_t n = st->n_records;
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint64_t g = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
-    uint8_t* sink = P.sink + g * 64;                               // the wave's placeholder line
-    // Records go to waves in chunks of 64 lanes x rpc consecutive records (each lane one contiguous
-    // range: one stream, no drain between its records). Chunk g is wave g's; a wave that finishes
-    // takes the next unclaimed chunk, so waves whose records decode slower, or that start later, do
-    // not hold the kernel's tail. About eight chunks per wave.
-    constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
-    const uint64_t rpc = n >= kCpw * 64 * waves ? n / (kCpw * 64 * waves) : 1;
-    const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
-    uint64_t chunk = g;
-    while (chunk < nchunks) {
-        const uint64_t r0 = min(chunk * per + lane * rpc, n), r1 = min(r0 + rpc, n);
-        uint64_t bad_rec = 0;
-        if (!snappy_lane(P, r0, r1, hist[wave], inring[wave], lane, sink, &bad_rec)) {
-            // a record of this lane did not decode: k_finish re-decodes the lane's records one
-            // thread each and flags the failing ones
-            const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
-            if (at < kFailLanes) {
-                P.fail_lanes[2 * at] = r0;
-                P.fail_lanes[2 * at + 1] = r1;
-            }
-        }
-        uint32_t next = 0;
-        if (lane == 0) next = atomicAdd(&st->pipe_next, 1u);
-        chunk = waves + __shfl(next, 0);
-    }
 }
 
 // rio_device_decode_batch: one launch for every lane-decoder file of the batch. The lanes of the grid
@@ -829,18 +800,50 @@ __device__ __forceinline__ bool pipe_active(const FrameParams& P) {
            !snappy_wide(P, st) && !(st->n_records && st->total_bytes / st->n_records >= P.coop_min);
 }
 
+__global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kColLds];
+    ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK || st->capacity_fail || st->compression != RIO_COMP_SNAPPY) return;
+    if (!st->any_mixed) return;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (coop_active(P, st)) {
+        coop_file(P, *reinterpret_cast<CoopLds*>(lds + kColI + wave * kCoopSlice), lane,
+                  (uint64_t)blockIdx.x * (kSnappyBlock / 64) + wave, (uint64_t)gridDim.x * (kSnappyBlock / 64));
+        return;
+    }
+    const uint64_t n = st->n_records;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t g = (uint64_t)wave * gridDim.x + blockIdx.x;
+    uint8_t* sink = P.sink + g * 64;
+    constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
+    const uint64_t rpc = n >= kCpw * 64 * waves ? n / (kCpw * 64 * waves) : 1;
+    const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
+    uint64_t chunk = g;
+    while (chunk < nchunks) {
+        const uint64_t r0 = min(chunk * per + lane * rpc, n), r1 = min(r0 + rpc, n);
+        uint64_t bad_rec = 0;
+        if (!snappy_lane(P, r0, r1, lds, wave, lane, sink, &bad_rec)) {
+            const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
+            if (at < kFailLanes) {
+                P.fail_lanes[2 * at] = r0;
+                P.fail_lanes[2 * at + 1] = r1;
+            }
+        }
+        uint32_t next = 0;
+        if (lane == 0) next = atomicAdd(&st->pipe_next, 1u);
+        chunk = waves + __shfl(next, 0);
+    }
+}
+
 __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B) {
-    __shared__ __attribute__((aligned(16))) uint8_t hist[kSnappyBlock / 64][kOutCh * 1024];
-    __shared__ __attribute__((aligned(16))) uint8_t inring[kSnappyBlock / 64][kInCh * 1024];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kColLds];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;  // waves numbered across workgroups first
+    const uint64_t wg = (uint64_t)wave * gridDim.x + blockIdx.x;
     uint64_t N = 0;
     for (uint32_t f = 0; f < B.n; f++)
         if (pipe_active(B.f[f])) N += B.f[f].state->n_records;
     if (N == 0) return;
-    // the fewest records per lane whose whole-wave shares (ceil per file) fit the grid: every wave
-    // of the grid is resident at once (2 per SIMD), so a share past it would run as a second round
     uint64_t rpl = (N + 64 * waves - 1) / (64 * waves);
     for (;;) {
         uint64_t need = 0;
@@ -860,7 +863,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
             const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
             uint8_t* sink = P.sink + wg * 64;
             uint64_t bad_rec = 0;
-            if (!snappy_lane(P, r0, r1, hist[wave], inring[wave], lane, sink, &bad_rec)) {
+            if (!snappy_lane(P, r0, r1, lds, wave, lane, sink, &bad_rec)) {
                 const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
                 if (at < kFailLanes) {
                     P.fail_lanes[2 * at] = r0;
