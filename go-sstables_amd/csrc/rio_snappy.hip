@@ -44,10 +44,11 @@ constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 #ifndef RIO_CHUNKS_PER_WAVE
 #define RIO_CHUNKS_PER_WAVE 8
 #endif
-// copies reaching further back than kFarOff read the output arena (flushed: see snappy_lane)
-constexpr uint32_t kFarOff = 16 * (kD - 1) + 16 + 128;
+// copies reaching further back than kFarOff read the output arena (flushed: see snappy_lane); the
+// flush is pipelined one step (+16 bytes of lag)
+constexpr uint32_t kFarOff = 16 * (kD - 1) + 16 + 128 + 16;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
-static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128, "far history must be flushed before the parser reads it");
+static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128 + 16, "far history must be flushed before the parser reads it");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
 
 // materialize x in a VGPR here: the selects that use it can no longer be turned into branches that
@@ -559,6 +560,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     // the next emit's source rows (ring copy) and shift, and the row holding bytes [d & ~3, d)
     uint32_t wL0 = 0, wL1 = 0, wL2 = 0, wL3 = 0, wL4 = 0, wSh = 0, wP = 0;
     uint32_t aD = hrow(0);  // history row of d
+    // the flush in flight: this step's owners' blocks, read during the previous step
+    uint4 pfv = zero4();
+    uint32_t pofb = 0, pfpos = 0;
+    bool pready = false;
     // the parser's window: rows s >> 2 and (s >> 2) + 1, read one step ahead
     uint32_t Wa, Wb;
     {
@@ -573,14 +578,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         nds = S.desc ? 2u : nds;
         const uint32_t pos = s;
 
-        // 2. flush owner exchange first (its LDS round trip overlaps the emit): this step's owners
-        // are lanes 16 (j % 4) .. + 15; a block is ready once the emit below completes it
-        const uint32_t fo = 16u * (j & 3u) + (lane >> 2), fpart = lane & 3u;
-        const uint32_t dn = d + S.n;
-        const bool fready = dn - fb >= 64;
-        const uint32_t ofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fo * 4), (int)(fb | (fready ? 0x80000000u : 0u)));
-
-        // 3. emit the piece parsed kD steps ago: destination dwords of bytes [d - r, d - r + 16)
+        // 2. emit the piece parsed kD steps ago: destination dwords of bytes [d - r, d - r + 16)
         {
             const bool ring = S.kind == 1;
             uint32_t X0 = ring ? wL0 : S.x0, X1 = ring ? wL1 : S.x1, X2 = ring ? wL2 : S.x2, X3 = ring ? wL3 : S.x3,
@@ -612,31 +610,20 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             col_hst(L, a1, D1);
             col_hst(L, a2, D2);
             col_hst(L, a3, D3);
-            d = dn;
+            d += S.n;
         }
 
-        // 4. cooperative flush: lane writes 16 bytes of owner fo's next 64-byte block if complete
-        // (rows fpos >> 2 .. + 3 of column fo: 16-byte aligned, no wrap inside); its reads go before
-        // the next emit's source reads, so the store waits for them only
+        // 3. cooperative flush, pipelined one step: the owners of this step (lanes 16 (j % 4) .. + 15)
+        // had their ready blocks read during the previous step; every quad of lanes stores one
+        // owner's 64-byte block (16 bytes per lane). Then the NEXT step's owners publish their flush
+        // state; their blocks are read at the end of this step, so no LDS round trip sits in front of
+        // a store (the far threshold covers the extra step of lag).
         {
-            const uint32_t fpos = (ofb & 0x7FFFFFFFu) + 16u * fpart;
-            const uint32_t fa = ((fpos << 8) & (kColH - kColRow)) | (wave * 256u + fo * 4u);
-            const uint4 fv = make_uint4(col_hld(L, fa), col_hld(L, fa + kColRow), col_hld(L, fa + 2 * kColRow),
-                                        col_hld(L, fa + 3 * kColRow));
-            // the NEXT slot: its destination row, and (ring copy) its five source rows
-            const uint32_t r2 = d & 3u;
-            aD = hrow(d);
-            wP = col_hld(L, aD);
-            const uint32_t src = N.q - r2;
-            wSh = src;  // alignbyte takes the low 2 bits
-            const uint32_t b0 = hrow(src), b1 = hnext(b0), b2 = hnext(b1), b3 = hnext(b2), b4 = hnext(b3);
-            wL0 = col_hld(L, b0);
-            wL1 = col_hld(L, b1);
-            wL2 = col_hld(L, b2);
-            wL3 = col_hld(L, b3);
-            wL4 = col_hld(L, b4);
-            st_out((ofb >> 31) ? obase[j & 3u] + fpos : sink, fv);
-            fb += ((lane >> 4) == (j & 3u) && fready) ? 64u : 0u;
+            st_out((pofb >> 31) ? obase[j & 3u] + pfpos : sink, pfv);
+            fb += ((lane >> 4) == (j & 3u) && pready) ? 64u : 0u;
+            const uint32_t fo = 16u * ((j + 1) & 3u) + (lane >> 2);
+            pready = d - fb >= 64;
+            pofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fo * 4), (int)(fb | (pready ? 0x80000000u : 0u)));
         }
 
         // 4. parse the next piece into this slot
@@ -752,6 +739,26 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
                 col_st(L, a + 3 * kColRow, N.in.w);
             }
             whi = landed ? N.in_c + 1 : whi;
+        }
+        // 7. the next owners' blocks (rows fpos >> 2 .. + 3 of column fo: 16-byte aligned, no wrap
+        // inside), the next emit's destination row and source rows, the next parser window
+        {
+            const uint32_t fo = 16u * ((j + 1) & 3u) + (lane >> 2);
+            pfpos = (pofb & 0x7FFFFFFFu) + 16u * (lane & 3u);
+            const uint32_t fa = ((pfpos << 8) & (kColH - kColRow)) | (wave * 256u + fo * 4u);
+            pfv = make_uint4(col_hld(L, fa), col_hld(L, fa + kColRow), col_hld(L, fa + 2 * kColRow),
+                             col_hld(L, fa + 3 * kColRow));
+            const uint32_t r2 = d & 3u;
+            aD = hrow(d);
+            wP = col_hld(L, aD);
+            const uint32_t src = N.q - r2;
+            wSh = src;  // alignbyte takes the low 2 bits
+            const uint32_t b0 = hrow(src), b1 = hnext(b0), b2 = hnext(b1), b3 = hnext(b2), b4 = hnext(b3);
+            wL0 = col_hld(L, b0);
+            wL1 = col_hld(L, b1);
+            wL2 = col_hld(L, b2);
+            wL3 = col_hld(L, b3);
+            wL4 = col_hld(L, b4);
             const uint32_t a = irow(s);
             Wa = col_ld(L, a);
             Wb = col_ld(L, inext(a));
