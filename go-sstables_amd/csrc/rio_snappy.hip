@@ -611,16 +611,29 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             col_hst(L, a2, D2);
             col_hst(L, a3, D3);
             d += S.n;
+            // the NEXT slot: its destination row and (ring copy) its five source rows, read right
+            // after this emit's writes so a whole step hides their latency
+            const uint32_t r2 = d & 3u;
+            aD = hrow(d);
+            wP = col_hld(L, aD);
+            const uint32_t src = N.q - r2;
+            wSh = src;  // alignbyte takes the low 2 bits
+            const uint32_t b0 = hrow(src), b1 = hnext(b0), b2 = hnext(b1), b3 = hnext(b2), b4 = hnext(b3);
+            wL0 = col_hld(L, b0);
+            wL1 = col_hld(L, b1);
+            wL2 = col_hld(L, b2);
+            wL3 = col_hld(L, b3);
+            wL4 = col_hld(L, b4);
         }
 
-        // 3. cooperative flush, pipelined one step: the owners of this step (lanes 16 (j % 4) .. + 15)
-        // had their ready blocks read during the previous step; every quad of lanes stores one
-        // owner's 64-byte block (16 bytes per lane). Then the NEXT step's owners publish their flush
-        // state; their blocks are read at the end of this step, so no LDS round trip sits in front of
-        // a store (the far threshold covers the extra step of lag).
+        // 3. cooperative flush, pipelined one step: the NEXT step's owners (lanes 16 ((j + 1) % 4) ..
+        // + 15) publish their flush state now and their blocks are read at the end of this step; the
+        // blocks of this step's owners, read during the previous step, are stored after the parse.
+        // So no LDS round trip sits in front of a store (the far threshold covers the step of lag).
+        const uint4 fv_now = pfv;
+        const uint32_t ofb_now = pofb, fpos_now = pfpos;
+        const bool ready_now = pready;
         {
-            st_out((pofb >> 31) ? obase[j & 3u] + pfpos : sink, pfv);
-            fb += ((lane >> 4) == (j & 3u) && pready) ? 64u : 0u;
             const uint32_t fo = 16u * ((j + 1) & 3u) + (lane >> 2);
             pready = d - fb >= 64;
             pofb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fo * 4), (int)(fb | (pready ? 0x80000000u : 0u)));
@@ -705,6 +718,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
                 nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
             }
         }
+        // this step's owners' blocks (the far-history load below is issued after the store)
+        st_out((ofb_now >> 31) ? obase[j & 3u] + fpos_now : sink, fv_now);
+        fb += ((lane >> 4) == (j & 3u) && ready_now) ? 64u : 0u;
+
         // far history (destination-aligned: from q - r), or the next record's descriptor, or a placeholder
         {
             const bool want_desc = S.kind != 2 && nds == 0;
@@ -741,24 +758,13 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             whi = landed ? N.in_c + 1 : whi;
         }
         // 7. the next owners' blocks (rows fpos >> 2 .. + 3 of column fo: 16-byte aligned, no wrap
-        // inside), the next emit's destination row and source rows, the next parser window
+        // inside), the next parser window
         {
             const uint32_t fo = 16u * ((j + 1) & 3u) + (lane >> 2);
             pfpos = (pofb & 0x7FFFFFFFu) + 16u * (lane & 3u);
             const uint32_t fa = ((pfpos << 8) & (kColH - kColRow)) | (wave * 256u + fo * 4u);
             pfv = make_uint4(col_hld(L, fa), col_hld(L, fa + kColRow), col_hld(L, fa + 2 * kColRow),
                              col_hld(L, fa + 3 * kColRow));
-            const uint32_t r2 = d & 3u;
-            aD = hrow(d);
-            wP = col_hld(L, aD);
-            const uint32_t src = N.q - r2;
-            wSh = src;  // alignbyte takes the low 2 bits
-            const uint32_t b0 = hrow(src), b1 = hnext(b0), b2 = hnext(b1), b3 = hnext(b2), b4 = hnext(b3);
-            wL0 = col_hld(L, b0);
-            wL1 = col_hld(L, b1);
-            wL2 = col_hld(L, b2);
-            wL3 = col_hld(L, b3);
-            wL4 = col_hld(L, b4);
             const uint32_t a = irow(s);
             Wa = col_ld(L, a);
             Wb = col_ld(L, inext(a));

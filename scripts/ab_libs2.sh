@@ -2,6 +2,7 @@
 # Parity subset on the current librio.so, then interleaved bench lines of librio.so against another build.
 # usage: scripts/ab_libs2.sh <tag> <other-lib-tag> [configs]   (other = go-sstables_amd/librio_<tag>.so)
 set -u
+# OTHER: one or more lib tags, space-separated
 TAG=$1; OTHER=$2; CFGS=${3:-"c2 c3 c4"}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_batch.py tests/test_gpu_codec_errors.py \
     tests/test_gpu_literal.py tests/test_gpu_reader_api.py tests/test_gpu_snappy_align.py tests/test_gpu_wide.py \
