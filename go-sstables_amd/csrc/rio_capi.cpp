@@ -1239,19 +1239,20 @@ static int readat_expand(rio_reader* r, uint64_t rec, const ReadAtResult& res, c
     return RIO_OK;
 }
 
-static int readat_check(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil) {
+static int readat_check(rio_reader* r, const uint8_t** data, uint64_t* len, int* is_nil, bool seek) {
     if (data) *data = nullptr;
     if (len) *len = 0;
     if (is_nil) *is_nil = 0;
     if (!r->open || r->closed) return RIO_ERR_STATE;
-    if (r->version < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
+    // SeekNext: "unsupported on files with version lower than v2" (mmap_reader.go:62-64)
+    if (seek && r->version < RIO_VERSION2) return RIO_ERR_UNSUPPORTED;
     return RIO_OK;
 }
 
 extern "C" int rio_reader_read_next_at(rio_reader* r, uint64_t offset, const uint8_t** data, uint64_t* len,
                                        int* is_nil) {
     if (!r) return RIO_ERR_ARG;
-    if (int rc = readat_check(r, data, len, is_nil)) return rc;
+    if (int rc = readat_check(r, data, len, is_nil, false)) return rc;
     tl_det = LastDetail{0, 0, offset};
     const ReadAtIndex* x = readat_index(r);
     const uint64_t i = x->find(offset);
@@ -1267,7 +1268,7 @@ extern "C" int rio_reader_seek_next(rio_reader* r, uint64_t offset, uint64_t* re
                                     uint64_t* len, int* is_nil) {
     if (!r) return RIO_ERR_ARG;
     if (rec_offset) *rec_offset = 0;
-    if (int rc = readat_check(r, data, len, is_nil)) return rc;
+    if (int rc = readat_check(r, data, len, is_nil, true)) return rc;
     tl_det = LastDetail{0, 0, offset};
     const uint64_t seek_len = r->seek_len.load(std::memory_order_relaxed);
     const ReadAtIndex* x = readat_index(r);
@@ -1566,7 +1567,7 @@ extern "C" int rio_index_open(rio_ctx* ctx, const uint8_t* file, uint64_t len, r
     if (!rc && len >= RIO_FILE_HEADER_BYTES) {
         const uint32_t v = file[0] | (uint32_t)file[1] << 8 | (uint32_t)file[2] << 16 | (uint32_t)file[3] << 24;
         const uint32_t c = file[4] | (uint32_t)file[5] << 8 | (uint32_t)file[6] << 16 | (uint32_t)file[7] << 24;
-        if (v >= RIO_VERSION3 && v <= RIO_VERSION4 && c != RIO_COMP_NONE && c <= RIO_COMP_LZW) rc = index_build_view(x, file, len);
+        if (v >= RIO_VERSION1 && v <= RIO_VERSION4 && c != RIO_COMP_NONE && c <= RIO_COMP_LZW) rc = index_build_view(x, file, len);
     }
     if (rc) {
         for (DevBuf* b : {&x->file, &x->v_out, &x->v_off, &x->v_rec, &x->v_flags, &x->v_P, &x->v_R}) b->release();

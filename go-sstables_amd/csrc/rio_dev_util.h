@@ -26,29 +26,6 @@ __device__ inline int uvarint_buf(const uint8_t* p, uint64_t n, uint64_t& x) {
     return 0;
 }
 
-// Re-parse an already validated record header: sizes and header length, no checks.
-__device__ __forceinline__ uint64_t vread(const uint8_t* f, uint64_t& i) {
-    uint64_t v = 0;
-    uint32_t sh = 0, b;
-    do {
-        b = f[i++];
-        v |= (uint64_t)(b & 0x7F) << sh;
-        sh += 7;
-    } while ((b & 0x80) && sh < 70);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t header_fields_fast(const uint8_t* f, uint64_t p, uint32_t ver, uint64_t& u,
-                                                       uint64_t& c) {
-    uint64_t i = p;
-    (void)vread(f, i);  // magic
-    i++;                // nil byte
-    u = vread(f, i);
-    c = vread(f, i);
-    if (ver == RIO_VERSION4) (void)vread(f, i);  // crc
-    return (uint32_t)(i - p);
-}
-
 // ---- 16-byte values: unaligned global access (gfx950 unaligned mode), byte shifts -----------
 typedef uint4 __attribute__((aligned(1))) u4u;
 

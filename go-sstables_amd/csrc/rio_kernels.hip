@@ -88,21 +88,43 @@ struct Hdr {
 
 __device__ __forceinline__ int later_field(int e) { return e == RIO_EOF ? RIO_EOF_HEADER : e; }
 
-// readRecordHeaderV4 (common_reader.go:110-151) / readRecordHeaderV3 (:83-108)
+// readRecordHeaderV4 (common_reader.go:110-151) / readRecordHeaderV3 (:83-108) / readRecordHeaderV2
+// (:61-81: no nil byte, no CRC)
 template <class B>
 __device__ __forceinline__ int parse_header_t(B& get, uint64_t p, uint64_t avail, uint64_t cap, uint32_t ver, Hdr& h,
                                               const uint32_t* crc_tab = nullptr) {
-    SrcT<B> s{get, p, avail, 0, cap};
-    uint64_t m = 0;
     h.nil = 0;
     h.hdr_len = 0;
+    if (ver == RIO_VERSION1) {
+        // readRecordHeaderV1 (common_reader.go:46-59) after io.ReadFull of 20 bytes (file_reader.go:282-293):
+        // nothing left -> io.EOF, a partial header -> io.ErrUnexpectedEOF; no zero-tail rule
+        h.magic_len = 0;
+        if (avail == 0) return RIO_EOF;
+        if (avail < RIO_RECORD_HEADER_V1_BYTES) return RIO_ERR_UNEXPECTED_EOF;
+        uint32_t m = 0;
+        uint64_t u = 0, c = 0;
+        for (uint32_t i = 0; i < 4; i++) m |= (uint32_t)get(p + i) << (8 * i);
+        if (m != RIO_MAGIC) return RIO_ERR_MAGIC;
+        for (uint32_t i = 0; i < 8; i++) {
+            u |= (uint64_t)get(p + 4 + i) << (8 * i);
+            c |= (uint64_t)get(p + 12 + i) << (8 * i);
+        }
+        h.u = u;
+        h.c = c;
+        h.hdr_len = RIO_RECORD_HEADER_V1_BYTES;
+        return RIO_OK;
+    }
+    SrcT<B> s{get, p, avail, 0, cap};
+    uint64_t m = 0;
     int e = read_uvarint(s, m);
     h.magic_len = (uint32_t)s.pos;
     if (e) return e;
     if (m != RIO_MAGIC) return RIO_ERR_MAGIC;
-    uint32_t nb;
-    e = src_byte(s, nb);
-    if (e) return later_field(e);
+    uint32_t nb = 0;
+    if (ver >= RIO_VERSION3) {
+        e = src_byte(s, nb);
+        if (e) return later_field(e);
+    }
     e = read_uvarint(s, h.u);
     if (e) return later_field(e);
     e = read_uvarint(s, h.c);
@@ -228,11 +250,22 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
     if (p + 32 <= len) {
         const uint4 a = ldu16(f + p), b = ldu16(f + p + 16);
         const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        if ((a.x & 0xFFFFFFu) == 0x4C8D91u) {
+        if (ver == RIO_VERSION1 ? a.x == RIO_MAGIC : (a.x & 0xFFFFFFu) == 0x4C8D91u) {
+            // v3 / v4: the nil byte at 3, the sizes from 4; v2: no nil byte (readRecordHeaderV2)
+            // v1: fixed 20 bytes, LE u64 sizes at 4 and 12 (readRecordHeaderV1)
+            const uint32_t hb = ver >= RIO_VERSION3 ? 4u : 3u;
             uint64_t u = 0, c = 0, crc = 0;
-            const uint32_t nu = varint8(win8(w, 4), u);
-            const uint32_t nc = nu ? varint8(win8(w, 4 + nu), c) : 0;
-            uint32_t hl = 4 + nu + nc;
+            uint32_t nu, nc;
+            if (ver == RIO_VERSION1) {
+                u = ((uint64_t)a.z << 32) | a.y;
+                c = ((uint64_t)b.x << 32) | a.w;
+                nu = 8;
+                nc = 9;  // hb (3) + 8 + 9 = 20
+            } else {
+                nu = varint8(win8(w, hb), u);
+                nc = nu ? varint8(win8(w, hb + nu), c) : 0;
+            }
+            uint32_t hl = hb + nu + nc;
             bool ok = nu && nc;
             uint32_t act = 0;
             if (ok && ver == RIO_VERSION4) {
@@ -250,7 +283,7 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
                 hl += ncrc;
             }
             if (ok) {
-                const bool nil = ((a.x >> 24) & 0xFF) == 1;
+                const bool nil = ver >= RIO_VERSION3 && ((a.x >> 24) & 0xFF) == 1;
                 const uint64_t plen = comp != RIO_COMP_NONE ? c : u;
                 const uint64_t avail = len - p - hl;
                 uint64_t dl = plen;
@@ -269,7 +302,7 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
                     h.exp_crc = crc;
                     h.act_crc = act;
                     h.hdr_len = hl;
-                    h.magic_len = 3;
+                    h.magic_len = ver == RIO_VERSION1 ? 0 : 3;
                     h.nil = nil;
                     if (nil) {  // file_reader.go:96-99: nil => no payload bytes
                         next = p + hl;
@@ -353,7 +386,6 @@ __device__ __forceinline__ int file_header_status(const FrameParams& P, uint32_t
     c = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
     if (v > RIO_VERSION4 || v < RIO_VERSION1) return RIO_ERR_VERSION;
     if (c > RIO_COMP_LZW) return RIO_ERR_COMPRESSION_TYPE;
-    if (v < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;  // reference reader keeps these
     return RIO_OK;
 }
 
@@ -398,8 +430,6 @@ __device__ void init_state(const FrameParams& P) {
     } else if (c > RIO_COMP_LZW) {
         hs = RIO_ERR_COMPRESSION_TYPE;
         st->det0 = c;
-    } else if (v < RIO_VERSION3) {
-        hs = RIO_ERR_UNSUPPORTED;  // reference reader keeps these
     }
     st->hdr_status = hs;
 }
@@ -415,10 +445,14 @@ __device__ __forceinline__ uint64_t chunk_end(const FrameParams& P, uint64_t c) 
     return e < P.len ? e : P.len;
 }
 
-// First position in [cs, ce) holding the canonical magic bytes 91 8d 4c whose header and payload
-// validate under FileReader semantics (CRC for v4). Speculative; stitched by the scan.
+// bytes 1 and 2 of a record's magic: 8d 4c (uvarint 0x130691, v2..v4), 06 13 (LE u32, v1)
+__device__ __forceinline__ uint32_t magic3(uint32_t ver) { return ver == RIO_VERSION1 ? 0x130691u : 0x4C8D91u; }
+
+// First position in [cs, ce) holding the canonical magic bytes 91 8d 4c (v1: 91 06 13) whose header
+// and payload validate under FileReader semantics (CRC for v4). Speculative; stitched by the scan.
 __device__ uint64_t find_entry(const FrameParams& P, uint64_t cs, uint64_t ce, uint32_t ver, uint32_t comp) {
     const uint8_t* f = P.file;
+    const uint32_t m3 = magic3(ver);
     for (uint64_t q = cs & ~15ull; q < ce; q += 16) {
         const uint4 w = *reinterpret_cast<const uint4*>(f + q);
         uint32_t ws[4] = {w.x, w.y, w.z, w.w};
@@ -431,7 +465,7 @@ __device__ uint64_t find_entry(const FrameParams& P, uint64_t cs, uint64_t ce, u
                 hit &= hit - 1;
                 uint64_t p = q + 4 * k + b;
                 if (p < cs || p >= ce || p + 2 >= P.len) continue;
-                if (f[p + 1] != 0x8D || f[p + 2] != 0x4C) continue;
+                if (f[p + 1] != ((m3 >> 8) & 0xFF) || f[p + 2] != (m3 >> 16)) continue;
                 Hdr h;
                 uint64_t nx, ol, pd, lf;
                 if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd, lf) == RIO_OK) return p;
@@ -587,7 +621,7 @@ __device__ __forceinline__ uint32_t bytes_eq(uint32_t d, uint32_t v4) {
 // candidate bits of the 16 positions q .. q+15 in [lo, hi) (91 8d 4c at the position, the magic
 // inside the file); d = the 16 bytes at q plus the next 4
 __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t q, uint64_t lo, uint64_t hi,
-                                               uint64_t len) {
+                                               uint64_t len, uint32_t m3) {
     // positions holding 0x91 (SWAR exact byte compare, byte high bits gathered into 16 bits); only
     // those (~1 in 256 bytes) get the full 3-byte test
     uint32_t m91 = 0;
@@ -605,7 +639,7 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
         const uint32_t d0 = k == 0 ? d[0] : (k == 1 ? d[1] : (k == 2 ? d[2] : d[3]));
         const uint32_t d1 = k == 0 ? d[1] : (k == 1 ? d[2] : (k == 2 ? d[3] : d[4]));
         const uint32_t x = __builtin_amdgcn_alignbyte(d1, d0, i & 3) & 0xFFFFFFu;
-        if (x == 0x4C8D91u && q + i + 2 < len) mask |= 1u << i;
+        if (x == m3 && q + i + 2 < len) mask |= 1u << i;
     }
     return mask;
 }
@@ -687,7 +721,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
                 masks[j] = 0;
                 if (q < ce) {
                     const uint32_t d[5] = {blk[j].x, blk[j].y, blk[j].z, blk[j].w, tail[j]};
-                    masks[j] = magic_mask(d, q, ws, ce, P.len);
+                    masks[j] = magic_mask(d, q, ws, ce, P.len, magic3(ver));
                 }
             }
             // list slots of the four blocks' candidates (file order: block j, then lane) from two
@@ -887,7 +921,7 @@ __device__ bool fused_totals(const FrameParams& P, bool write) {
         st->status = RIO_EOF;  // chain ended exactly at the file end
         st->status_offset = val(0);
     }
-    if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
+    if (st->status == RIO_ERR_MAGIC && st->version != RIO_VERSION1) st->zero_from = st->status_offset + st->det0;
     st->lb_fused = 1;
     return true;
 }
@@ -1011,7 +1045,7 @@ __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
     // total.key is chunk 0's forced entry (8): total describes the true chain unless broken.
     if (total.broken) {
         slow_path(P, ver, comp);
-        if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
+        if (st->status == RIO_ERR_MAGIC && st->version != RIO_VERSION1) st->zero_from = st->status_offset + st->det0;
         return;
     }
     st->n_records = total.cnt;
@@ -1026,7 +1060,7 @@ __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
         st->status = RIO_EOF;  // chain ended exactly at the file end
         st->status_offset = total.out;
     }
-    if (st->status == RIO_ERR_MAGIC) st->zero_from = st->status_offset + st->det0;
+    if (st->status == RIO_ERR_MAGIC && st->version != RIO_VERSION1) st->zero_from = st->status_offset + st->det0;
 }
 
 // Header length of a snappy stream that is one literal element producing exactly `len` bytes with
@@ -1540,6 +1574,8 @@ __device__ __forceinline__ int read_at_locate(B& get, uint64_t len, uint32_t ver
     r.len = 0;
     r.det0 = r.det1 = 0;
     if (off > len) return RIO_ERR_INVALID_OFFSET;  // x/exp/mmap ReadAt bounds
+    // readNextAtV1 (mmap_reader.go:205-221): a 20-byte ReadAt short of its buffer fails wrapping io.EOF
+    if (ver == RIO_VERSION1 && len - off < RIO_RECORD_HEADER_V1_BYTES) return RIO_EOF_HEADER;
     const uint64_t wmax = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : RIO_RECORD_HEADER_V3_MAX;
     const uint64_t w = len - off < wmax ? len - off : wmax;
     if (w == 0) return RIO_EOF;  // bare io.EOF
@@ -1606,7 +1642,6 @@ __global__ void k_read_at(const uint8_t* f, uint64_t len, uint64_t off, uint8_t*
         comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
         if (ver > RIO_VERSION4 || ver < RIO_VERSION1) e = RIO_ERR_VERSION;
         else if (comp > RIO_COMP_LZW) e = RIO_ERR_COMPRESSION_TYPE;
-        else if (ver < RIO_VERSION3) e = RIO_ERR_UNSUPPORTED;
     }
     if (e == RIO_OK) e = read_at_dev(f, len, ver, comp, off, out, out_cap, r, true);
     r.status = e;
@@ -1672,7 +1707,7 @@ __device__ __forceinline__ int file_header_dev(const uint8_t* f, uint64_t len, u
     comp = f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
     if (ver > RIO_VERSION4 || ver < RIO_VERSION1) return RIO_ERR_VERSION;
     if (comp > RIO_COMP_LZW) return RIO_ERR_COMPRESSION_TYPE;
-    if (ver < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
+    if (ver < RIO_VERSION2) return RIO_ERR_UNSUPPORTED;  // SeekNext: mmap_reader.go:62-64
     return RIO_OK;
 }
 

@@ -58,8 +58,17 @@ def _open_error(status: int, path: str, d0: int, what: str, size: int = -1) -> G
     return wrap(f"error while parsing header of '{path}'", inner)
 
 
-def read_next_error(rc: int, path: str, d0: int, d1: int) -> GoError:
-    """FileReader.ReadNext's error for a terminal status of the whole-file decode (file_reader.go:61-131)."""
+def read_next_error(rc: int, path: str, d0: int, d1: int, version: int = 4) -> GoError:
+    """FileReader.ReadNext's error for a terminal status of the whole-file decode (file_reader.go:61-131;
+    v1 files: readNextV1, :282-320)."""
+    if version == 1:
+        # io.ReadFull of the fixed 20-byte header, then readRecordHeaderV1; no zero-tail rule
+        if rc in (L.RIO_EOF, L.RIO_ERR_UNEXPECTED_EOF) and d0 != 1:
+            return wrap(f"error while reading record header of '{path}'", _base_error(rc))
+        if rc == L.RIO_ERR_MAGIC:
+            return wrap(f"error while parsing record header of '{path}'", MagicNumberMismatchErr)
+        if rc in (L.RIO_ERR_DECOMPRESS, L.RIO_EOF_CODEC):  # :311-316 wraps the codec's error
+            return wrap(f"error while decompressing record of '{path}'", ErrCorrupt if rc == L.RIO_ERR_DECOMPRESS else EOF)
     if rc in (L.RIO_EOF_ZERO_TAIL, L.RIO_EOF_CODEC):
         return EOF  # file_reader.go:89-90 (zero tail) / :119-121 (gzip's io.EOF): bare io.EOF
     if rc == L.RIO_ERR_MAGIC:
@@ -162,7 +171,7 @@ class FileReader(_Reader):
         if rc == L.RIO_ERR_STATE:
             return self._not_open()
         d0, d1, _ = self._detail()
-        return read_next_error(rc, self.path, d0, d1)
+        return read_next_error(rc, self.path, d0, d1, self.header.fileVersion if self.header else 4)
 
     def FileInfo(self):  # noqa: N802
         fi = L.FileInfo()
@@ -184,9 +193,12 @@ class MMapReader(_Reader):
         d0, d1, _ = self._detail()
         if rc == L.RIO_EOF:
             return EOF  # mmap_reader.go:153-155: bare io.EOF
-        if rc == L.RIO_ERR_INVALID_OFFSET:
-            return wrap(f"ReadNextAt failed reading at offset {offset} in mmap reader for '{self.path}'",
-                        GoError(f"mmap: invalid ReadAt offset {offset}"))
+        v = self.header.fileVersion if self.header else 4
+        if rc == L.RIO_ERR_INVALID_OFFSET:  # v1 / v2: mmap_reader.go:211,256; v3 / v4: :157,312
+            return wrap(f"{'ReadNextAt ' if v >= 3 else ''}failed reading at offset {offset} in mmap reader for "
+                        f"'{self.path}'", GoError(f"mmap: invalid ReadAt offset {offset}"))
+        if rc == L.RIO_EOF_HEADER and v == 1:  # readNextAtV1: the 20-byte ReadAt ran short (:209-212)
+            return wrap(f"failed reading at offset {offset} in mmap reader for '{self.path}'", EOF)
         if rc == L.RIO_EOF_PAYLOAD:
             return wrap(f"failed reading record at offset {offset} in mmap reader for '{self.path}'", EOF)
         if rc in (L.RIO_ERR_DECOMPRESS, L.RIO_EOF_CODEC):  # mmap_reader.go:189-191

@@ -39,6 +39,7 @@ extern "C" {
 #define RIO_VERSION4 4u
 #define RIO_MAGIC 0x130691u /* MagicNumberSeparatorLong, uvarint bytes 91 8d 4c */
 #define RIO_FILE_HEADER_BYTES 8u
+#define RIO_RECORD_HEADER_V1_BYTES 20u /* RecordHeaderSizeBytesV1V2: LE u32 magic, LE u64 u, LE u64 c */
 #define RIO_RECORD_HEADER_V3_MAX 31u /* RecordHeaderV3MaxSizeBytes */
 #define RIO_RECORD_HEADER_V4_MAX 36u /* RecordHeaderV4MaxSizeBytes */
 #define RIO_COMP_NONE 0u
@@ -77,8 +78,8 @@ typedef enum rio_status {
     RIO_ERR_COMPRESSION_TYPE = 12,/* "unknown compression type [N]" */
     RIO_ERR_SHORT_FILE_HEADER = 13,/* fewer than 8 bytes in the file */
     RIO_ERR_INVALID_OFFSET = 14,  /* "mmap: invalid ReadAt offset N" (offset > size) */
-    RIO_ERR_UNSUPPORTED = 15,     /* valid file the GPU path does not decode (v1/v2):      
-                                     the adapter keeps the reference reader for it */
+    RIO_ERR_UNSUPPORTED = 15,     /* a request the GPU path does not serve (SeekNext on v1 files
+                                     mmap_reader.go:62-64; see DESIGN.md §8 for the rest) */
     RIO_ERR_CAPACITY = 16,        /* caller-provided output arrays too small */
     RIO_ERR_ARG = 17,             /* bad argument */
     RIO_ERR_HIP = 18,             /* HIP runtime failure */
@@ -234,7 +235,7 @@ int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_
  * of every value on the device (the two calls above), D2H of what the iterator needs. The handle owns
  * host copies; pointers from rio_sst_entry stay valid until rio_sst_free.
  * Returns RIO_ERR_UNSUPPORTED (no handle, `info` filled) when either file is one the device path hands
- * back (recordio v1/v2): the adapter keeps the reference reader. Otherwise the
+ * back (none of recordio v1..v4 is; the code stays for the adapter's contract). Otherwise the
  * handle is returned and `info` says which of the reference's load errors applies: index/data status
  * outside the EOF family (reading error), first_bad_proto (proto.Unmarshal error, slice_key_index.go:
  * 107-110), first_unplaced (not the writer's layout: keep the reference reader), first_bad_crc
@@ -292,8 +293,9 @@ int rio_encode_file(rio_ctx* ctx, const uint8_t* records, const uint64_t* rec_of
  * probe hit io.EOF; later lookups on the same Go object then see that entry: see DESIGN.md §8).
  *   status  RIO_OK (no error; `found` tells Get / Contains), else findAt's error: SeekNext's
  *           non-EOF error (e.g. RIO_ERR_UNEXPECTED_EOF) or RIO_ERR_PROTO. RIO_ERR_UNSUPPORTED for a
- *           v1/v2 index, and from rio_device_index_search for a compressed one (keep the reference
- *           index); the rio_index handle answers compressed indexes from their decoded view.
+ *           v1 index (SeekNext's "unsupported on files with version lower than v2", mmap_reader.go:62-64),
+ *           and from rio_device_index_search for a compressed one (keep the reference index); the
+ *           rio_index handle answers compressed indexes from their decoded view.
  *   offset  binarySearch's offset (IteratorStartingAt starts there; size when an io.EOF probe ended it)
  *   value_offset / checksum  IndexVal when found. */
 typedef struct rio_index_hit {

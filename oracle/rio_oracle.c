@@ -710,7 +710,8 @@ void orc_file_result_free(orc_file_result* res) {
 }
 
 /* ---------------------------------------------------------------------------------------- */
-/* MMapReader.ReadNextAt (mmap_reader.go:130-203 v4; readNextAtV3 :298-356)                  */
+/* MMapReader.ReadNextAt (mmap_reader.go:130-203 v4; readNextAtV3 :298-356; V2 :242-296;      */
+/* V1 :205-240)                                                                              */
 /* ---------------------------------------------------------------------------------------- */
 int orc_read_next_at(const uint8_t* f, uint64_t len, uint64_t offset, uint8_t** out,
                      uint64_t* out_len, int* is_nil, uint64_t* detail0, uint64_t* detail1) {
@@ -722,16 +723,22 @@ int orc_read_next_at(const uint8_t* f, uint64_t len, uint64_t offset, uint8_t** 
     *detail0 = *detail1 = 0;
     int e = orc_file_header(f, len, &ver, &comp, &det);
     if (e) return e;
-    if (ver < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
     /* x/exp/mmap ReadAt: off > len => "mmap: invalid ReadAt offset"; 0 bytes => bare io.EOF */
     if (offset > len) return RIO_ERR_INVALID_OFFSET;
+    /* V1: a 20-byte ReadAt; short of it (0 bytes included) the error wraps io.EOF (:209-212) */
+    if (ver == RIO_VERSION1 && len - offset < 20) return RIO_EOF_HEADER;
     uint64_t wmax = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : RIO_RECORD_HEADER_V3_MAX;
     uint64_t w = len - offset < wmax ? len - offset : wmax;
     if (w == 0) return RIO_EOF;
     brd r = {f + offset, w, 0, ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : UINT64_MAX};
     hdr_t h;
     memset(&h, 0, sizeof h);
-    e = ver == RIO_VERSION4 ? read_header_v4(&r, &h) : read_header_v3(&r, &h);
+    switch (ver) {
+    case RIO_VERSION1: e = read_header_v1(f + offset, len - offset, &h); break;
+    case RIO_VERSION2: e = read_header_v2(&r, &h); break;
+    case RIO_VERSION3: e = read_header_v3(&r, &h); break;
+    default: e = read_header_v4(&r, &h); break;
+    }
     if (e == RIO_EOF) e = RIO_EOF_HEADER; /* wrapped: "failed reading record header at offset" */
     if (e == RIO_ERR_HEADER_CRC) { *detail0 = h.exp_crc; *detail1 = h.act_crc; }
     if (e) return e;
@@ -762,7 +769,6 @@ int orc_seek_next(const uint8_t* f, uint64_t len, uint64_t offset, uint64_t seek
     int e = orc_file_header(f, len, &ver, &comp, &det);
     if (e) return e;
     if (ver < RIO_VERSION2) return RIO_ERR_UNSUPPORTED; /* :62-64 */
-    if (ver < RIO_VERSION3) return RIO_ERR_UNSUPPORTED;
     if (seek_len == 0) seek_len = 4096;
     uint64_t next = offset;
     for (;;) {

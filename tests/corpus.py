@@ -46,6 +46,25 @@ def header_v3(u, c, nil=False, magic=b"\x91\x8d\x4c"):
     return magic + bytes([1 if nil else 0]) + uvarint(u) + uvarint(c)
 
 
+def header_v2(u, c):
+    """readRecordHeaderV2 (common_reader.go:61-81): magic, u, c varints; no nil byte, no CRC."""
+    return b"\x91\x8d\x4c" + uvarint(u) + uvarint(c)
+
+
+def header_v1(u, c, magic=0x130691):
+    """readRecordHeaderV1 (common_reader.go:46-59): LE u32 magic, LE u64 u, LE u64 c."""
+    return struct.pack("<IQQ", magic, u, c)
+
+
+def header_for(version, u, c, nil=False):
+    if version == 4:
+        return header_v4(u, c, nil=nil)
+    if version == 3:
+        return header_v3(u, c, nil=nil)
+    assert not nil, "v1 / v2 records have no nil flag"
+    return header_v2(u, c) if version == 2 else header_v1(u, c)
+
+
 def file_header(version=4, comp=0):
     return struct.pack("<II", version, comp)
 
@@ -69,6 +88,30 @@ def v3_file(records, comp=0):
             out += header_v3(len(r), len(pay)) + pay
         else:
             out += header_v3(len(r), 0) + bytes(r)
+    return bytes(out)
+
+
+def snappy_encode(r: bytes) -> bytes:
+    from recordio import _lib as L
+    import ctypes
+
+    cap = int(L.lib().rio_snappy_max_encoded_len(len(r)))
+    buf = ctypes.create_string_buffer(cap + 1)
+    n = L.lib().rio_snappy_encode(buf, cap, ctypes.c_char_p(bytes(r) or b"\0"), len(r))
+    return buf.raw[:n]
+
+
+def legacy_file(records, comp=0, version=2):
+    """v1 / v2 image as the old writers laid it out (uncompressed: c = 0, the fixtures' headers;
+    snappy: c = the payload length). Nil records (v3+ only) are written as empty ones."""
+    out = bytearray(file_header(version, comp))
+    for r in records:
+        r = b"" if r is None else bytes(r)
+        if comp == 2:
+            pay = snappy_encode(r)
+            out += header_for(version, len(r), len(pay)) + pay
+        else:
+            out += header_for(version, len(r), 0) + r
     return bytes(out)
 
 
@@ -185,6 +228,28 @@ def cases():
     v3 = v3_file(mixed_records(800, 9), 0)
     out.append(("v3_zero_tail", v3 + bytes(9000)))
     out.append(("v3_trunc", v3[: len(v3) - 7]))
+    # v2 / v1 files (file_reader.go:282-388: no nil byte / no CRC; v1 fixed 20-byte headers and
+    # no zero-tail rule: DirectIO padding after a v1 file is a magic mismatch)
+    for ver in (2, 1):
+        for comp in (0, 2):
+            lg = legacy_file(mixed_records(1500, 20 + ver + comp), comp, ver)
+            out.append((f"v{ver}_mixed_c{comp}", lg))
+            rng = random.Random(40 + ver + comp)
+            for k in range(3):
+                out.append((f"v{ver}_mixed_c{comp}_trunc{k}", lg[:rng.randint(9, len(lg) - 1)]))
+            out.append((f"v{ver}_mixed_c{comp}_zero_tail", lg + bytes(5000)))
+            out.append((f"v{ver}_mixed_c{comp}_garbage_tail", lg + bytes(300) + b"\x01" + bytes(7)))
+        out.append((f"v{ver}_embedded", legacy_file(embedded_file_records(40, 9), 0, ver)))
+        out.append((f"v{ver}_text_snappy_1k", legacy_file(
+            [bytes(r) for r in text_records(3000, 30 + ver, 900, 1100)], 2, ver)))
+    # v1 record headers cut at every length, and a wrong magic in the middle
+    v1 = legacy_file([b"abc" * k for k in range(40)], 0, 1)
+    for cut in (1, 4, 12, 19, 20):
+        out.append((f"v1_torn_header_{cut}", v1 + header_v1(50, 0)[:cut]))
+    b1 = bytearray(v1)
+    b1[8 + 20 * 10 + 3 * sum(range(10)) + 1] ^= 0x40
+    out.append(("v1_bad_magic_mid", bytes(b1)))
+    out.append(("v1_huge_u", v1 + header_v1(1 << 40, 0) + b"abc"))
     # small files damaged in several places (every failure class of ReadNextAt / SeekNext within a
     # few KiB): a flipped CRC byte, an overflowing size varint, a header longer than 36 bytes, a
     # truncated header at the end; snappy variant with a corrupt element stream in the middle
@@ -256,10 +321,10 @@ def gz_file(payloads, version=4):
     out = bytearray(file_header(version, 1))
     for p in payloads:
         if p is None:
-            out += header_v4(0, 0, nil=True) if version == 4 else header_v3(0, 0, nil=True)
+            out += header_for(version, 0, 0, nil=True)
             continue
         u, pay = p
-        out += (header_v4(u, len(pay)) if version == 4 else header_v3(u, len(pay))) + pay
+        out += header_for(version, u, len(pay)) + pay
     return bytes(out)
 
 
@@ -357,6 +422,8 @@ def gzip_cases():
     cases.append(("gz_multi_stored", gz_file([(len(r), gzip_members(r, [len(r) // 2], level=0)) for r in large[:3]]),
                   False))
     cases.append(("gz_v3", gz_file([(len(r), gzip_member(r)) for r in text[:30]], version=3), False))
+    cases.append(("gz_v2", gz_file([(len(r), gzip_member(r)) for r in text[:30]], version=2), False))
+    cases.append(("gz_v1", gz_file([(len(r), gzip_member(r)) for r in text[:30]], version=1), False))
     return cases
 
 
@@ -390,10 +457,10 @@ def lzw_file(payloads, version=4):
     out = bytearray(file_header(version, 3))
     for p in payloads:
         if p is None:
-            out += header_v4(0, 0, nil=True) if version == 4 else header_v3(0, 0, nil=True)
+            out += header_for(version, 0, 0, nil=True)
             continue
         u, pay = p
-        out += (header_v4(u, len(pay)) if version == 4 else header_v3(u, len(pay))) + pay
+        out += header_for(version, u, len(pay)) + pay
     return bytes(out)
 
 
@@ -422,6 +489,8 @@ def lzw_cases():
     text = text_records(80, 13, 1, 1500)
     cases = [("lzw_text_small", lzw_file([(len(r), enc(r)) for r in text]))]
     cases.append(("lzw_text_v3", lzw_file([(len(r), enc(r)) for r in text[:40]], version=3)))
+    cases.append(("lzw_text_v2", lzw_file([(len(r), enc(r)) for r in text[:40]], version=2)))
+    cases.append(("lzw_text_v1", lzw_file([(len(r), enc(r)) for r in text[:40]], version=1)))
     # random bytes: about one code per byte, so these lengths sit on the width steps (255 / 767 /
     # 1791 codes) and the writer's clear at 3838 codes
     rand = [bytes(rnd.randrange(256) for _ in range(n)) for n in

@@ -23,7 +23,7 @@ def _fixture_images():
     from conftest import GOLDEN
 
     out = []
-    for vd in ("v4_compat", "v3_compat"):
+    for vd in ("v4_compat", "v3_compat", "v2_compat", "v1_compat"):
         for name in sorted(os.listdir(os.path.join(GOLDEN, vd))):
             out.append((f"{vd}/{name}", read_fixture(vd, name)))
     return out

@@ -286,3 +286,122 @@ def test_end_to_end_berlin52(tmp_path, comp):
     assert err is None and b is None
     _, err = r.ReadNext()
     assert errors_is(err, EOF)
+
+
+# ---- recordio v1 / v2 files (file_reader_v{1,2}compat_test.go, mmap_reader_v{1,2}compat_test.go) ----
+LEGACY = ["v2_compat", "v1_compat"]
+
+
+@pytest.mark.parametrize("vd", LEGACY)
+def test_legacy_reader_happy_paths(vd):  # file_reader_v2compat_test.go:13-103 / v1compat :12-102
+    r = opened(vd, "recordio_UncompressedSingleRecord")
+    buf, err = r.ReadNext()
+    assert err is None and buf == asc(13)
+    expect_eof(r)
+    for name in ("recordio_UncompressedWriterMultiRecord_asc", "recordio_SnappyWriterMultiRecord_asc"):
+        r = opened(vd, name)
+        for n in range(255):
+            buf, err = r.ReadNext()
+            assert err is None and buf == asc(n), (name, n)
+        expect_eof(r)
+        r = opened(vd, name)
+        for n in range(255):
+            if n % 2 == 0:
+                buf, err = r.ReadNext()
+                assert err is None and buf == asc(n)
+            else:
+                assert r.SkipNext() is None
+        expect_eof(r)
+    r = opened(vd, "recordio_UncompressedWriterMultiRecord_asc")
+    for _ in range(255):
+        assert r.SkipNext() is None
+    expect_eof(r)
+
+
+@pytest.mark.parametrize("vd", LEGACY)
+def test_legacy_reader_headers_and_mismatch(vd):  # v2compat :105-139 / v1compat :104-138
+    for name, msg in [("recordio_UncompressedSingleRecord_v0", "version mismatch, expected a value from 1 to 4 but was 0"),
+                      ("recordio_UncompressedSingleRecord_v256", "version mismatch, expected a value from 1 to 4 but was 256")]:
+        r, _ = NewFileReaderWithPath(fixture_path(vd, name))
+        assert msg in str(r.Open())
+    for name, comp in [("recordio_UncompressedSingleRecord_comp1", 1), ("recordio_UncompressedSingleRecord_comp2", 2)]:
+        r = opened(vd, name)
+        assert r.header.compressionType == comp and r.header.fileVersion == int(vd[1])
+    r = opened(vd, "recordio_UncompressedSingleRecord_mnm")
+    _, err = r.ReadNext()
+    assert str(errors_unwrap(err)) == "magic number mismatch"
+
+
+def test_v2_reader_direct_io():  # file_reader_v2compat_test.go:141-167
+    r = opened("v2_compat", "recordio_UncompressedSingleRecord_directio")
+    rec, err = r.ReadNext()
+    assert err is None and rec == bytes([13, 6, 29, 7])
+    _, err = r.ReadNext()
+    assert errors_is(err, EOF)
+    r = opened("v2_compat", "recordio_UncompressedSingleRecord_directio_trailer")
+    rec, err = r.ReadNext()
+    assert err is None and rec == bytes([13, 6, 29, 7])
+    _, err = r.ReadNext()
+    assert errors_is(err, MagicNumberMismatchErr)
+
+
+@pytest.mark.parametrize("vd", LEGACY)
+def test_legacy_reader_forbids_closed_and_double_open(vd):  # v2compat :169-188 / v1compat :140-159
+    r, _ = NewFileReaderWithPath(fixture_path(vd, "recordio_UncompressedSingleRecord"))
+    assert r.Close() is None
+    _, err = r.ReadNext()
+    assert "was either not opened yet or is closed already" in str(err)
+    assert "already closed" in str(r.Open())
+    r, _ = NewFileReaderWithPath(fixture_path(vd, "recordio_UncompressedSingleRecord"))
+    assert r.Open() is None
+    assert "already opened" in str(r.Open())
+
+
+@pytest.mark.parametrize("vd", LEGACY)
+def test_legacy_mmap_single_record_and_offsets(vd):  # mmap_reader_v2compat_test.go:11-35 / v1compat :12-36
+    r = mm(vd, "recordio_UncompressedSingleRecord")
+    buf, err = r.ReadNextAt(FileHeaderSizeBytes)
+    assert err is None and buf == asc(13)
+    _, err = r.ReadNextAt(FileHeaderSizeBytes + 1)
+    assert str(errors_unwrap(err)) == "magic number mismatch"
+    _, err = r.ReadNextAt(42000)
+    assert str(errors_unwrap(err)) == "mmap: invalid ReadAt offset 42000"
+    assert str(err).startswith("failed reading at offset 42000 in mmap reader")  # mmap_reader.go:211 / :256
+    for name, msg in [("recordio_UncompressedSingleRecord_v0", "but was 0"),
+                      ("recordio_UncompressedSingleRecord_v256", "but was 256")]:
+        r2, _ = NewMemoryMappedReaderWithPath(fixture_path(vd, name))
+        assert msg in str(r2.Open())
+    if vd == "v2_compat":
+        r2, _ = NewMemoryMappedReaderWithPath(fixture_path(vd, "recordio_UncompressedSingleRecord_comp300"))
+        assert "unknown compression type [300]" in str(r2.Open())
+
+
+def test_v2_mmap_small_varint_header_eof():  # mmap_reader_v2compat_test.go:91-104
+    r = mm("v2_compat", "recordio_UncompressedSingleRecord")
+    b, err = r.ReadNextAt(FileHeaderSizeBytes)
+    assert err is None and len(b) == 13
+    b2, err = r.ReadNextAt(FileHeaderSizeBytes + 5 + len(b))
+    assert b2 is None and err is EOF
+    b2, err = r.ReadNextAt(FileHeaderSizeBytes + 4 + len(b))
+    assert b2 is None and str(errors_unwrap(err)) == "magic number mismatch"
+
+
+def test_v1_mmap_short_header_and_seek():
+    # readNextAtV1 (mmap_reader.go:205-221): a 20-byte ReadAt past the last record fails wrapping
+    # io.EOF; SeekNext on v1: "unsupported on files with version lower than v2" (:62-64)
+    r = mm("v1_compat", "recordio_UncompressedSingleRecord")
+    b, err = r.ReadNextAt(41)
+    assert b is None and errors_is(err, EOF) and str(err).startswith("failed reading at offset 41 in mmap reader")
+    b, err = r.ReadNextAt(30)
+    assert b is None and errors_is(err, EOF)
+    _, _, err = r.SeekNext(0)
+    assert str(err) == "unsupported on files with version lower than v2"
+
+
+def test_v2_mmap_seek_next():
+    r = mm("v2_compat", "recordio_UncompressedWriterMultiRecord_asc")
+    nxt, rec, err = r.SeekNext(0)
+    assert err is None and nxt == FileHeaderSizeBytes and rec == b""
+    for n in range(1, 6):
+        nxt, rec, err = r.SeekNext(nxt + 1)
+        assert err is None and rec == asc(n)

@@ -3,8 +3,8 @@
 NewSSTableReader (sstables/sstable_reader.go:250-345: index via SliceKeyIndexLoader, validateDataFile
 unless SkipHashCheckOnLoad) and Scan (SSTableFullScanIterator, sstable_iterator.go:68-111) on tables
 the mirror's writer produced (v4 recordio, as sstable_writer.go writes them), compared with the
-oracle's restatement; the reference's fixture content (sstable_reader_test.go) is re-encoded as v4,
-its recordio v1/v2 originals must be handed back (UnsupportedError)."""
+oracle's restatement, and on the reference's own fixtures (recordio v2, sstable_reader_test.go's
+expectations); the v0-values fixture must be handed back (UnsupportedError)."""
 import os
 import random
 import struct
@@ -133,12 +133,72 @@ def test_zero_checksum_is_unchecked(tmp_path):
     assert o["first_bad"] is None and r is not None
 
 
-def test_reference_fixtures_are_handed_back():
-    # recordio v1/v2 data files (and v0 protobuf values): the reference reader keeps them
-    for name in ("SimpleWriteHappyPathSSTable", "SimpleWriteHappyPathSSTableRecordIOV2",
-                 "SimpleWriteHappyPathSSTableWithCRCHashesMismatch"):
-        r, err = S.NewSSTableReader(S.ReadBasePath(os.path.join(GOLDEN, "sstables", name)))
-        assert r is None and isinstance(err, S.UnsupportedError), (name, err)
+def _fixture(name):
+    return os.path.join(GOLDEN, "sstables", name)
+
+
+SEVEN = [(be(i), be(i + 1)) for i in range(1, 8)]  # TEST_ONLY_NewSkipListMapWithElements (sstable_test.go:245-258)
+
+
+@pytest.mark.parametrize("name", ["SimpleWriteHappyPathSSTableRecordIOV2", "SimpleWriteHappyPathSSTableWithMetaData",
+                                  "SimpleWriteHappyPathSSTableWithCRCHashes"])
+def test_reference_fixtures_on_device(name):
+    """sstable_reader_test.go:28-87: recordio v2 tables with metadata version 1 load on the device, with
+    the tests' metadata, content (assertContentMatchesSkipList), full scan and negative lookups."""
+    r, err = S.NewSSTableReader(S.ReadBasePath(_fixture(name)))
+    assert err is None, err
+    m = r.MetaData()
+    assert (m.NumRecords, m.NullValues, m.MinKey, m.MaxKey) == (7, 0, be(1), be(7))
+    for k, v in SEVEN:
+        assert r.Contains(k) == (True, None)
+        assert r.Get(k) == (v, None)
+    assert scan_all(r) == (SEVEN, None)
+    for k in (b"", b"\x01", b"\x01\x02\x03"):  # assertNegativeContains (:305-324)
+        assert r.Contains(k) == (False, None)
+        assert r.Get(k)[1] is S.NotFound
+    assert r.t.index_info["version"] == 2 and r.t.data_info["version"] == 2
+    o, _ = check_against_oracle(_fixture(name))
+    assert o["first_bad"] is None
+
+
+def test_reference_fixture_empty_values():
+    # sstable_reader_test.go:164-183
+    r, err = S.NewSSTableReader(S.ReadBasePath(_fixture("SimpleWriteHappyPathSSTableWithCRCHashesEmptyValues")))
+    assert err is None, err
+    m = r.MetaData()
+    assert (m.NumRecords, m.NullValues, m.MinKey, m.MaxKey) == (2, 0, be(0x2A), be(0x2D))
+    assert r.Get(be(45)) == (b"", None)
+    assert r.Get(be(42)) == (be(0), None)
+
+
+def test_reference_fixture_checksum_mismatch():
+    # sstable_reader_test.go:89-162
+    base = _fixture("SimpleWriteHappyPathSSTableWithCRCHashesMismatch")
+    r, err = S.NewSSTableReader(S.ReadBasePath(base))
+    assert r is None
+    assert "offset [41]: Checksum mismatch: expected 688fffff90000000, got 738fffff90000000" in str(err)
+    assert "at key [[0 0 0 4]]" in str(err)
+    r, err = S.NewSSTableReader(S.ReadBasePath(base), S.SkipHashCheckOnLoad(), S.EnableHashCheckOnReads())
+    assert err is None
+    m = r.MetaData()
+    assert (m.NumRecords, m.NullValues, m.MinKey, m.MaxKey) == (7, 0, be(1), be(7))
+    for i in range(1, 8):
+        v, gerr = r.Get(be(i))
+        if i == 4:
+            assert v == be(0x15)
+            assert "offset [41]: Checksum mismatch: expected 688fffff90000000, got 738fffff90000000" in str(gerr)
+        else:
+            assert (v, gerr) == (be(i + 1), None)
+    got, serr = scan_all(r)
+    assert got == SEVEN[:3]
+    assert serr == S.ChecksumError(0x738FFFFF90000000, 0x688FFFFF90000000)
+
+
+def test_v0_values_table_is_handed_back():
+    # SimpleWriteHappyPathSSTable: recordio v1 files and no meta.pb.bin, i.e. metadata version 0 with
+    # protobuf DataEntry values (sstable_reader.go:303-314): the reference reader keeps it
+    r, err = S.NewSSTableReader(S.ReadBasePath(_fixture("SimpleWriteHappyPathSSTable")))
+    assert r is None and isinstance(err, S.UnsupportedError), err
 
 
 def test_index_out_of_layout_is_handed_back(tmp_path):
@@ -240,9 +300,10 @@ def test_host_handle_mismatch_and_handback(tmp_path):
     assert rc == 0 and info.first_bad_crc == 3 and ents[3][5] == crc64_iso(be(0x15))
     from recordio import _lib as L
 
-    for name in ("SimpleWriteHappyPathSSTable", "SimpleWriteHappyPathSSTableRecordIOV2"):
-        rc, info, _ = sst_open_host(os.path.join(GOLDEN, "sstables", name))
-        assert rc == L.RIO_ERR_UNSUPPORTED, (name, rc)
+    # the reference's v2 fixture through the host handle: the seven entries, their CRCs match
+    rc, info, ents = sst_open_host(_fixture("SimpleWriteHappyPathSSTableRecordIOV2"))
+    assert rc == 0 and info.n_entries == 7 and info.first_bad_crc == (1 << 64) - 1
+    assert [(e[1], e[2]) for e in ents] == SEVEN and all(e[5] == e[4] for e in ents)
     base2 = str(tmp_path / "m")
     write_triples(base2, triples_for([(be(i), be(i)) for i in range(20)]),
                   tamper=lambda i, e, off: b"\x0a\x7fab" if i == 6 else e)

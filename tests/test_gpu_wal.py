@@ -12,7 +12,7 @@ import oracle_py as orc
 from corpus import header_v4, mixed_records
 import wal as W
 from recordio import NewFileReaderWithPath, encode_file
-from recordio.errors import EOF, ErrUnsupported, GoError, errors_is
+from recordio.errors import EOF, GoError, errors_is
 
 pytestmark = pytest.mark.gpu
 TestMaxWalFileSize = 8 * 1024
@@ -205,14 +205,14 @@ def test_header_errors(tmp_path):
     assert got == [] and "version mismatch, expected a value from 1 to 4 but was 9" in str(err)
 
 
-def test_unsupported_file_is_handed_back(tmp_path):
-    # a recordio v2 file (written by older versions of the library): the Go adapter re-reads it with
-    # the reference reader; the mirror reports ErrUnsupported before delivering any of its records
-    v2 = struct.pack("<II", 2, 0) + b"\x91\x8d\x4c\x01\x01z"
-    base = write_wal_dir(tmp_path, [encode_file([b"a"], 0), v2])
-    opts, _ = W.NewWriteAheadLogOptions(W.BasePath(base))
-    got, err = replay(opts)
-    assert got == [b"a"] and errors_is(err, ErrUnsupported)
+def test_legacy_recordio_files_replay(tmp_path):
+    # WAL files written by older versions of the library (recordio v2 and v1 headers) replay on the
+    # device like v4 ones: readNextV2 / readNextV1 (file_reader.go:282-388)
+    v2 = struct.pack("<II", 2, 0) + b"\x91\x8d\x4c\x01\x00z"
+    v1 = struct.pack("<II", 1, 0) + struct.pack("<IQQ", 0x130691, 2, 0) + b"yy"
+    base = write_wal_dir(tmp_path, [encode_file([b"a"], 0), v2, v1])
+    got, err = both_paths_agree(base)
+    assert got == [b"a", b"z", b"yy"] and err is None
 
 
 def test_empty_directory(tmp_path):

@@ -1,7 +1,7 @@
 """Pins the oracle (oracle/rio_oracle.c) to the reference's fixtures and test assertions (CPU).
 
-Mirrors recordio/file_reader_test.go, file_reader_v3compat_test.go, mmap_reader_test.go,
-mmap_reader_v3compat_test.go and checksum_byte_reader_test.go on the copied fixture files.
+Mirrors recordio/file_reader_test.go, file_reader_v{1,2,3}compat_test.go, mmap_reader_test.go,
+mmap_reader_v{1,2,3}compat_test.go and checksum_byte_reader_test.go on the copied fixture files.
 """
 import ctypes
 import zlib
@@ -11,7 +11,7 @@ import pytest
 import oracle_py as orc
 from conftest import STATUS, read_fixture, spec_bytes
 
-VERSIONS = ["v4_compat", "v3_compat"]
+VERSIONS = ["v4_compat", "v3_compat", "v2_compat", "v1_compat"]
 
 
 def _cases(expectations, key):
@@ -41,6 +41,9 @@ def test_file_reader_fixtures(vd, expectations):
             assert res["detail0"] == val, name
             continue
         assert res["compression"] == exp.get("compression", 0), name
+        assert res["version"] == int(vd[1]), name
+        if exp.get("header_only"):  # the reference checks only the header's compression type
+            continue
         want = [spec_bytes(s) for s in exp["records"]]
         assert res["records"] == want, name
         assert res["status"] == STATUS[exp["end"]], (name, res["status"])
@@ -72,7 +75,32 @@ def test_read_at_every_record_start_equals_sequential(vd, expectations):
             assert st == 0 and r2 == rec, (name, off)
 
 
-@pytest.mark.parametrize("vd", VERSIONS)
+def test_seek_next_legacy_versions():
+    # mmap_reader.go:62-64: SeekNext on v1 is "unsupported on files with version lower than v2";
+    # v2 has the same marker bytes and scan as v3 / v4
+    v1 = read_fixture("v1_compat", "recordio_UncompressedWriterMultiRecord_asc")
+    assert orc.seek_next(v1, 0)[0] == STATUS["UNSUPPORTED"]
+    v2 = read_fixture("v2_compat", "recordio_UncompressedWriterMultiRecord_asc")
+    res = orc.file_reader_decode(v2)
+    nxt, got = 0, []
+    for i in range(5):
+        st, ro, rec = orc.seek_next(v2, 0 if i == 0 else nxt + 1)
+        assert st == 0
+        nxt = ro
+        got.append((ro, rec))
+    assert got == list(zip(res["rec_off"][:5], res["records"][:5]))
+
+
+def test_v2_comp1_gzip_content():
+    # the v2 _comp1 fixture's record is a gzip member of ascending(1337), checked with zlib
+    data = read_fixture("v2_compat", "recordio_UncompressedSingleRecord_comp1")
+    res = orc.file_reader_decode(data)
+    asc = bytes(i & 0xFF for i in range(1337))
+    gz = data.index(b"\x1f\x8b", 8)
+    assert zlib.decompress(data[gz:], 16 + 15) == asc and res["records"] == [asc]
+
+
+@pytest.mark.parametrize("vd", VERSIONS[:2])
 def test_seek_next_magic_number_content(vd):
     # mmap_reader_test.go:244-260 / v3compat: SeekNext(0) -> rec1, SeekNext(next+1) -> ... -> EOF
     data = read_fixture(vd, "recordio_UncompressedMagicNumberContent")
