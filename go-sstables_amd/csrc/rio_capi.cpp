@@ -40,7 +40,10 @@ hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t 
                             hipStream_t s);
 hipError_t launch_sst_validate(const uint8_t* data, const uint64_t* data_off, const uint64_t* data_rec_off,
                                uint64_t n_data, const uint64_t* value_off, const uint64_t* checksum,
-                               uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s);
+                               uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s,
+                               const uint64_t* view = nullptr);
+hipError_t launch_sst_data_entry(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* view,
+                                 uint64_t* result, hipStream_t s);
 hipError_t launch_index_search(const uint8_t* f, uint64_t len, uint64_t seek_len, const uint8_t* keys,
                                const uint64_t* key_off, uint64_t nq, const uint32_t* perm, rio_index_hit* hits,
                                hipStream_t s);
@@ -199,7 +202,7 @@ struct rio_ctx {
     // reader handles sharing this ctx take this around every device use (rio_reader_*)
     std::mutex mu;
     // rio_sst_open: parsed index fields (4 x n), per-entry CRC-64, kernel results
-    DevBuf sst_fields, sst_crc, sst_res;
+    DevBuf sst_fields, sst_crc, sst_res, sst_view;
     // rio_device_encode: compressed payloads, their offsets and lengths, hash tables, headers,
     // record sizes, scan temp; rio_encode_file: records, offsets, flags, file image, record offsets
     DevBuf enc_scr, enc_scr_off, enc_clen, enc_tab, enc_hdr, enc_size, enc_tmp, enc_cub;
@@ -325,7 +328,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
     c->fa.release();
     for (auto& a : c->batch) a->release();
     for (DevBuf* b : {&c->sink, &c->file, &c->out, &c->out_off, &c->rec_off, &c->flags,
-                      &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res, &c->enc_scr, &c->enc_scr_off, &c->enc_clen, &c->enc_tab,
+                      &c->readat_out, &c->readat_res, &c->seek_off, &c->sst_fields, &c->sst_crc, &c->sst_res, &c->sst_view, &c->enc_scr, &c->enc_scr_off, &c->enc_clen, &c->enc_tab,
                       &c->enc_hdr, &c->enc_size, &c->enc_tmp, &c->enc_cub, &c->enc_rec, &c->enc_rec_off, &c->enc_flags, &c->enc_out,
                       &c->enc_out_off, &c->enc_len, &c->q_pfx, &c->q_pfx_out, &c->q_idx, &c->q_perm, &c->q_tmp})
         b->release();
@@ -1344,6 +1347,29 @@ extern "C" int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const u
     return RIO_OK;
 }
 
+extern "C" int rio_sst_data_entries(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_data_off, uint64_t n_data,
+                                    uint64_t* d_view, uint64_t* d_result, void* stream) {
+    if (!ctx || !d_data_off || !d_result || (n_data && (!d_data_out || !d_view))) return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(launch_sst_data_entry(d_data_out, d_data_off, n_data, d_view, d_result, s));
+    return RIO_OK;
+}
+
+extern "C" int rio_sst_validate_view(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_data_off,
+                                     const uint64_t* d_data_rec_off, uint64_t n_data, const uint64_t* d_view,
+                                     const uint64_t* d_value_off, const uint64_t* d_checksum, uint64_t n_index,
+                                     uint64_t* d_crc_out, uint64_t* d_result, void* stream) {
+    if (!ctx || !d_result ||
+        (n_index && (!d_value_off || !d_checksum || !d_crc_out || !d_data_off || !d_data_rec_off || !d_view)))
+        return RIO_ERR_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(launch_sst_validate(d_data_out, d_data_off, d_data_rec_off, n_data, d_value_off, d_checksum, n_index,
+                                d_crc_out, d_result, s, d_view));
+    return RIO_OK;
+}
+
 // ------------------------------------------------------------------------------------------
 // sstables: host-memory table handle (the cgo NewSSTableReader binding)
 // ------------------------------------------------------------------------------------------
@@ -1351,6 +1377,8 @@ struct rio_sst {
     std::vector<uint8_t> index, data, index_flags, data_flags;
     std::vector<uint64_t> index_off, index_rec_off, data_off, data_rec_off;
     std::vector<uint64_t> key_off, key_len, value_off, checksum, crc;
+    std::vector<uint64_t> view;  // v0 tables: DataEntry.value ranges per data record (rio_sst_data_entries)
+    bool v0 = false;
     rio_sst_info info{};
 };
 
@@ -1378,13 +1406,19 @@ static bool sst_header_level(int s) {
 
 extern "C" int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, const uint8_t* data_file,
                             uint64_t data_len, rio_sst** out, rio_sst_info* info) {
+    return rio_sst_open_ex(ctx, index_file, index_len, data_file, data_len, 0, out, info);
+}
+
+extern "C" int rio_sst_open_ex(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, const uint8_t* data_file,
+                               uint64_t data_len, uint32_t flags, rio_sst** out, rio_sst_info* info) {
     if (!ctx || !out || !info || (!index_file && index_len) || (!data_file && data_len)) return RIO_ERR_ARG;
     *out = nullptr;
     memset(info, 0, sizeof *info);
     HIP_TRY(hipSetDevice(ctx->device));
     auto* t = new rio_sst();
+    t->v0 = (flags & RIO_SST_V0_VALUES) != 0;
     rio_sst_info& I = t->info;
-    I.first_bad_proto = I.first_bad_crc = I.first_unplaced = I.index_bad = ~0ull;
+    I.first_bad_proto = I.first_bad_crc = I.first_unplaced = I.index_bad = I.first_bad_value = ~0ull;
     int rc = sst_decode_host(ctx, index_file, index_len, t->index, t->index_off, t->index_rec_off, t->index_flags, I.index);
     uint64_t n = 0;
     if (!rc && !sst_header_level(I.index.status) && I.index.status != RIO_ERR_UNSUPPORTED) {
@@ -1417,14 +1451,26 @@ extern "C" int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t in
             rc = sst_decode_host(ctx, data_file, data_len, t->data, t->data_off, t->data_rec_off, t->data_flags, I.data);
         }
         if (!rc && !sst_header_level(I.data.status) && I.data.status != RIO_ERR_UNSUPPORTED) {
-            if (launch_sst_validate(ctx->out.as<uint8_t>(), ctx->out_off.as<uint64_t>(), ctx->rec_off.as<uint64_t>(),
-                                    I.data.n_records, f + 2 * nn, f + 3 * nn, n, ctx->sst_crc.as<uint64_t>(), res + 1,
-                                    ctx->stream) != hipSuccess)
+            const uint64_t* view = nullptr;
+            if (t->v0) {  // DataEntry values: their ranges in the data arena, then hashed as such
+                const uint64_t nd = std::max<uint64_t>(I.data.n_records, 1);
+                if (ctx->sst_view.ensure(nd * 16)) rc = RIO_ERR_HIP;
+                if (!rc && launch_sst_data_entry(ctx->out.as<uint8_t>(), ctx->out_off.as<uint64_t>(), I.data.n_records,
+                                                 ctx->sst_view.as<uint64_t>(), res + 3, ctx->stream) != hipSuccess)
+                    rc = RIO_ERR_HIP;
+                t->view.assign(2 * nd, 0);
+                if (!rc) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(t->view.data()), ctx->sst_view.p, nd * 16);
+                if (!rc) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(&I.first_bad_value), res + 3, 8);
+                view = ctx->sst_view.as<uint64_t>();
+            }
+            if (!rc && launch_sst_validate(ctx->out.as<uint8_t>(), ctx->out_off.as<uint64_t>(), ctx->rec_off.as<uint64_t>(),
+                                           I.data.n_records, f + 2 * nn, f + 3 * nn, n, ctx->sst_crc.as<uint64_t>(),
+                                           res + 1, ctx->stream, view) != hipSuccess)
                 rc = RIO_ERR_HIP;
             if (!rc) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(t->crc.data()), ctx->sst_crc.p, nn * 8);
             uint64_t vr[2] = {~0ull, ~0ull};
             if (!rc) rc = d2h_staged(ctx, reinterpret_cast<uint8_t*>(vr), res + 1, 16);
-            I.first_bad_crc = vr[0];
+            I.first_bad_crc = t->v0 ? ~0ull : vr[0];  // validateDataFile returns at once for v0 (:205-209)
             I.first_unplaced = vr[1];
         }
     }
@@ -1462,6 +1508,14 @@ extern "C" int rio_sst_entry(const rio_sst* t, uint64_t i, const uint8_t** key, 
         if (value_len) *value_len = 0;
         if (is_nil) *is_nil = 0;
         return (t->data_flags[i] & RIO_FLAG_EOF) ? RIO_EOF_CODEC : RIO_ERR_DECOMPRESS;
+    }
+    if (t->v0) {  // DataEntry.value of data record i
+        const uint64_t b = t->view[2 * i], e = t->view[2 * i + 1];
+        const bool nil = b == RIO_VALUE_NIL || b == RIO_VALUE_BAD;
+        if (value) *value = nil ? nullptr : t->data.data() + b;
+        if (value_len) *value_len = nil ? 0 : e - b;
+        if (is_nil) *is_nil = b == RIO_VALUE_NIL ? 1 : 0;
+        return b == RIO_VALUE_BAD ? RIO_ERR_PROTO : RIO_OK;
     }
     const bool nil = (t->data_flags[i] & RIO_FLAG_NIL) != 0;
     if (value) *value = nil ? nullptr : t->data.data() + t->data_off[i];

@@ -128,6 +128,34 @@ __device__ __forceinline__ bool pb_index_entry_t(B& g, uint64_t base, uint64_t l
     return true;
 }
 
+// proto.Unmarshal into a reset DataEntry {value = 1} (sstables/proto/sstable.proto:12-14), the v0
+// tables' value records: present = field 1 seen as bytes (last occurrence wins; present with length 0
+// is Go's non-nil empty slice), [vo, vo + vl) relative to base. Returns false for malformed input.
+template <class B>
+__device__ __forceinline__ bool pb_data_entry_t(B& g, uint64_t base, uint64_t len, bool& present, uint64_t& vo,
+                                                uint64_t& vl) {
+    uint64_t pos = 0;
+    present = false;
+    vo = vl = 0;
+    while (pos < len) {
+        uint64_t tag, v;
+        if (!pb_varint_t(g, base, len, pos, tag)) return false;
+        const uint64_t fn = tag >> 3;
+        const uint32_t wt = (uint32_t)(tag & 7);
+        if (fn < 1 || fn > 0x1FFFFFFFull) return false;
+        if (fn == 1 && wt == 2) {
+            if (!pb_varint_t(g, base, len, pos, v) || v > len - pos) return false;
+            present = true;
+            vo = pos;
+            vl = v;
+            pos += v;
+        } else if (!pb_skip_t(g, base, len, pos, fn, wt)) {
+            return false;
+        }
+    }
+    return true;
+}
+
 // pointer forms (b[0, n))
 __device__ __forceinline__ bool pb_varint(const uint8_t* b, uint64_t n, uint64_t& pos, uint64_t& v) {
     RawBytes g{b};

@@ -21,6 +21,12 @@
 //                first entry not in the writer's layout (valueOffset is not data record i's offset:
 //                the scan's positional pairing and validation would diverge; the adapter keeps the
 //                reference reader).
+// k_sst_data_entry one lane per data record of a v0 table (metadata version 0, sstable_reader.go:
+//                303-314): proto.Unmarshal into a DataEntry {value = 1} (sstable.proto:12-14), as
+//                MMapProtoReader.ReadNextAt / ProtoReader.ReadNext do for every value
+//                (recordio/proto/mmap_proto_reader.go:12-24). Outputs the value's [begin, end) in the data
+//                arena (kValueNil both for an absent field: value nil), the first malformed record.
+//                k_sst_validate then hashes these ranges instead of the whole records.
 #include <hip/hip_runtime.h>
 
 #include "rio_device.h"
@@ -55,11 +61,28 @@ __device__ __forceinline__ uint64_t crc64_step8(const uint64_t (*tab)[256], uint
            tab[3][(c >> 32) & 0xFF] ^ tab[2][(c >> 40) & 0xFF] ^ tab[1][(c >> 48) & 0xFF] ^ tab[0][c >> 56];
 }
 
+__global__ void __launch_bounds__(256) k_sst_data_entry(const uint8_t* arena, const uint64_t* off, uint64_t n,
+                                                        uint64_t* view, unsigned long long* first_bad) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+        const uint64_t base = off[j], len = off[j + 1] - base;
+        RawBytes g{arena};
+        bool present;
+        uint64_t vo, vl;
+        const bool ok = pb_data_entry_t(g, base, len, present, vo, vl);
+        view[2 * j] = ok ? (present ? base + vo : RIO_VALUE_NIL) : RIO_VALUE_BAD;
+        view[2 * j + 1] = ok ? (present ? base + vo + vl : RIO_VALUE_NIL) : RIO_VALUE_BAD;
+        if (!ok) atomicMin(first_bad, (unsigned long long)j);
+    }
+}
+
+// view == nullptr: the value of data record j is the whole record; else [view[2j], view[2j+1]) (v0
+// DataEntry values; a nil or malformed one hashes as empty)
 __global__ void __launch_bounds__(256) k_sst_validate(const uint8_t* data, const uint64_t* data_off,
                                                       const uint64_t* data_rec_off, uint64_t n_data,
                                                       const uint64_t* value_off, const uint64_t* checksum,
                                                       uint64_t n_index, uint64_t* crc_out,
-                                                      unsigned long long* result) {
+                                                      unsigned long long* result, const uint64_t* view) {
     __shared__ uint64_t tab[8][256];  // 16 KiB
     for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) {
         uint64_t c = k;
@@ -93,8 +116,14 @@ __global__ void __launch_bounds__(256) k_sst_validate(const uint8_t* data, const
             j = lo;
             atomicMin(&result[1], (unsigned long long)i);
         }
-        const uint8_t* v = data + data_off[j];
-        const uint64_t len = data_off[j + 1] - data_off[j];
+        uint64_t vb = data_off[j], ve = data_off[j + 1];
+        if (view) {
+            vb = view[2 * j];
+            ve = view[2 * j + 1];
+            if (vb >= RIO_VALUE_BAD) vb = ve = 0;
+        }
+        const uint8_t* v = data + vb;
+        const uint64_t len = ve - vb;
         uint64_t c = ~0ull, k = 0;
         // 64 bytes per iteration: four unaligned 16-byte loads in flight before the CRC steps
         for (; k + 64 <= len; k += 64) {
@@ -134,15 +163,27 @@ hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t 
     return hipGetLastError();
 }
 
+hipError_t launch_sst_data_entry(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* view,
+                                 uint64_t* result, hipStream_t s) {
+    unsigned long long* r = reinterpret_cast<unsigned long long*>(result);
+    hipLaunchKernelGGL(k_sst_init, dim3(1), dim3(64), 0, s, r, 1);
+    const uint64_t blocks = (n + 255) / 256;
+    if (n)
+        hipLaunchKernelGGL(k_sst_data_entry, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, arena, off,
+                           n, view, r);
+    return hipGetLastError();
+}
+
 hipError_t launch_sst_validate(const uint8_t* data, const uint64_t* data_off, const uint64_t* data_rec_off,
                                uint64_t n_data, const uint64_t* value_off, const uint64_t* checksum,
-                               uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s) {
+                               uint64_t n_index, uint64_t* crc_out, uint64_t* result, hipStream_t s,
+                               const uint64_t* view) {
     unsigned long long* r = reinterpret_cast<unsigned long long*>(result);
     hipLaunchKernelGGL(k_sst_init, dim3(1), dim3(64), 0, s, r, 2);
     const uint64_t blocks = (n_index + 255) / 256;
     if (n_index)
         hipLaunchKernelGGL(k_sst_validate, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, data,
-                           data_off, data_rec_off, n_data, value_off, checksum, n_index, crc_out, r);
+                           data_off, data_rec_off, n_data, value_off, checksum, n_index, crc_out, r, view);
     return hipGetLastError();
 }
 

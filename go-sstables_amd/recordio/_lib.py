@@ -45,6 +45,9 @@ RIO_FLAG_NIL = 1
 RIO_FLAG_CORRUPT = 2
 RIO_FLAG_EOF = 4
 RIO_DEVICE_PAD = 64
+RIO_VALUE_NIL = 0xFFFFFFFFFFFFFFFF  # rio_sst_data_entries: DataEntry without a value field
+RIO_VALUE_BAD = 0xFFFFFFFFFFFFFFFE  # rio_sst_data_entries: not a valid DataEntry
+RIO_SST_V0_VALUES = 1
 RIO_COMP_UNKNOWN = 0xFFFFFFFF
 COMP_NONE, COMP_GZIP, COMP_SNAPPY, COMP_LZW = 0, 1, 2, 3
 
@@ -81,6 +84,7 @@ class SstInfo(ctypes.Structure):
         ("first_bad_crc", c_uint64),
         ("first_unplaced", c_uint64),
         ("index_bad", c_uint64),
+        ("first_bad_value", c_uint64),
     ]
 
 
@@ -162,7 +166,14 @@ _SIGS = {
     "rio_sst_validate": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "rio_sst_data_entries": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "rio_sst_validate_view": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
+         c_void_p]),
     "rio_sst_open": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_void_p), POINTER(SstInfo)]),
+    "rio_sst_open_ex": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint32, POINTER(c_void_p), POINTER(SstInfo)]),
     "rio_sst_entry": (
         c_int,
         [c_void_p, c_uint64, POINTER(c_void_p), POINTER(c_uint64), POINTER(c_void_p), POINTER(c_uint64), POINTER(c_int),

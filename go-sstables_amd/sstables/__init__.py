@@ -7,9 +7,10 @@ the index records are parsed and every value's CRC-64/ISO is computed by the ker
 rio_sstable.hip (rio_sst_index_parse / rio_sst_validate). This module keeps the reference's API
 shape: NewSSTableReader(options...) -> (reader, err), reader.Scan() -> iterator whose Next()
 returns (key, value, err) with the Done sentinel, MetaData(), Get, Contains, Close; errors carry
-the reference's message texts. Tables the device path does not handle (v0 protobuf values,
-recordio v1/v2 files, an index not in the writer's layout) return UnsupportedError: the adapter
-keeps the reference reader for them. There is no CPU fallback.
+the reference's message texts. v0 tables (metadata version 0: every value a protobuf DataEntry,
+sstable_reader.go:303-314) have their values unwrapped on the device (rio_sst_data_entries). A table
+whose index is not in the writer's layout returns UnsupportedError: the adapter keeps the reference
+reader for it. There is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -33,6 +34,7 @@ Version = 1
 Done = GoError("no more items in iterator")  # sstable.go:18
 NotFound = GoError("key was not found")  # sstable.go:19
 _NONE = 0xFFFFFFFFFFFFFFFF
+ProtoWireError = GoError("proto: cannot parse invalid wire-format data")  # protobuf-go's proto.Unmarshal
 
 
 class ChecksumError(GoError):
@@ -95,7 +97,7 @@ def _fmt_key(k: bytes) -> str:
 class _DeviceTable:
     """Both files decoded on the device, index parsed, every value's CRC-64 computed."""
 
-    def __init__(self, base: str, device: int, need_crc: bool):
+    def __init__(self, base: str, device: int, need_crc: bool, v0: bool = False):
         import torch
 
         from recordio.device import DeviceDecoder, header_codec, to_device_file
@@ -144,10 +146,25 @@ class _DeviceTable:
             raise GoError(f"rio_sst_index_parse: {L.strerror(rc)}")
         self.crc = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         vres = torch.empty(2, dtype=torch.int64, device=dev)
-        rc = lib.rio_sst_validate(self.dec.ctx, self.db.out.data_ptr(), self.db.out_off.data_ptr(),
-                                  self.db.rec_off.data_ptr(), self.n_data, self.value_off.data_ptr(),
-                                  self.checksum.data_ptr(), n, self.crc.data_ptr(), vres.data_ptr(),
-                                  ctypes.c_void_p(stream.cuda_stream))
+        self.v0 = v0
+        st = ctypes.c_void_p(stream.cuda_stream)
+        if v0:
+            # every value record is a DataEntry: its value's range in the data arena (MMapProtoReader /
+            # ProtoReader unmarshal, recordio/proto/mmap_proto_reader.go:12-24), hashed as such
+            self.view = torch.empty(2 * max(self.n_data, 1), dtype=torch.int64, device=dev)
+            dres = torch.empty(1, dtype=torch.int64, device=dev)
+            rc = lib.rio_sst_data_entries(self.dec.ctx, self.db.out.data_ptr(), self.db.out_off.data_ptr(), self.n_data,
+                                          self.view.data_ptr(), dres.data_ptr(), st)
+            if rc:
+                raise GoError(f"rio_sst_data_entries: {L.strerror(rc)}")
+            rc = lib.rio_sst_validate_view(self.dec.ctx, self.db.out.data_ptr(), self.db.out_off.data_ptr(),
+                                           self.db.rec_off.data_ptr(), self.n_data, self.view.data_ptr(),
+                                           self.value_off.data_ptr(), self.checksum.data_ptr(), n, self.crc.data_ptr(),
+                                           vres.data_ptr(), st)
+        else:
+            rc = lib.rio_sst_validate(self.dec.ctx, self.db.out.data_ptr(), self.db.out_off.data_ptr(),
+                                      self.db.rec_off.data_ptr(), self.n_data, self.value_off.data_ptr(),
+                                      self.checksum.data_ptr(), n, self.crc.data_ptr(), vres.data_ptr(), st)
         if rc:
             raise GoError(f"rio_sst_validate: {L.strerror(rc)}")
         torch.cuda.synchronize(device)
@@ -162,15 +179,23 @@ class _DeviceTable:
         self.h_data = bytes(self.db.out[:nb_d].cpu().numpy())
         self.h_data_off = u(self.db.out_off, self.n_data + 1)
         self.h_data_flags = self.db.flags[:self.n_data].cpu().tolist()
+        self.h_view = u(self.view, 2 * self.n_data) if v0 else None
 
     def key(self, i) -> bytes:
         o = self.h_key_off[i]
         return self.h_index[o:o + self.h_key_len[i]]
 
     def value(self, j):
+        if self.v0:  # DataEntry.value: nil when the field is absent
+            b, e = self.h_view[2 * j], self.h_view[2 * j + 1]
+            return None if b >= L.RIO_VALUE_BAD else self.h_data[b:e]
         if self.h_data_flags[j] & L.RIO_FLAG_NIL:
             return None
         return self.h_data[self.h_data_off[j]:self.h_data_off[j + 1]]
+
+    def value_proto_bad(self, j) -> bool:
+        """v0 tables: data record j is not a valid DataEntry (proto.Unmarshal fails)."""
+        return self.v0 and self.h_view[2 * j] == L.RIO_VALUE_BAD
 
     def value_failed(self, j) -> bool:
         """Data record j does not decompress (RIO_FLAG_CORRUPT / RIO_FLAG_EOF)."""
@@ -195,7 +220,8 @@ class SSTableReader:
     def Scan(self):  # noqa: N802
         """SSTableFullScanIterator (sstable_iterator.go:68-111): index entries in file order paired
         with data records read sequentially."""
-        return _FullScanIterator(self, self.opts.skipHashCheckOnRead), None
+        # v0 tables: V0SSTableFullScanIterator (sstable_iterator.go:34-66) never checks hashes
+        return _FullScanIterator(self, self.opts.skipHashCheckOnRead or self.t.v0), None
 
     def _value_at(self, i, skip_check):
         """getValueAtOffset (sstable_reader.go:80-117) for index entry i (the writer's layout)."""
@@ -204,6 +230,9 @@ class SSTableReader:
             vo, path = t.h_value_off[i], os.path.join(self.opts.basePath, DataFileName)
             inner = wrap(f"failed decompressing record at offset {vo} in mmap reader for '{path}'", t.codec_error(i))
             return None, wrap(f"error in sstable '{self.opts.basePath}' while getting value at offset {vo}", inner)
+        if t.value_proto_bad(i):  # v0: MMapProtoReader.ReadNextAt's proto.Unmarshal error (sstable_reader.go:79-86)
+            return None, wrap(f"error in sstable '{self.opts.basePath}' while getting value at offset {t.h_value_off[i]}",
+                              ProtoWireError)
         v = t.value(i)
         if skip_check:
             return v, None
@@ -256,6 +285,8 @@ class _FullScanIterator:
                                        f"{L.strerror(t.data_info['status'])}")
         if t.value_failed(i):  # dataReader.ReadNext's codec error, returned as is (sstable_iterator.go:87-90)
             return None, None, t.codec_error(i)
+        if t.value_proto_bad(i):  # v0: the proto reader's ReadNext, unmarshal error as is (:52-56)
+            return None, None, ProtoWireError
         v = t.value(i)
         if self.skip:
             return key, v, None
@@ -275,10 +306,9 @@ def NewSSTableReader(*options):  # noqa: N802
     meta, err = proto.read_metadata_if_exists(os.path.join(o.basePath, MetaFileName))
     if err is not None:
         return None, GoError(f"error while reading metadata of sstable in '{o.basePath}': {err}", wrapped=err)
-    if meta.version == 0:
-        return None, UnsupportedError(f"sstable '{o.basePath}' has v0 (protobuf DataEntry) values")
+    v0 = meta.version == 0  # values are protobuf DataEntry records (sstable_reader.go:303-314)
     try:
-        t = _DeviceTable(o.basePath, o.device, True)
+        t = _DeviceTable(o.basePath, o.device, True, v0)
     except UnsupportedError as e:
         return None, e
     # a flagged index record ends Load's loop before any later terminal status is reached
@@ -295,7 +325,8 @@ def NewSSTableReader(*options):  # noqa: N802
     if t.unplaced != _NONE:
         return None, UnsupportedError(f"sstable '{o.basePath}': index entry {t.unplaced} is not in the writer's layout")
     r = SSTableReader(o, meta, t)
-    if not o.skipHashCheckOnLoad and (t.bad_crc != _NONE or t.value_bad != _NONE):
+    # validateDataFile returns at once for v0 tables (sstable_reader.go:205-209)
+    if not v0 and not o.skipHashCheckOnLoad and (t.bad_crc != _NONE or t.value_bad != _NONE):
         # validateDataFile stops at the first entry whose value fails to read or to hash; a value
         # that does not decompress has no meaningful CRC, so on a tie it is the read error
         i = min(t.bad_crc, t.value_bad)

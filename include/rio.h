@@ -228,6 +228,22 @@ int rio_sst_validate(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_
                      const uint64_t* d_data_rec_off, uint64_t n_data, const uint64_t* d_value_off,
                      const uint64_t* d_checksum, uint64_t n_index, uint64_t* d_crc_out, uint64_t* d_result,
                      void* stream);
+/* v0 tables (metadata version 0: values are protobuf DataEntry {value = 1}, sstable_reader.go:303-314,
+ * sstables/proto/sstable.proto:12-14). rio_sst_data_entries replaces the proto.Unmarshal of every value
+ * record (MMapProtoReader.ReadNextAt / ProtoReader.ReadNext, recordio/proto/mmap_proto_reader.go:12-24)
+ * on the decoded data arena: d_view[2j], d_view[2j+1] = [begin, end) of record j's DataEntry.value in
+ * d_data_out, both RIO_VALUE_NIL when the field is absent (value nil) and RIO_VALUE_BAD when the
+ * record is not a valid DataEntry ("proto: cannot parse invalid wire-format data").
+ * d_result[0] = first malformed record or ~0. rio_sst_validate_view is rio_sst_validate over those
+ * ranges (a nil or malformed value hashes as empty). */
+#define RIO_VALUE_NIL (~0ull)
+#define RIO_VALUE_BAD (~0ull - 1)
+int rio_sst_data_entries(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_data_off, uint64_t n_data,
+                         uint64_t* d_view, uint64_t* d_result, void* stream);
+int rio_sst_validate_view(rio_ctx* ctx, const uint8_t* d_data_out, const uint64_t* d_data_off,
+                          const uint64_t* d_data_rec_off, uint64_t n_data, const uint64_t* d_view,
+                          const uint64_t* d_value_off, const uint64_t* d_checksum, uint64_t n_index,
+                          uint64_t* d_crc_out, uint64_t* d_result, void* stream);
 
 /* ---- sstables, host-memory API (the cgo binding: one call per table) ------------------------
  * rio_sst_open replaces NewSSTableReader's load (sstable_reader.go:250-345) for the tables the device
@@ -254,10 +270,18 @@ typedef struct rio_sst_info {
                                  ReadNext error there, before any later index status; ~0 = none.
                                  n_entries stops at the first flagged index record (gzip's bare io.EOF
                                  ends the index cleanly, slice_key_index.go:117-126) */
+    uint64_t first_bad_value; /* v0 tables: first data record that is not a valid DataEntry; ~0 = none */
 } rio_sst_info;
 typedef struct rio_sst rio_sst;
 int rio_sst_open(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, const uint8_t* data_file,
                  uint64_t data_len, rio_sst** out, rio_sst_info* info);
+/* flags: RIO_SST_V0_VALUES for a table whose metadata version is 0 (no meta.pb.bin, or version 0):
+ * values are DataEntry protos (rio_sst_data_entries), rio_sst_entry returns DataEntry.value and
+ * RIO_ERR_PROTO for a malformed one; validateDataFile does not run for such tables (:205-209), so
+ * first_bad_crc is left ~0 and crc still holds each value's CRC-64. */
+#define RIO_SST_V0_VALUES 1u
+int rio_sst_open_ex(rio_ctx* ctx, const uint8_t* index_file, uint64_t index_len, const uint8_t* data_file,
+                    uint64_t data_len, uint32_t flags, rio_sst** out, rio_sst_info* info);
 /* Entry i in index order (SSTableFullScanIterator.Next, sstable_iterator.go:77-111): key, the value of
  * data record i (is_nil for a nil record), the stored valueOffset and checksum and the value's CRC-64.
  * Returns RIO_OK, RIO_ERR_ARG for i >= n_entries, the data file's terminal status when data record i

@@ -952,6 +952,33 @@ int orc_index_entry(const uint8_t* b, uint64_t n, uint64_t* key_off, uint64_t* k
     return 0;
 }
 
+/* proto.Unmarshal into a reset DataEntry {value = 1} (sstables/proto/sstable.proto:12-14; v0 tables'
+ * values, read through MMapProtoReader.ReadNextAt, recordio/proto/mmap_proto_reader.go:12-24):
+ * *present = 1 when field 1 was seen with wire type 2 (the last one wins), [value_off, + value_len).
+ * Returns -1 for malformed input. */
+int orc_data_entry(const uint8_t* b, uint64_t n, int* present, uint64_t* value_off, uint64_t* value_len) {
+    uint64_t pos = 0;
+    *present = 0;
+    *value_off = *value_len = 0;
+    while (pos < n) {
+        uint64_t tag, v;
+        if (pb_varint(b, n, &pos, &tag)) return -1;
+        uint64_t fn = tag >> 3;
+        int wt = (int)(tag & 7);
+        if (fn < 1 || fn > 0x1FFFFFFFull) return -1;
+        if (fn == 1 && wt == 2) {
+            if (pb_varint(b, n, &pos, &v) || v > n - pos) return -1;
+            *present = 1;
+            *value_off = pos;
+            *value_len = v;
+            pos += v;
+        } else if (pb_skip(b, n, &pos, fn, wt, 0)) {
+            return -1;
+        }
+    }
+    return 0;
+}
+
 /* NewSSTableReader (index load + validateDataFile) + Scan over in-memory data.rio / index.rio
  * images, for the CPU baseline: returns the entries scanned (0 on a decode / proto failure),
  * *first_bad = first checksum mismatch or UINT64_MAX. Values pair with entries by position after

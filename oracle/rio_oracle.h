@@ -82,6 +82,7 @@ int orc_disk_index_search(const uint8_t* f, uint64_t len, const uint8_t* key, ui
 uint64_t orc_snappy_encode(uint8_t* dst, const uint8_t* src, uint64_t n);
 uint64_t orc_encode_file(const uint8_t* records, const uint64_t* off, const uint8_t* flags, uint64_t n, uint32_t comp,
                          uint8_t* out, uint64_t cap, uint64_t* rec_off);
+int orc_data_entry(const uint8_t* b, uint64_t n, int* present, uint64_t* value_off, uint64_t* value_len);
 uint64_t orc_sst_scan(const uint8_t* index, uint64_t ilen, const uint8_t* data, uint64_t dlen, uint64_t* first_bad);
 
 #ifdef __cplusplus

@@ -213,14 +213,71 @@ def index_entry(rec: bytes):
     return r[ko.value:ko.value + kl.value], vo.value, cs.value
 
 
+class BadProto:
+    """A v0 value record that is not a valid DataEntry (proto.Unmarshal's error)."""
+
+
+def data_entry(rec):
+    """proto.Unmarshal of one DataEntry record -> its value (None when absent), BadProto if malformed."""
+    b, n = _buf(rec or b"")
+    present, vo, vl = c_int(), c_uint64(), c_uint64()
+    L = lib()
+    L.orc_data_entry.argtypes = [c_void_p, c_uint64, POINTER(c_int), POINTER(c_uint64), POINTER(c_uint64)]
+    if L.orc_data_entry(b, n, byref(present), byref(vo), byref(vl)):
+        return BadProto()
+    r = bytes(rec or b"")
+    return r[vo.value:vo.value + vl.value] if present.value else None
+
+
+def meta_version(base: str) -> int:
+    """MetaData.version (field 7, sstable.proto:16-26) of meta.pb.bin; 0 when the file is absent
+    (readMetaDataIfExists, sstable_reader.go:356-377). Wire format read field by field (varints,
+    length-delimited and fixed fields skipped)."""
+    p = os.path.join(base, "meta.pb.bin")
+    if not os.path.exists(p):
+        return 0
+    b, i, ver = open(p, "rb").read(), 0, 0
+
+    def varint():
+        nonlocal i
+        v = s = 0
+        while True:
+            c = b[i]
+            i += 1
+            v |= (c & 0x7F) << s
+            s += 7
+            if c < 0x80:
+                return v
+    while i < len(b):
+        tag = varint()
+        fn, wt = tag >> 3, tag & 7
+        if wt == 0:
+            v = varint()
+            if fn == 7:
+                ver = v
+        elif wt == 2:
+            ln = varint()  # (not `i += varint()`: that reads i before the call advances it)
+            i += ln
+        elif wt in (1, 5):
+            i += 8 if wt == 1 else 4
+        else:
+            raise ValueError("meta.pb.bin: unexpected wire type")
+    return ver
+
+
 def sstable_oracle(base: str) -> dict:
     """NewSSTableReader + validateDataFile + Scan restated on the host: index entries in file order
     (SliceKeyIndexLoader.Load, slice_key_index.go:91-131), value at valueOffset via ReadNextAt
     (sstable_reader.go:80-117), CRC-64/ISO vs the stored checksum (0 = unchecked), and the scan's
-    positional pairing of index entries with data records (sstable_iterator.go:77-111)."""
+    positional pairing of index entries with data records (sstable_iterator.go:77-111). v0 tables
+    (metadata version 0): values are DataEntry records unwrapped by proto.Unmarshal, and
+    validateDataFile does not run (sstable_reader.go:205-209): first_bad / value_bad stay None."""
+    v0 = meta_version(base) == 0
     idx = file_reader_decode(open(os.path.join(base, "index.rio"), "rb").read())
     data_img = open(os.path.join(base, "data.rio"), "rb").read()
     dat = file_reader_decode(data_img)
+    if v0:
+        dat["records"] = [r if isinstance(r, BadRecord) else data_entry(r) for r in dat["records"]]
     entries, bad_proto, index_bad = [], None, None
     for i, r in enumerate(idx["records"]):
         if isinstance(r, BadRecord):  # Load's ReadNext error; gzip's bare io.EOF ends the loop
@@ -239,18 +296,18 @@ def sstable_oracle(base: str) -> dict:
         if j != i and unplaced is None:
             unplaced = i
         val = dat["records"][j] if j is not None else None
-        if isinstance(val, BadRecord):  # getValueAtOffset's ReadNextAt error (sstable_reader.go:90-94)
+        if isinstance(val, (BadRecord, BadProto)):  # getValueAtOffset's ReadNextAt / Unmarshal error (:79-94)
             crcs.append(None)
-            if value_bad is None:
+            if value_bad is None and not v0:
                 value_bad = i
             continue
         c = crc64_iso(val or b"")
         crcs.append(c)
-        if first_bad is None and cs != 0 and c != cs:
+        if first_bad is None and cs != 0 and c != cs and not v0:
             first_bad = i
     return {"index_status": idx["status"], "data_status": dat["status"], "entries": entries,
             "bad_proto": bad_proto, "index_bad": index_bad, "values": dat["records"], "crcs": crcs,
-            "first_bad": first_bad, "value_bad": value_bad, "unplaced": unplaced}
+            "first_bad": first_bad, "value_bad": value_bad, "unplaced": unplaced, "v0": v0}
 
 
 def disk_index_search(index: bytes, key: bytes, seek_len: int = 4096):

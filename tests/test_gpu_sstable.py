@@ -4,7 +4,7 @@ NewSSTableReader (sstables/sstable_reader.go:250-345: index via SliceKeyIndexLoa
 unless SkipHashCheckOnLoad) and Scan (SSTableFullScanIterator, sstable_iterator.go:68-111) on tables
 the mirror's writer produced (v4 recordio, as sstable_writer.go writes them), compared with the
 oracle's restatement, and on the reference's own fixtures (recordio v2, sstable_reader_test.go's
-expectations); the v0-values fixture must be handed back (UnsupportedError)."""
+expectations), including the v0 fixture whose values are protobuf DataEntry records."""
 import os
 import random
 import struct
@@ -194,11 +194,98 @@ def test_reference_fixture_checksum_mismatch():
     assert serr == S.ChecksumError(0x738FFFFF90000000, 0x688FFFFF90000000)
 
 
-def test_v0_values_table_is_handed_back():
-    # SimpleWriteHappyPathSSTable: recordio v1 files and no meta.pb.bin, i.e. metadata version 0 with
-    # protobuf DataEntry values (sstable_reader.go:303-314): the reference reader keeps it
+def test_reference_v0_fixture_on_device():
+    """sstable_reader_test.go:11-26, 185-193: SimpleWriteHappyPathSSTable (recordio v1 files, no
+    meta.pb.bin: metadata version 0, every value a protobuf DataEntry) loads on the device."""
     r, err = S.NewSSTableReader(S.ReadBasePath(_fixture("SimpleWriteHappyPathSSTable")))
-    assert r is None and isinstance(err, S.UnsupportedError), err
+    assert err is None, err
+    m = r.MetaData()
+    assert (m.NumRecords, m.NullValues, len(m.MinKey), len(m.MaxKey), m.version) == (0, 0, 0, 0, 0)
+    for k, v in SEVEN:
+        assert r.Contains(k) == (True, None)
+        assert r.Get(k) == (v, None)
+    assert scan_all(r) == (SEVEN, None)  # V0SSTableFullScanIterator (sstable_iterator.go:34-66)
+    for k in (b"", b"\x01", b"\x01\x02\x03"):
+        assert r.Contains(k) == (False, None)
+        assert r.Get(k)[1] is S.NotFound
+    assert r.t.v0 and r.t.index_info["version"] == 1 and r.t.data_info["version"] == 1
+    check_against_oracle(_fixture("SimpleWriteHappyPathSSTable"))
+
+
+def data_entry(v):
+    """DataEntry {value = 1} as protobuf-go marshals it (the field is omitted for nil / empty)."""
+    return b"" if not v else b"\x0a" + proto_uvarint(len(v)) + v
+
+
+def proto_uvarint(n):
+    out = bytearray()
+    while n >= 0x80:
+        out.append(n & 0x7F | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def write_v0_table(base, values, comp=2, keys=None):
+    """A v0 table (no meta.pb.bin): index entries without checksums, data records given raw (the
+    DataEntry bytes, or anything else for malformed ones)."""
+    os.makedirs(base, exist_ok=True)
+    d, ix = _Image(comp), _Image(0)
+    keys = keys or [be(i) for i in range(len(values))]
+    for k, raw in zip(keys, values):
+        ix.write(proto.encode_index_entry(k, d.write(raw), 0))
+    for name, b in (("data.rio", d.bytes()), ("index.rio", ix.bytes())):
+        with open(os.path.join(base, name), "wb") as fh:
+            fh.write(b)
+
+
+@pytest.mark.parametrize("comp", [0, 2])
+def test_v0_table_matches_oracle(tmp_path, comp):
+    rng = random.Random(50 + comp)
+    raws = []
+    for i in range(1200):
+        v = text(rng, rng.randint(0, 900))
+        k = rng.random()
+        if k < 0.05:
+            raws.append(b"")                                           # value nil (field absent)
+        elif k < 0.1:
+            raws.append(b"\x0a\x00")                                   # present, empty
+        elif k < 0.15:
+            raws.append(b"\x12\x03abc" + data_entry(v) + b"\x18\x07")  # unknown fields around it
+        elif k < 0.2:
+            raws.append(data_entry(b"old") + data_entry(v))            # last occurrence wins
+        else:
+            raws.append(data_entry(v))
+    base = str(tmp_path / "t")
+    write_v0_table(base, raws, comp)
+    o, r = check_against_oracle(base)
+    assert o["v0"]
+    for i in range(0, 1200, 7):
+        assert r.Get(be(i)) == (o["values"][i], None)
+
+
+def test_v0_malformed_value(tmp_path):
+    raws = [data_entry(be(i + 1)) for i in range(20)]
+    raws[7] = b"\x0a\x09abc"  # truncated bytes field
+    base = str(tmp_path / "t")
+    write_v0_table(base, raws)
+    o = orc.sstable_oracle(base)
+    assert isinstance(o["values"][7], orc.BadProto) and o["first_bad"] is None
+    r, err = S.NewSSTableReader(S.ReadBasePath(base))  # validateDataFile skips v0 tables (:205-209)
+    assert err is None
+    v, gerr = r.Get(be(7))
+    assert v is None and str(gerr).endswith("proto: cannot parse invalid wire-format data")
+    assert f"while getting value at offset {o['entries'][7][1]}" in str(gerr)
+    assert r.Get(be(8)) == (be(9), None)
+    got, serr = scan_all(r)
+    assert got == [(be(i), be(i + 1)) for i in range(7)] and str(serr) == "proto: cannot parse invalid wire-format data"
+    # the host handle with RIO_SST_V0_VALUES
+    rc, info, ents = sst_open_host(base, v0=True)
+    from recordio import _lib as L
+
+    assert rc == 0 and info.first_bad_value == 7 and info.n_entries == 20
+    assert [e[0] for e in ents] == [0] * 7 + [L.RIO_ERR_PROTO] + [0] * 12
+    assert [e[2] for e in ents[:7] + ents[8:]] == [be(i + 1) for i in range(20) if i != 7]
 
 
 def test_index_out_of_layout_is_handed_back(tmp_path):
@@ -244,7 +331,7 @@ def test_large_table_sha1_keys(tmp_path):
 
 
 # ---- the host-memory handle (rio_sst_open / rio_sst_entry): what the cgo NewSSTableReader binds ----
-def sst_open_host(base):
+def sst_open_host(base, v0=False):
     import ctypes
 
     from recordio import _lib as L
@@ -255,7 +342,11 @@ def sst_open_host(base):
     imgs = [open(os.path.join(base, f), "rb").read() for f in ("index.rio", "data.rio")]
     h = ctypes.c_void_p()
     info = L.SstInfo()
-    rc = lib.rio_sst_open(dec.ctx, imgs[0], len(imgs[0]), imgs[1], len(imgs[1]), ctypes.byref(h), ctypes.byref(info))
+    if v0:
+        rc = lib.rio_sst_open_ex(dec.ctx, imgs[0], len(imgs[0]), imgs[1], len(imgs[1]), L.RIO_SST_V0_VALUES,
+                                 ctypes.byref(h), ctypes.byref(info))
+    else:
+        rc = lib.rio_sst_open(dec.ctx, imgs[0], len(imgs[0]), imgs[1], len(imgs[1]), ctypes.byref(h), ctypes.byref(info))
     if rc:
         return rc, info, None
     ents = []
@@ -304,6 +395,9 @@ def test_host_handle_mismatch_and_handback(tmp_path):
     rc, info, ents = sst_open_host(_fixture("SimpleWriteHappyPathSSTableRecordIOV2"))
     assert rc == 0 and info.n_entries == 7 and info.first_bad_crc == (1 << 64) - 1
     assert [(e[1], e[2]) for e in ents] == SEVEN and all(e[5] == e[4] for e in ents)
+    rc, info, ents = sst_open_host(_fixture("SimpleWriteHappyPathSSTable"), v0=True)
+    assert rc == 0 and info.n_entries == 7 and info.first_bad_value == (1 << 64) - 1
+    assert [(e[1], e[2]) for e in ents] == SEVEN and all(e[0] == 0 and e[4] == 0 for e in ents)
     base2 = str(tmp_path / "m")
     write_triples(base2, triples_for([(be(i), be(i)) for i in range(20)]),
                   tamper=lambda i, e, off: b"\x0a\x7fab" if i == 6 else e)

@@ -51,10 +51,25 @@ def test_fixture_v0_proto_values():  # sstable_reader_test.go:11-26: no metadata
     m, err = proto.read_metadata_if_exists(os.path.join(base, "meta.pb.bin"))
     assert err is None and m.version == 0 and m.numRecords == 0
     o = orc.sstable_oracle(base)
-    assert [e[0] for e in o["entries"]] == [be(i) for i in range(1, 8)]
-    # each data record is a DataEntry proto {value = 1: bytes}
-    assert [v[2:] for v in o["values"]] == [be(i + 1) for i in range(1, 8)]
-    assert all(v[:2] == b"\x0a\x04" for v in o["values"])
+    assert o["v0"] and [e[0] for e in o["entries"]] == [be(i) for i in range(1, 8)]
+    # each data record is a DataEntry proto {value = 1: bytes}; the oracle unwraps it
+    assert o["values"] == [be(i + 1) for i in range(1, 8)]
+    raw = orc.file_reader_decode(open(os.path.join(base, "data.rio"), "rb").read())["records"]
+    assert all(r == b"\x0a\x04" + v for r, v in zip(raw, o["values"]))
+    assert o["first_bad"] is None and o["unplaced"] is None
+
+
+def test_data_entry_wire_rules():
+    de = orc.data_entry
+    assert de(b"") is None                                            # no field 1: value nil
+    assert de(b"\x0a\x00") == b""                                     # present and empty
+    assert de(b"\x0a\x02ab\x0a\x01c") == b"c"                         # last occurrence wins
+    assert de(b"\x08\x05\x0a\x01z") == b"z"                           # field 1 as varint: unknown, skipped
+    assert de(b"\x08\x05") is None
+    assert de(b"\x12\x01x\x0a\x01y\x25\x00\x00\x00\x00") == b"y"      # unknown bytes / fixed32 skipped
+    assert de(b"\x2b\x08\x01\x2c\x0a\x01q") == b"q"                   # group skipped to its end tag
+    for bad in (b"\x0a\x05ab", b"\x00", b"\x2c", b"\x0a", b"\x08" + b"\xff" * 9 + b"\x02", b"\x0e"):
+        assert isinstance(de(bad), orc.BadProto), bad
 
 
 def test_crc64_iso_known_answer():
