@@ -223,6 +223,28 @@ class SSTableReader:
         # v0 tables: V0SSTableFullScanIterator (sstable_iterator.go:34-66) never checks hashes
         return _FullScanIterator(self, self.opts.skipHashCheckOnRead or self.t.v0), None
 
+    def ScanStartingAt(self, key: bytes):  # noqa: N802
+        """SSTableIterator over IteratorStartingAt (sstable_reader.go:161-167, slice_key_index.go:49-52):
+        entries from the first key >= key, values by getValueAtOffset."""
+        import bisect
+
+        return _KeyRangeIterator(self, bisect.bisect_left(self._index_keys(), bytes(key)), self.t.n_index), None
+
+    def ScanRange(self, key_lower: bytes, key_higher: bytes):  # noqa: N802
+        """SSTableIterator over IteratorBetween (sstable_reader.go:169-175, slice_key_index.go:54-70):
+        both ends inclusive."""
+        import bisect
+
+        lo, hi = bytes(key_lower), bytes(key_higher)
+        if lo > hi:
+            return None, wrap(f"error in sstable '{self.opts.basePath}' in ScanRange",
+                              GoError("keyHigher is lower than keyLower"))
+        ks = self._index_keys()
+        start, end = bisect.bisect_left(ks, lo), bisect.bisect_left(ks, hi)
+        if end < len(ks) and ks[end] <= hi:
+            end += 1
+        return _KeyRangeIterator(self, start, end), None
+
     def _value_at(self, i, skip_check):
         """getValueAtOffset (sstable_reader.go:80-117) for index entry i (the writer's layout)."""
         t = self.t
@@ -267,6 +289,23 @@ class SSTableReader:
     def Close(self):  # noqa: N802
         self.t = None
         return None
+
+
+class _KeyRangeIterator:
+    """SSTableIterator (sstable_iterator.go:11-32): index entries [i, end) with getValueAtOffset."""
+
+    def __init__(self, r: SSTableReader, i: int, end: int):
+        self.r, self.i, self.end = r, i, end
+
+    def Next(self):  # noqa: N802
+        if self.i >= self.end:
+            return None, None, Done
+        i = self.i
+        self.i += 1
+        v, err = self.r._value_at(i, self.r.opts.skipHashCheckOnRead)
+        if err is not None:
+            return None, None, err
+        return self.r.t.key(i), v, None
 
 
 class _FullScanIterator:

@@ -511,3 +511,68 @@ def test_flagged_index_record_comes_before_a_later_index_error(tmp_path, flag):
         assert err is None
         got, serr = scan_all(r)
         assert serr is None and got == items[:4]
+
+
+V0C = os.path.join(GOLDEN, "sstables_v0_compat")
+
+
+@pytest.mark.parametrize("name,meta", [("SimpleWriteHappyPathSSTable", (0, b"", b"")),
+                                       ("SimpleWriteHappyPathSSTableRecordIOV2", (7, be(1), be(7))),
+                                       ("SimpleWriteHappyPathSSTableWithBloom", (0, b"", b"")),
+                                       ("SimpleWriteHappyPathSSTableWithMetaData", (7, be(1), be(7)))])
+def test_v0_compat_fixtures_on_device(name, meta):
+    """sstable_reader_v0compat_test.go:9-91: metadata version 0 tables (DataEntry values, recordio v1 /
+    v2, snappy) with their metadata, content, negative lookups and full scan."""
+    r, err = S.NewSSTableReader(S.ReadBasePath(os.path.join(V0C, name)))
+    assert err is None, err
+    m = r.MetaData()
+    assert (m.NumRecords, m.MinKey, m.MaxKey, m.version) == meta + (0,)
+    for k, v in SEVEN:
+        assert r.Contains(k) == (True, None) and r.Get(k) == (v, None)
+    for k in (b"", b"\x01", b"\x01\x02\x03"):
+        assert r.Contains(k) == (False, None) and r.Get(k)[1] is S.NotFound
+    assert scan_all(r) == (SEVEN, None)
+    check_against_oracle(os.path.join(V0C, name))
+
+
+def drain(it):
+    out = []
+    while True:
+        k, v, err = it.Next()
+        if err is S.Done:
+            return out
+        assert err is None
+        out.append((k, v))
+
+
+def test_v0_compat_scan_starting_at_and_range():  # sstable_reader_v0compat_test.go:99-160
+    r, err = S.NewSSTableReader(S.ReadBasePath(os.path.join(V0C, "SimpleWriteHappyPathSSTableWithMetaData")))
+    assert err is None
+    it, err = r.ScanStartingAt(be(0))
+    assert err is None and drain(it) == SEVEN
+    for i in range(7):
+        it, _ = r.ScanStartingAt(SEVEN[i][0])
+        assert drain(it) == SEVEN[i:]
+    it, _ = r.ScanStartingAt(be(10))
+    assert it.Next() == (None, None, S.Done)
+    it, err = r.ScanRange(be(0), be(10))
+    assert err is None and drain(it) == SEVEN
+    it, _ = r.ScanRange(be(1), be(7))
+    assert drain(it) == SEVEN
+    it, _ = r.ScanRange(be(4), be(4))
+    assert drain(it) == [SEVEN[3]]
+    _, err = r.ScanRange(be(1), be(0))
+    assert err is not None
+    for i in range(7):
+        it, _ = r.ScanRange(SEVEN[i][0], be(10))
+        assert drain(it) == SEVEN[i:]
+        it, _ = r.ScanRange(be(0), SEVEN[i][0])
+        assert drain(it) == SEVEN[:i + 1]
+    for i in range(7):  # end crossing to the left
+        it, err = r.ScanRange(SEVEN[i][0], SEVEN[6 - i][0])
+        if i <= 3:
+            assert err is None and drain(it) == SEVEN[i:7 - i]
+        else:
+            assert err is not None
+    it, err = r.ScanRange(be(10), be(100))
+    assert err is None and it.Next() == (None, None, S.Done)

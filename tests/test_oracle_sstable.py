@@ -104,3 +104,12 @@ def test_index_entry_wire_rules():
     assert ie(b"\x00") is None                                       # field number 0
     assert ie(b"\x2c") is None                                       # unmatched end group
     assert ie(b"\x10" + b"\xff" * 9 + b"\x02") is None               # varint overflow
+
+
+@pytest.mark.parametrize("name", ["SimpleWriteHappyPathSSTable", "SimpleWriteHappyPathSSTableRecordIOV2",
+                                  "SimpleWriteHappyPathSSTableWithBloom", "SimpleWriteHappyPathSSTableWithMetaData"])
+def test_v0_compat_fixtures(name):  # sstable_reader_v0compat_test.go: keys 1..7 -> DataEntry value key+1
+    o = orc.sstable_oracle(os.path.join(GOLDEN, "sstables_v0_compat", name))
+    assert o["v0"] and o["unplaced"] is None and o["bad_proto"] is None
+    assert [e[0] for e in o["entries"]] == [be(i) for i in range(1, 8)]
+    assert o["values"] == [be(i + 1) for i in range(1, 8)]
