@@ -231,6 +231,8 @@ def lib():
             pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("RIO_LIB_PATH") and not hasattr(L, name):
+                continue  # an older experiment build (A/B timing) may predate some entry points
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
