@@ -115,6 +115,34 @@ def legacy_file(records, comp=0, version=2):
     return bytes(out)
 
 
+def to_version(img: bytes, version: int) -> bytes:
+    """A v4 image re-framed as v3 / v2 / v1 (file_writer.go's older header layouts): the same payloads,
+    each header rewritten; nil records need v3+."""
+    assert struct.unpack_from("<I", img, 0)[0] == 4
+    out = bytearray(file_header(version, struct.unpack_from("<I", img, 4)[0]))
+    p, n = 8, len(img)
+
+    def uv(i):
+        v = s = 0
+        while True:
+            c = img[i]
+            i += 1
+            v |= (c & 0x7F) << s
+            s += 7
+            if c < 0x80:
+                return v, i
+    comp = struct.unpack_from("<I", img, 4)[0]
+    while p < n:
+        nil = img[p + 3] == 1
+        u, q = uv(p + 4)
+        c, q = uv(q)
+        _, q = uv(q)  # header CRC
+        plen = 0 if nil else (c if comp else u)
+        out += header_for(version, u, c, nil=nil) + img[q:q + plen]
+        p = q + plen
+    return bytes(out)
+
+
 def mixed_records(n, seed, max_len=3000, nil_frac=0.05):
     rng = random.Random(seed)
     recs = []

@@ -209,6 +209,17 @@ def test_full_size_headline_workload_exact():
     assert_same_as_oracle(g, o, "C2")
 
 
+@pytest.mark.parametrize("version", [3, 2, 1])
+def test_full_size_headline_workload_older_versions(version):
+    """The C2 workload (1M x 1 KiB snappy text-like) re-framed with the v3 / v2 / v1 header layouts
+    (readRecordHeaderV3 / V2 / V1): every byte and offset equals the oracle."""
+    img = corpus.to_version(bytes(corpus.generate(1_000_000, 1024, 2, kind=1, seed=1)), version)
+    o = orc.file_reader_decode_arrays(img)
+    g = gpu_decode_arrays(img)
+    assert o["n_records"] == 1_000_000 and o["status"] == STATUS["EOF"] and img[0] == version
+    assert_same_as_oracle(g, o, f"C2 v{version}")
+
+
 def test_full_size_c3_10m_64b_records_exact():
     """C3 at full size (10M x 64 B snappy text-like, seed 3 as bench.py): sortedness and sizes, then
     every byte and offset against the oracle."""
