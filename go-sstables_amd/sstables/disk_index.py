@@ -39,6 +39,8 @@ class IndexVal:
 def _error(status: int) -> GoError:
     if status == L.RIO_ERR_PROTO:
         return GoError("proto: cannot parse invalid wire-format data")
+    if status == L.RIO_ERR_UNSUPPORTED:  # a v1 index: every probe's SeekNext fails (mmap_reader.go:62-64)
+        return GoError("unsupported on files with version lower than v2")
     from recordio.reader import _base_error
 
     return _base_error(status)

@@ -257,3 +257,19 @@ def test_reference_v2_fixture_index():
     qs = [be(i) for i in range(0, 10)] + [b"", b"\x00\x00\x00\x04\x00"]
     got = check(img, qs)
     assert [g[2] for g in got[:10]] == [False] + [True] * 7 + [False, False]
+
+
+def test_v1_index_through_the_api(tmp_path):
+    """DiskKeyIndex over a v1 index.rio: Get / Contains fail with the reference's SeekNext error."""
+    import corpus
+
+    p = tmp_path / "index.rio"
+    p.write_bytes(corpus.to_version(bytes(index_image(entries_for([be(i) for i in range(1, 8)]))), 1))
+    idx, err = DiskIndexLoader().Load(str(p), None)
+    assert err is None and idx.Open() is None
+    try:
+        v, err = idx.Get(be(3))
+        assert str(err) == "unsupported on files with version lower than v2"
+        assert str(idx.Contains(be(3))[1]) == "unsupported on files with version lower than v2"
+    finally:
+        idx.Close()
