@@ -107,7 +107,7 @@ extern "C" int rio_status_is_eof(int s) {
 extern "C" const char* rio_build_info(void) { return "librio gfx950 recordio v3/v4 decode"; }
 
 extern "C" uint64_t rio_max_records(uint64_t len) {
-    return len <= RIO_FILE_HEADER_BYTES ? 1 : (len - RIO_FILE_HEADER_BYTES) / 6 + 1;
+    return len <= RIO_FILE_HEADER_BYTES ? 1 : (len - RIO_FILE_HEADER_BYTES) / 5 + 1;  // v2's 5-byte empty record
 }
 
 #define HIP_TRY(x)                                  \
@@ -233,7 +233,7 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     P.comp_hint = RIO_COMP_UNKNOWN;
     P.zero_done = 0;
     P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + ctx->chunk_bytes - 1) / ctx->chunk_bytes : 0;
-    P.slots = ctx->chunk_bytes / 6 + 1;
+    P.slots = ctx->chunk_bytes / 5 + 1;  // records starting in a chunk: the smallest is v2's 5 bytes
     P.n_blocks = (P.n_chunks + 255) / 256;
     const uint64_t nc = std::max<uint64_t>(P.n_chunks, 1), nb = std::max<uint64_t>(P.n_blocks, 1);
     HIP_TRY(A.scratch_off.ensure(nc * P.slots * 8));

@@ -199,7 +199,8 @@ int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uint8_t* const
                             uint8_t* const* d_out, const uint64_t* out_cap, uint64_t* const* d_out_off,
                             uint64_t* const* d_rec_off, uint8_t* const* d_flags, const uint64_t* rec_cap,
                             rio_file_info* const* d_info, void* stream);
-/* Upper bound on records in a file of `len` bytes (smallest v3/v4 record is 6/7 bytes). */
+/* Upper bound on records in a file of `len` bytes (the smallest record is v2's empty one, 5 bytes:
+ * magic, u = 0, c = 0; v3 / v4 / v1 take 6 / 7 / 20). */
 uint64_t rio_max_records(uint64_t len);
 /* Kernel-timing probe for benchmarks: per-stage device milliseconds of the last
  * rio_device_decode on this ctx (frame, scan, decode); fills up to n entries, returns count. */

@@ -270,6 +270,9 @@ def cases():
         out.append((f"v{ver}_embedded", legacy_file(embedded_file_records(40, 9), 0, ver)))
         out.append((f"v{ver}_text_snappy_1k", legacy_file(
             [bytes(r) for r in text_records(3000, 30 + ver, 900, 1100)], 2, ver)))
+    # v2's smallest record (5 bytes: magic, u = 0, c = 0): more records start in a 32 KiB chunk than
+    # any v3 / v4 record size allows (the framing's per-chunk slots and rio_max_records bound on it)
+    out.append(("v2_empty_records", legacy_file([b""] * 30000 + [b"x"] * 5 + [b""] * 9000, 0, 2)))
     # v1 record headers cut at every length, and a wrong magic in the middle
     v1 = legacy_file([b"abc" * k for k in range(40)], 0, 1)
     for cut in (1, 4, 12, 19, 20):
