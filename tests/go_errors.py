@@ -20,13 +20,17 @@ _HEADER = {
 }
 
 
-def expect_read_next_at(status: int, offset: int, path: str, d0: int = 0, d1: int = 0):
-    """(message, sentinel or None, wraps above the sentinel) of MMapReader.ReadNextAt's error."""
+def expect_read_next_at(status: int, offset: int, path: str, d0: int = 0, d1: int = 0, version: int = 4):
+    """(message, sentinel or None, wraps above the sentinel) of MMapReader.ReadNextAt's error
+    (readNextAtV2 / V1 for version 2 / 1: mmap_reader.go:205-296)."""
     where = f"at offset {offset} in mmap reader for '{path}'"
     if status == L.RIO_EOF:  # mmap_reader.go:150-155: 0 bytes readable -> bare io.EOF
         return "EOF", EOF, 0
-    if status == L.RIO_ERR_INVALID_OFFSET:  # :156-158 wraps x/exp/mmap's error
-        return f"ReadNextAt failed reading {where}: mmap: invalid ReadAt offset {offset}", None, 1
+    if status == L.RIO_ERR_INVALID_OFFSET:  # :156-158 wraps x/exp/mmap's error (v1 / v2: :211, :256)
+        pre = "ReadNextAt failed reading" if version >= 3 else "failed reading"
+        return f"{pre} {where}: mmap: invalid ReadAt offset {offset}", None, 1
+    if status == L.RIO_EOF_HEADER and version == 1:  # :209-212: the 20-byte ReadAt ran short
+        return f"failed reading {where}: EOF", EOF, 1
     if status == L.RIO_ERR_HEADER_CRC:  # common_reader.go:145-147 wraps the sentinel once more
         inner = f"header checksum mismatch: expected [{d0:x}], but found [{d1:x}]"
         return f"failed reading record header {where}: {inner}", HeaderChecksumMismatchErr, 2
@@ -42,14 +46,14 @@ def expect_read_next_at(status: int, offset: int, path: str, d0: int = 0, d1: in
     raise AssertionError(f"status {status} is not a ReadNextAt error")
 
 
-def expect_seek_next(status: int, offset: int, trial: int, path: str):
+def expect_seek_next(status: int, offset: int, trial: int, path: str, version: int = 4):
     """SeekNext's error (mmap_reader.go:58-128): io.EOF and x/exp/mmap's ReadAt error come back
     unwrapped; anything else is the failing trial ReadNextAt's error at the trial offset."""
     if status == L.RIO_EOF:
         return "EOF", EOF, 0
     if status == L.RIO_ERR_INVALID_OFFSET:  # :70-83: ReadAt's own error, returned as is
         return f"mmap: invalid ReadAt offset {offset}", None, 0
-    return expect_read_next_at(status, trial, path)
+    return expect_read_next_at(status, trial, path, version=version)
 
 
 def wraps_above(err, sentinel) -> int:

@@ -130,7 +130,9 @@ def _offsets(img, k=150):
 @pytest.mark.parametrize("name", ["mixed_c0", "mixed_c2", "v3_mixed_snappy", "nil_snappy", "mixed_c2_trunc3",
                                   "mixed_c2_flip", "damaged_small_c0", "damaged_small_c2", "header_too_long",
                                   "size_overflow", "snappy_corrupt_mid", "huge_u", "snappy_short_mid",
-                                  "snappy_bad_preamble_mid"])
+                                  "snappy_bad_preamble_mid", "v2_mixed_c2", "v2_mixed_c0_trunc1", "v2_embedded",
+                                  "v2_empty_records", "v1_mixed_c2", "v1_mixed_c0_trunc2", "v1_torn_header_12",
+                                  "v1_bad_magic_mid", "v1_huge_u"])
 def test_read_next_at_every_record_start_and_random_offsets(name, tmp_path):
     """ReadNextAt at record starts and at random offsets: the record, or exactly the oracle's status
     class (and CRC details), and through the mirror the reference's error value (message, sentinel,
@@ -149,7 +151,7 @@ def test_read_next_at_every_record_start_and_random_offsets(name, tmp_path):
             continue
         got, err = r.ReadNextAt(off)
         if isinstance(rec, orc.BadRecord):  # mmap_reader.go:186-191: the codec error, wrapped once
-            assert_go_error(err, expect_read_next_at(STATUS["DECOMPRESS"], off, str(p)))
+            assert_go_error(err, expect_read_next_at(STATUS["DECOMPRESS"], off, str(p), version=img[0]))
             continue
         assert err is None and got == rec, off
     n_fail = 0
@@ -165,13 +167,14 @@ def test_read_next_at_every_record_start_and_random_offsets(name, tmp_path):
         if st == STATUS["HEADER_CRC"]:
             assert (g0, g1) == (d0, d1), off
         assert got is None
-        assert_go_error(err, expect_read_next_at(st, off, str(p), d0, d1))
+        assert_go_error(err, expect_read_next_at(st, off, str(p), d0, d1, version=img[0]))
     assert n_fail > 0
     r.Close()
 
 
 @pytest.mark.parametrize("name", ["asc_none", "nil_snappy", "v3_mixed_none", "damaged_small_c0", "damaged_small_c2",
-                                  "snappy_corrupt_mid", "snappy_short_mid", "random_snappy_1k", "text_snappy_64"])
+                                  "snappy_corrupt_mid", "snappy_short_mid", "random_snappy_1k", "text_snappy_64",
+                                  "v2_mixed_c2", "v2_embedded", "v2_empty_records", "v1_mixed_c0"])
 def test_seek_next_matches_oracle_on_every_offset(name, tmp_path):
     """SeekNext from every third offset: the record and its offset, or exactly the oracle's status
     (with the failing trial's offset), and the reference's error value through the mirror."""
@@ -196,7 +199,10 @@ def test_seek_next_matches_oracle_on_every_offset(name, tmp_path):
             if st not in (STATUS["EOF"], STATUS["INVALID_OFFSET"]):
                 assert g_ro == ro, (off, seek_len)  # the failing trial
             assert (g_off, got) == (0, None)
-            assert_go_error(err, expect_seek_next(st, off, ro, str(p)))
+            if st == STATUS["UNSUPPORTED"]:  # v1: mmap_reader.go:62-64, before any scan
+                assert str(err) == "unsupported on files with version lower than v2"
+                continue
+            assert_go_error(err, expect_seek_next(st, off, ro, str(p), version=img[0]))
     r.Close()
 
 

@@ -115,7 +115,7 @@ GZ = {n: img for n, img, _ in corpus.gzip_cases()}
 
 
 @pytest.mark.parametrize("name", ["gz_text_small", "gz_mixed_nil_empty", "gz_empty_payload", "gz_bad_crc",
-                                  "gz_header_fields", "gz_v3", "gz_large"])
+                                  "gz_header_fields", "gz_v3", "gz_large", "gz_v2", "gz_v1"])
 def test_gzip_read_next_at_and_seek_next(name, tmp_path):
     """gzip files through ReadAtI: every record start, offsets inside records, SeekNext from a
     sample of offsets; the oracle's status class and record, and the reference's error value."""
@@ -132,13 +132,16 @@ def test_gzip_read_next_at_and_seek_next(name, tmp_path):
         assert (rc, got) == (st, want), (name, off)
         if st:
             _, err = r.ReadNextAt(off)
-            assert_go_error(err, expect_read_next_at(st, off, path, d0, d1))
+            assert_go_error(err, expect_read_next_at(st, off, path, d0, d1, version=img[0]))
     for off in offs[::3]:
         st, ro, want = orc.seek_next(img, off)
         assert _call_seek(r, off) == (st, ro if st == 0 else None, want), (name, off)
-        if st:
+        if st == L.RIO_ERR_UNSUPPORTED:  # v1 (mmap_reader.go:62-64)
             _, _, err = r.SeekNext(off)
-            assert_go_error(err, expect_seek_next(st, off, ro, path))
+            assert str(err) == "unsupported on files with version lower than v2"
+        elif st:
+            _, _, err = r.SeekNext(off)
+            assert_go_error(err, expect_seek_next(st, off, ro, path, version=img[0]))
     r.Close()
 
 
