@@ -123,3 +123,41 @@ def test_sstable_damage(tmp_path, seed):
     n = len(o["entries"])
     assert got == [(e[0], v) for e, v in zip(o["entries"], o["values"])][:len(got)]
     assert len(got) == min(n, len(o["values"]))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_older_versions_damage(seed, tmp_path):
+    """Whole-file decode of damaged v3 / v2 / v1 files (random bytes, 0x91 runs, zeros, truncation;
+    the damage lands in headers and payloads alike): device == the oracle's ReadNext loop, and
+    ReadNextAt / SeekNext at a sample of offsets == the oracle's."""
+    import corpus
+    from gpu_util import assert_same_as_oracle, gpu_decode_arrays
+
+    rng = random.Random(500 + seed)
+    version = (3, 2, 1)[seed % 3]
+    comp = rng.choice([0, 2])
+    recs = [r if r is not None else b"" for r in mixed_records(rng.randint(20, 400), 900 + seed, max_len=900)]
+    img = corpus.legacy_file(recs, comp, version) if version < 3 else corpus.to_version(encode_file(recs, comp), 3)
+    for _ in range(rng.randint(1, 3)):
+        img = damage(rng, img)
+    assert_same_as_oracle(gpu_decode_arrays(img), orc.file_reader_decode_arrays(img), f"v{version} seed {seed}")
+    from recordio import NewMemoryMappedReaderWithPath
+
+    p = tmp_path / "f"
+    p.write_bytes(img)
+    r, _ = NewMemoryMappedReaderWithPath(str(p))
+    assert r.Open() is None or len(img) < 8 or img[0] not in (1, 2, 3)
+    if r.header is None:
+        return
+    for off in [rng.randrange(len(img) + 2) for _ in range(40)]:
+        st, want = orc.read_next_at(img, off)
+        got, err = r.ReadNextAt(off)
+        assert (err is None) == (st == 0), (off, st, err)
+        if st == 0:
+            assert got == want, off
+        st, ro, want = orc.seek_next(img, off)
+        g_off, got, err = r.SeekNext(off)
+        assert (err is None) == (st == 0), (off, st, err)
+        if st == 0:
+            assert (g_off, got) == (ro, want), off
+    r.Close()
