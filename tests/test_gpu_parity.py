@@ -80,7 +80,8 @@ def test_chunk_size_independent(chunk, fused, monkeypatch):
     try:
         dec = DeviceDecoder.__new__(DeviceDecoder)
         dec.device, dec.ctx = 0, h.value
-        for name in ("mixed_c2", "mixed_c0_embedded", "text_snappy_64k", "mixed_c2_flip"):
+        for name in ("mixed_c2", "mixed_c0_embedded", "text_snappy_64k", "mixed_c2_flip", "v2_embedded", "v2_empty_records",
+                     "v1_mixed_c2", "v1_torn_header_12"):
             img = dict(CASES)[name]
             o = orc.file_reader_decode_arrays(img)
             d_file, n = to_device_file(img)
