@@ -45,8 +45,10 @@ constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 #define RIO_CHUNKS_PER_WAVE 8
 #endif
 // copies reaching further back than kFarOff read the output arena (flushed: see snappy_lane); the
-// flush is pipelined one step (+16 bytes of lag)
-constexpr uint32_t kFarOff = 16 * (kD - 1) + 16 + 128 + 16;
+// flush is pipelined one step (+16 bytes of lag). Anything from that bound (208) up to what the
+// history ring still holds (233, static_assert below) is correct; 232 turns the copies of offset
+// 209-232 into ring copies (A/B on MI355X, two rounds: C2 decode -0.6/-0.9 %, C4 -0.7/-0.9 %, C3 equal)
+constexpr uint32_t kFarOff = 232;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
 static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128 + 16, "far history must be flushed before the parser reads it");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
