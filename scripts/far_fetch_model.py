@@ -5,7 +5,7 @@ Snappy element and counts, for the copies the lane decoder reads from the output
 kFarOff = 208), the 64-byte and 128-byte lines its 16-byte far loads touch (one load per piece of
 <= 16 bytes, at the 4-aligned source). The result, in fetched bytes per decoded byte, is what the
 PMC FETCH_SIZE counts on top of the input stream when no far line survives in L2 between uses.
-    python scripts/far_fetch_model.py [records] [record_len]
+    python scripts/far_fetch_model.py [records] [record_len] [far threshold, default 232]
 """
 import sys
 
@@ -14,7 +14,7 @@ import numpy as np
 sys.path.insert(0, __file__.rsplit("/", 2)[0] + "/go-sstables_amd")
 from recordio.writer import generate  # noqa: E402
 
-K_FAR = 208
+K_FAR = int(sys.argv[3]) if len(sys.argv) > 3 else 232  # kFarOff (rio_snappy.hip)
 
 
 def uvarint(b, i):
