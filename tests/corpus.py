@@ -268,6 +268,12 @@ def cases():
             out.append((f"v{ver}_mixed_c{comp}_zero_tail", lg + bytes(5000)))
             out.append((f"v{ver}_mixed_c{comp}_garbage_tail", lg + bytes(300) + b"\x01" + bytes(7)))
         out.append((f"v{ver}_embedded", legacy_file(embedded_file_records(40, 9), 0, ver)))
+        # payloads that are themselves files of the same version: candidate headers with this version's
+        # marker bytes inside every chunk (the speculative walk has to repair)
+        rng2 = random.Random(30 + ver)
+        inner = legacy_file([bytes([rng2.getrandbits(8)]) * rng2.randint(1, 40) for _ in range(600)], 0, ver)[8:]
+        out.append((f"v{ver}_embedded_same", legacy_file([inner if i % 2 == 0 else b"y" * rng2.randint(0, 50)
+                                                          for i in range(40)], 0, ver)))
         out.append((f"v{ver}_text_snappy_1k", legacy_file(
             [bytes(r) for r in text_records(3000, 30 + ver, 900, 1100)], 2, ver)))
     # v2's smallest record (5 bytes: magic, u = 0, c = 0): more records start in a 32 KiB chunk than

@@ -59,6 +59,11 @@ def test_repairs_happen_and_stay_exact():
     g = gpu_decode_arrays(img)
     assert g["n_repairs"] > 0
     assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), "embedded")
+    for name in ("v2_embedded_same", "v1_embedded_same"):  # the older layouts' own marker bytes
+        img = dict(CASES)[name]
+        g = gpu_decode_arrays(img)
+        assert g["n_repairs"] > 0, name
+        assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), name)
 
 
 @pytest.mark.parametrize("fused", [1, 0])
