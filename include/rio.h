@@ -1,5 +1,5 @@
 /*
- * rio.h — C-ABI of the MI355X-native recordio v3/v4 decode path.
+ * rio.h — C-ABI of the MI355X-native recordio decode path (v3/v4, and the legacy v1/v2 layouts).
  *
  * This is the drop-in boundary a Go `recordio` adapter (behind `//go:build cgo && rocm`) binds
  * with cgo; see INTEGRATION.md for the binding. Plain pointers and sizes only, no torch/HIP types
@@ -12,12 +12,18 @@
  *   NewFileReaderWithPath / NewFileReader                         recordio/file_reader.go:490-524
  *   NewMemoryMappedReaderWithPath                                 recordio/mmap_reader.go:364-371
  *   FileReader.ReadNext v4 / v3 (sequential whole-file semantics) recordio/file_reader.go:61-131, 389-447
+ *     readNextV2 / readNextV1                                     recordio/file_reader.go:322-388, 282-320
  *   MMapReader.ReadNextAt v4 / v3                                 recordio/mmap_reader.go:130-203, 298-356
+ *     readNextAtV2 / readNextAtV1                                 recordio/mmap_reader.go:242-296, 205-240
  *   MMapReader.SeekNext                                           recordio/mmap_reader.go:58-128
  *   readFileHeaderFromBuffer                                      recordio/common_reader.go:22-44
+ *   readRecordHeaderV1 / V2                                       recordio/common_reader.go:46-81
  *   readRecordHeaderV3 / V4 + checksumByteReader                  recordio/common_reader.go:83-151,
  *                                                                 recordio/checksum_byte_reader.go:11-60
  *   SnappyCompressor.DecompressWithBuf (golang/snappy v1.0.0)     recordio/compressor/snappy_compression.go:22-24
+ *   NewSSTableReader load / validateDataFile / Scan (rio_sst_*)   sstables/sstable_reader.go:250-345, 205-238, 119-159
+ *   DiskKeyIndex binarySearch (rio_index_*)                       sstables/disk_key_index.go:87-140
+ *   wal.Replayer.Replay (rio_replay_*)                            wal/replayer.go:18-77
  *   FileWriter.Write + fillRecordHeaderV4 (input generator only)  recordio/file_writer.go:160-233
  */
 #ifndef RIO_H
