@@ -132,10 +132,8 @@ def cpu_baseline(images, rec_offs=None, n_records=None, budget_s: float = 20.0) 
     """The oracle (oracle/rio_oracle.c, a C restatement of the reference reader) on host cores, timed
     on a bounded sample of the same workload:
       one core  — FileReader.ReadNext loop over one file (orc_file_reader_decode), sequential;
-      all cores — one file: MMapReader.ReadNextAt record-parallel over its known offset table
-                  (orc_parallel_read_at); several files: file-sharded, one whole-file loop per thread."""
-    import threading
-
+      all cores — MMapReader.ReadNextAt record-parallel over each file's known offset table
+                  (orc_parallel_read_at), the files one after another."""
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import oracle_py as orc
 
@@ -159,32 +157,24 @@ def cpu_baseline(images, rec_offs=None, n_records=None, budget_s: float = 20.0) 
             raise RuntimeError("oracle baseline decoded a different record count")
     one = image.shape[0] / 2**30 * runs / t_total
     cores = host_cores()
-    if len(images) > 1:  # file-sharded over the cores
-        t0 = time.perf_counter()
-        th = [threading.Thread(target=one_file, args=(img,)) for img in images[:cores]]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        dt = time.perf_counter() - t0
-        all_v = sum(img.shape[0] for img in images[:cores]) / 2**30 / dt
-        used = min(cores, len(images))
-        how = f"{used} files decoded concurrently, one thread each (file-sharded)"
-    else:
-        import numpy as np
+    import numpy as np
 
-        ro = np.ascontiguousarray(rec_offs, dtype=np.uint64)
-        runs_a, t_a = 0, 0.0
-        while runs_a < 5 and t_a < budget_s:
-            t0 = time.perf_counter()
-            got = lib.orc_parallel_read_at(image.ctypes.data, image.shape[0], ro.ctypes.data, ro.shape[0], cores)
-            t_a += time.perf_counter() - t0
-            runs_a += 1
-            if not got:
+    # all cores: MMapReader.ReadNextAt record-parallel over every file's known offset table, the files
+    # one after another, so a set of fewer files than cores (C4: 8 files, 16 cores) still uses the
+    # whole CPU share (one thread per file left half of it idle)
+    offs = [np.ascontiguousarray(ro, dtype=np.uint64) for ro in (rec_offs if len(images) > 1 else [rec_offs])]
+    runs_a, t_a = 0, 0.0
+    while runs_a < 5 and t_a < budget_s:
+        t0 = time.perf_counter()
+        for img, ro in zip(images, offs):
+            if not lib.orc_parallel_read_at(img.ctypes.data, img.shape[0], ro.ctypes.data, ro.shape[0], cores):
                 raise RuntimeError("oracle parallel ReadNextAt failed")
-        all_v = image.shape[0] / 2**30 * runs_a / t_a
-        used = cores
-        how = f"ReadNextAt over the {ro.shape[0]} known record offsets, {cores} threads, x{runs_a} runs"
+        t_a += time.perf_counter() - t0
+        runs_a += 1
+    all_v = sum(img.shape[0] for img in images) / 2**30 * runs_a / t_a
+    used = cores
+    how = (f"ReadNextAt over the known record offsets of {len(images)} file(s) "
+           f"({sum(o.shape[0] for o in offs)} records), {cores} threads, x{runs_a} runs")
     return {"value": round(all_v, 4), "unit": "GiB/s", "cores": used, "kind": "port",
             "sample": f"{how}; {os.cpu_count()} cpus visible on the host, CPU share {cores}, {_cpu_model()}",
             "one_core": {"value": round(one, 4), "unit": "GiB/s", "cores": 1,
@@ -875,7 +865,12 @@ class DeviceBackend:
         self._evict.fill_(1)
 
     def rec_offs(self, n):
-        return self.bufs[0].rec_off[:n].cpu().numpy()
+        """Record offsets of every loaded file (the CPU baseline's ReadNextAt table)."""
+        out = []
+        for b in self.bufs:
+            k = self.dec.info(b)["n_records"]
+            out.append(b.rec_off[:k].cpu().numpy())
+        return out[0] if len(out) == 1 else out
 
 
 def plan_files(config: str, world: int, rank: int) -> list:
@@ -1025,14 +1020,60 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     if warm:
         line["warm_mall"] = warm
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec_offs = None if batch else backend.rec_offs(n)
-        line["cpu_baseline"] = cpu_baseline(images, rec_offs, n_rec)
+        line["cpu_baseline"] = cpu_baseline(images, backend.rec_offs(n), n_rec)
     if rank == 0 and world == 1 and not args.no_e2e and not batch:
         line["e2e"] = e2e_rate(images[0], nb)
     return line
 
 
-def main():
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_contract(gpus: int, argv: list[str]) -> int | None:
+    """`--gpus N` is authoritative. Runs BEFORE anything touches the GPU:
+      * WORLD_SIZE unset and N > 1: no launcher started us, so start one (torch.distributed.run, one
+        rank per GPU, rendezvous on 127.0.0.1) on this very script and return its exit code — the
+        parent never initialises HIP, so nothing is exec'd from a GPU process;
+      * WORLD_SIZE set and != N: a launcher and the flag disagree; refuse rather than report a job of
+        the wrong size;
+      * otherwise None: run this process as the rank the environment names (N = 1, or under a launcher).
+    """
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if gpus <= 1:
+            return None
+        import subprocess
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(sys.argv[0])] + argv
+        print(f"bench.py: --gpus {gpus} without a launcher: starting {gpus} ranks", file=sys.stderr, flush=True)
+        return subprocess.call(cmd)
+    if int(ws) != gpus:
+        print(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}: refusing to report a {ws}-rank job as {gpus} GPUs",
+              file=sys.stderr, flush=True)
+        return 2
+    return None
+
+
+def make_device(local: int):
+    """This rank's GPU: cuda:LOCAL_RANK."""
+    import torch
+
+    torch.cuda.set_device(local)
+    return torch.device(f"cuda:{local}")
+
+
+def make_backend(local: int, device):
+    """The decode configs' device call (tests/bench_cli_oracle.py substitutes the CPU oracle)."""
+    return DeviceBackend(local, device)
+
+
+def main(argv: list[str] | None = None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -1042,14 +1083,18 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic file (default: profiles/traffic_<config>.json, then traffic_latest.json)")
-    args = ap.parse_args()
+    argv = sys.argv[1:] if argv is None else argv
+    args = ap.parse_args(argv)
+    rc = launch_contract(args.gpus, argv)
+    if rc is not None:
+        sys.exit(rc)
 
     world, rank, local = dist_env()
-    import numpy as np
+    assert world == args.gpus
+    import numpy as np  # noqa: F401
     import torch
 
-    torch.cuda.set_device(local)
-    device = torch.device(f"cuda:{local}")
+    device = make_device(local)
     if world > 1:
         import torch.distributed as dist
 
@@ -1064,7 +1109,7 @@ def main():
             torch.distributed.destroy_process_group()
         return
 
-    line = run_decode(args, world, rank, DeviceBackend(local, device))
+    line = run_decode(args, world, rank, make_backend(local, device))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

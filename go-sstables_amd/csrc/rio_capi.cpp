@@ -1226,10 +1226,18 @@ static int readat_expand(rio_reader* r, uint64_t rec, const ReadAtResult& res, c
     if (rc) return rc;
     if (fi.n_records == 0) return RIO_ERR_UNSUPPORTED;  // (the kernel framed it: not reached)
     const uint64_t n = fi.n_records;
-    tl_x_out.resize(fi.total_out_bytes + 1);
-    tl_x_off.resize(n + 1);
-    tl_x_rec.resize(n);
-    tl_x_flags.resize(n);
+    // the sizes are what the (possibly damaged) headers claim: an lzw u may be 4096x its payload.
+    // Bounded like the index (readat_index_cap), and an allocation failure is a status, never an
+    // exception through the C-ABI
+    if (fi.total_out_bytes > readat_index_cap() || n > readat_index_cap() / 16) return RIO_ERR_CAPACITY;
+    try {
+        tl_x_out.resize(fi.total_out_bytes + 1);
+        tl_x_off.resize(n + 1);
+        tl_x_rec.resize(n);
+        tl_x_flags.resize(n);
+    } catch (const std::exception&) {
+        return RIO_ERR_CAPACITY;
+    }
     rc = rio_decode(r->ctx, tl_x_out.data(), fi.total_out_bytes, tl_x_off.data(), tl_x_rec.data(), tl_x_flags.data(), n,
                     &fi);
     if (rc) return rc;

@@ -4,9 +4,28 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rio.h"
 
 namespace rio {
+
+// Same-type min / max. HIP's global min/max are overloaded for int, unsigned, 64-bit and floating
+// types; a call with mixed operands (say uint32_t and int, or a readfirstlane result) can resolve to
+// the double overload and silently convert (round 3: the parser/emitter hang). Every
+// kernel calls these instead; tests/test_kernel_lint.py rejects a bare min( / max( in csrc/*.hip.
+template <typename A, typename B>
+__host__ __device__ __forceinline__ A umin(A a, B b) {
+    static_assert(std::is_same<A, B>::value, "rio::umin: operands of different types; cast explicitly");
+    static_assert(std::is_integral<A>::value, "rio::umin: integer operands only");
+    return a < b ? a : b;
+}
+template <typename A, typename B>
+__host__ __device__ __forceinline__ A umax(A a, B b) {
+    static_assert(std::is_same<A, B>::value, "rio::umax: operands of different types; cast explicitly");
+    static_assert(std::is_integral<A>::value, "rio::umax: integer operands only");
+    return a > b ? a : b;
+}
 
 // encoding/binary.Uvarint semantics: >0 bytes read, 0 buffer too small, <0 overflow
 __device__ inline int uvarint_buf(const uint8_t* p, uint64_t n, uint64_t& x) {

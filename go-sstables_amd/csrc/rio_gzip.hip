@@ -347,13 +347,13 @@ __device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t 
                 else
                     st_partial(out + q, v, upto - q);
             }
-            flushed = min(upto, flushed + 16 * G);
+            flushed = umin(upto, flushed + 16 * G);
         }
     };
   for (;;) {  // members
     B.refill(lane);
     // ---- member header (gzip reader.go readHeader: io.ReadFull of 10 bytes) ----
-    if (slen - min(slen, (uint32_t)(B.consumed() >> 3)) < 10) return kGzCorrupt;
+    if (slen - umin(slen, (uint32_t)(B.consumed() >> 3)) < 10) return kGzCorrupt;
     const uint32_t id = B.bits(16), cm = B.bits(8), flg = B.bits(8);
     if (id != 0x8B1Fu || cm != 8u) return kGzCorrupt;
     B.refill(lane);
@@ -414,11 +414,11 @@ __device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t 
             const uint32_t ln = B.bits(16), nl = B.bits(16);
             if (B.overrun() || (ln ^ 0xFFFFu) != nl) return kGzCorrupt;
             const uint32_t p0 = p + 4;
-            if (ln > slen - min(slen, p0)) return kGzCorrupt;
+            if (ln > slen - umin(slen, p0)) return kGzCorrupt;
             if (ln > cap - d) return kCount ? kGzUnsupported : kGzResize;
             // 1 KiB at a time, flushing in between: the window never overruns unflushed bytes
             for (uint32_t k0 = 0; k0 < ln; k0 += 1024) {
-                const uint32_t m = min(1024u, ln - k0);
+                const uint32_t m = umin(1024u, ln - k0);
                 for (uint32_t k = gl; k < m; k += G) S.win[(d + k) & (kWin - 1)] = src[p0 + k0 + k];
                 __builtin_amdgcn_wave_barrier();
                 d += m;
@@ -464,7 +464,7 @@ __device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t 
                 // runs of plain code lengths (symbols 0..15) as in the data loop: every offset looked
                 // up at once, the chain followed through the lanes, the lengths stored in one write
                 {
-                    const uint32_t lim = (uint32_t)min((uint64_t)B.nb, (uint64_t)8 * slen - min((uint64_t)8 * slen, (uint64_t)B.consumed()));
+                    const uint32_t lim = (uint32_t)umin((uint64_t)B.nb, (uint64_t)8 * slen - umin((uint64_t)8 * slen, (uint64_t)B.consumed()));
                     const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
                     uint32_t o = 0, cnt = 0, eo = 0, last = prev;
                     uint64_t m = 0;
@@ -555,7 +555,7 @@ __device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t 
             // (Matches decoded from the same lookup as well measured slower: the extra uniform state
             // spills scalar registers inside the loop; C2-gzip 52.1 -> 66.0 ms.)
             {
-                const uint32_t lim = (uint32_t)min((uint64_t)B.nb, (uint64_t)8 * slen - min((uint64_t)8 * slen, (uint64_t)B.consumed()));
+                const uint32_t lim = (uint32_t)umin((uint64_t)B.nb, (uint64_t)8 * slen - umin((uint64_t)8 * slen, (uint64_t)B.consumed()));
                 const uint32_t e = T.lfast[(uint32_t)(B.bb >> lane) & (kFastSize - 1)];
                 uint32_t o = 0, cnt = 0, eo = 0;
                 uint64_t m = 0;
@@ -652,7 +652,7 @@ __device__ int gz_record(GzLds<kWin, kIn, kDB>& S, const uint8_t* src, uint32_t 
         } else {
             // bytes already flushed from the arena, the rest from the window (no extra flush: the
             // flush position stays 1 KiB aligned, so no 16-byte read straddles the window's end)
-            const uint32_t g_end = max(dm, flushed);
+            const uint32_t g_end = umax(dm, flushed);
             uint32_t c = 0xFFFFFFFFu;
             if (g_end > dm) {
                 __threadfence_block();  // the member's stores complete before lane 0 reads them back

@@ -628,8 +628,8 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++)
         m91 |= (((bytes_eq(d[k], 0x91919191u) & 0x80808080u) * 0x00204081u) >> 28) << (4 * k);
-    const uint32_t a = lo > q ? (uint32_t)min(lo - q, (uint64_t)16) : 0u;
-    const uint32_t b = hi > q ? (uint32_t)min(hi - q, (uint64_t)16) : 0u;
+    const uint32_t a = lo > q ? (uint32_t)umin(lo - q, (uint64_t)16) : 0u;
+    const uint32_t b = hi > q ? (uint32_t)umin(hi - q, (uint64_t)16) : 0u;
     m91 &= (b >= 16 ? 0xFFFFu : (1u << b) - 1u) & ~(a >= 16 ? 0xFFFFu : (1u << a) - 1u);
     uint32_t mask = 0;
     while (m91) {
@@ -693,7 +693,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
     while (ws < ce && mode < 2) {
         if (mode == 1) {
             if (p >= ce) break;
-            ws = max(ws, p);  // skip what the chain jumped over
+            ws = umax(ws, p);  // skip what the chain jumped over
         }
         // 1. fill the window [ws, we)
         if (lane == 0) L.overflow = kNone;
@@ -755,9 +755,9 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         }
         wave_sync_lds();
         const uint64_t overflow = L.overflow;
-        const uint64_t we = overflow != kNone ? overflow : min(rd, ce);  // window end
+        const uint64_t we = overflow != kNone ? overflow : umin(rd, ce);  // window end
         // 2. frame one candidate per lane
-        const uint32_t nst = min(total, 64u);
+        const uint32_t nst = umin(total, 64u);
         const bool have = lane < nst;
         const uint64_t cpos = have ? L.pos[lane] : kNone;
         Hdr h;
@@ -1734,7 +1734,8 @@ __global__ void k_seek_next(const uint8_t* f, uint64_t len, uint64_t off, uint64
 // P = every 0x91 position in file order, R[k] = the walk's end from P[k] — a record j of the decoded
 // sequence (its trial is record j, answered from the decoded arena), kSeekEof (the walk passes the
 // last 0x91 and the scan reads to the file end: io.EOF) or kSeekOther (a trial outside the sequence
-// that ends the walk, or a partial marker at the file end: the single-record kernel answers those). Built once per reader:
+// that ends the walk: the single-record kernel answers those; a partial marker at the file end is
+// kSeekEof, as the reference's rewind there returns io.EOF). Built once per reader:
 //   k_count91 / k_scan_segs / k_list91: P (a wave per 4 KiB segment, ballot-free lane prefix);
 //   k_seek_step: each position's own step (terminal, or the index of the next 0x91 visited);
 //   k_seek_jump: pointer jumping to each walk's end (log2 of the longest walk rounds).
@@ -1847,10 +1848,14 @@ __global__ void __launch_bounds__(256) k_seek_step(const uint8_t* f, uint64_t le
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
         const uint64_t p = P[k];
         uint64_t out = kSeekTerm | kSeekOther, c = 0;
-        if (he == RIO_OK && p + 1 < len) {
+        if (he == RIO_OK && (p + 1 >= len || (f[p + 1] == 0x8D && p + 2 >= len))) {
+            // a partial marker at the file end: SeekNext re-reads from it, its window ends inside the
+            // marker with i == 0, and the call returns io.EOF (mmap_reader.go:88-124)
+            out = kSeekTerm | kSeekEof;
+        } else if (he == RIO_OK) {
             if (f[p + 1] != 0x8D) {
                 c = p + 2;
-            } else if (p + 2 < len) {
+            } else {
                 if (f[p + 2] != 0x4C) {
                     c = p + 3;
                 } else {

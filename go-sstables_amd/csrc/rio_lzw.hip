@@ -64,7 +64,7 @@ struct LzLds {
 // 10 for 255..766, 11 for 767..1790, 12 after)
 __device__ __forceinline__ uint32_t lz_width(uint32_t k) { return k < 255 ? 9u : k < 767 ? 10u : k < 1791 ? 11u : 12u; }
 __device__ __forceinline__ uint64_t lz_bits(uint32_t k) {
-    const uint64_t a = min(k, 255u), b = min(k, 767u) - a, c = min(k, 1791u) - a - b, d = (uint64_t)k - a - b - c;
+    const uint64_t a = umin(k, 255u), b = umin(k, 767u) - a, c = umin(k, 1791u) - a - b, d = (uint64_t)k - a - b - c;
     return 9 * a + 10 * b + 11 * c + 12 * d;
 }
 
@@ -109,7 +109,7 @@ __device__ int lz_record(LzLds<kMaxK>& S, const uint8_t* p, uint32_t slen, uint8
             const uint32_t win = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(byte & 3u));  // bytes [byte, byte + 4)
             code = (win >> (bp & 7u)) & ((1u << w) - 1u);
         }
-        const uint32_t hi = min(257u + k, 4095u);
+        const uint32_t hi = umin(257u + k, 4095u);
         const uint32_t kind = !avail ? kMissing : code < 256 ? kLit : code == 256 ? kClear : code == 257 ? kEnd
                               : code <= hi ? kCopy : kBad;
         const uint64_t spec = __ballot(kind >= kClear);

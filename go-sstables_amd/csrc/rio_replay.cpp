@@ -289,7 +289,11 @@ struct rio_replay {
 
 extern "C" int rio_replay_open(int device, const char* const* paths, uint64_t n_paths, uint32_t depth,
                                uint32_t workers, rio_replay** out) {
-    return rio_replay_open_devices(&device, 1, paths, n_paths, depth, workers, out);
+    // rio.h's single-device contract: workers (0 = 2) at most depth (0 = 2), so at most `depth`
+    // decoded files are held (the device-list form raises depth to its worker count instead)
+    const uint32_t d = depth ? depth : 2u;
+    const uint32_t w = std::min<uint32_t>(workers ? workers : 2u, d);
+    return rio_replay_open_devices(&device, 1, paths, n_paths, d, w, out);
 }
 
 // Workers are dealt to the devices round-robin (worker w on devices[w % n_devices]), each with a

@@ -526,9 +526,9 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     const uint64_t start0 = ((uint64_t)d0.y << 32) | d0.x;
     const uint64_t base = start0 & ~15ull;
     const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
-    const uint32_t lastc = live && base < P.len ? (uint32_t)min((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
+    const uint32_t lastc = live && base < P.len ? (uint32_t)umin((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
     // prime the input image with chunks [0, 4)
-    uint32_t whi = live ? min(kInCh, lastc + 1) : 0u;
+    uint32_t whi = live ? umin(kInCh, lastc + 1) : 0u;
     for (uint32_t c = 0; c < whi; c++) {
         const uint4 v = sa[c];
         const uint32_t a = wl | (c << 12);
@@ -647,7 +647,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t W0 = __builtin_amdgcn_alignbyte(Wb, Wa, pos);  // bytes s .. s + 3
             const uint32_t W1 = __builtin_amdgcn_alignbyte(Wb >> ((pos << 3) & 31u), W0, 1u);  // s + 1 .. s + 4
             const uint32_t tag = W0 & 0xFFu, t = tag & 3u, x = tag >> 2;
-            const bool avail = min((pos + 15) >> 4, lastc) < whi;
+            const bool avail = umin((pos + 15) >> 4, lastc) < whi;
             const bool is0 = t == 0, is1 = t == 1;
             const bool is2 = t == 2;
             const bool lng = x >= 60;
@@ -680,8 +680,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             // destination-aligned pieces: at most 16 - r bytes (r = pd & 3); a literal's bytes also
             // stay inside the window [s, s + 16) the availability check covers
             const uint32_t r = pd & 3u;
-            const uint32_t cap = 16u - max(lit1 ? sh : 0u, r);
-            const uint32_t n = go ? min(rem1, lit1 ? cap : min(cap, eff1)) : 0u;
+            const uint32_t cap = 16u - umax(lit1 ? sh : 0u, r);
+            const uint32_t n = go ? umin(rem1, lit1 ? cap : umin(cap, eff1)) : 0u;
             S.n = n;
             S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
             qsrc = pd - eff1;
@@ -835,7 +835,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
     uint64_t chunk = g;
     while (chunk < nchunks) {
-        const uint64_t r0 = min(chunk * per + lane * rpc, n), r1 = min(r0 + rpc, n);
+        const uint64_t r0 = umin(chunk * per + lane * rpc, n), r1 = umin(r0 + rpc, n);
         uint64_t bad_rec = 0;
         if (!snappy_lane(P, r0, r1, lds, wave, lane, sink, &bad_rec)) {
             const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
@@ -875,7 +875,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
         const uint64_t n = P.state->n_records, wf = (n + per_wave - 1) / per_wave;
         if (wg < w0 + wf) {
             const uint64_t t = ((wg - w0) << 6) | lane;
-            const uint64_t r0 = min(t * rpl, n), r1 = min(r0 + rpl, n);
+            const uint64_t r0 = umin(t * rpl, n), r1 = umin(r0 + rpl, n);
             uint8_t* sink = P.sink + wg * 64;
             uint64_t bad_rec = 0;
             if (!snappy_lane(P, r0, r1, lds, wave, lane, sink, &bad_rec)) {

@@ -36,11 +36,15 @@ class IndexVal:
         return f"IndexVal(Offset={self.Offset}, Checksum={self.Checksum})"
 
 
-def _error(status: int) -> GoError:
+def _error(status: int, version: int = 0) -> GoError:
     if status == L.RIO_ERR_PROTO:
         return GoError("proto: cannot parse invalid wire-format data")
-    if status == L.RIO_ERR_UNSUPPORTED:  # a v1 index: every probe's SeekNext fails (mmap_reader.go:62-64)
-        return GoError("unsupported on files with version lower than v2")
+    if status == L.RIO_ERR_UNSUPPORTED:
+        if version < 2:  # a v1 index: every probe's SeekNext fails (mmap_reader.go:62-64)
+            return GoError("unsupported on files with version lower than v2")
+        # v2+ compressed index: a probe whose SeekNext walk ends at a trial outside the decoded
+        # sequence is handed back by the device search
+        return GoError("rio: SeekNext probe ends outside the decoded record sequence (unsupported on the device)")
     from recordio.reader import _base_error
 
     return _base_error(status)
@@ -52,6 +56,7 @@ class DiskKeyIndex:
         self.device = device
         self._h = None
         self._reader = None
+        self.version = 0
 
     def Open(self):  # noqa: N802
         with open(self.path, "rb") as fh:
@@ -61,6 +66,8 @@ class DiskKeyIndex:
         if rc:
             return GoError(f"error while loading index '{self.path}' to the device: {L.strerror(rc)}")
         self._h, self.size = h, len(img)
+        # recordio file version (common_reader.go:22-44: LE u32 at offset 0)
+        self.version = int.from_bytes(img[:4], "little") if len(img) >= 4 else 0
         self._reader, err = NewMemoryMappedReaderWithPath(self.path, self.device)
         if err is not None:
             return err
@@ -97,7 +104,7 @@ class DiskKeyIndex:
         out = []
         for off, found, vo, cs, st in self.search(keys):
             if st:
-                out.append((IndexVal(), _error(st)))
+                out.append((IndexVal(), _error(st, self.version)))
             elif not found:
                 out.append((IndexVal(), NotFound))
             else:
@@ -109,7 +116,7 @@ class DiskKeyIndex:
 
     def Contains(self, key):  # noqa: N802
         off, found, _, _, st = self.search([key])[0]
-        return (False, _error(st)) if st else (found, None)
+        return (False, _error(st, self.version)) if st else (found, None)
 
     def Iterator(self):  # noqa: N802
         return _DiskKeyIndexIterator(self._reader, 8, self.size), None
@@ -117,7 +124,7 @@ class DiskKeyIndex:
     def IteratorStartingAt(self, key):  # noqa: N802
         off, _, _, _, st = self.search([key])[0]
         if st:
-            return None, _error(st)
+            return None, _error(st, self.version)
         return _DiskKeyIndexIterator(self._reader, off, self.size), None
 
     def IteratorBetween(self, lo, hi):  # noqa: N802
@@ -125,7 +132,7 @@ class DiskKeyIndex:
             return None, GoError("keyHigher is lower than keyLower")
         (s, _, _, _, st1), (e, found, _, _, st2) = self.search([lo, hi])
         if st1 or st2:
-            return None, _error(st1 or st2)
+            return None, _error(st1 or st2, self.version)
         if not found:
             e -= 1  # keyHigher is inclusive
         return _DiskKeyIndexIterator(self._reader, s, e), None

@@ -369,7 +369,8 @@ int rio_replay_open(int device, const char* const* paths, uint64_t n_paths, uint
 /* The same over several GPUs of one node (one host thread + context per GPU, no
  * communication): workers_per_device workers per device, worker w on devices[w % n_devices], file i
  * to worker i % W; files are still handed out strictly in list order. A device may be listed twice
- * (two workers' contexts on one GPU). */
+ * (two workers' contexts on one GPU). depth (0 = 2) is raised to the worker count
+ * workers_per_device * n_devices (0 = 2 per device), so every worker has a file in flight. */
 int rio_replay_open_devices(const int* devices, uint32_t n_devices, const char* const* paths, uint64_t n_paths,
                             uint32_t depth, uint32_t workers_per_device, rio_replay** out);
 int rio_replay_next(rio_replay* r, uint64_t* index, const uint8_t** out, const uint64_t** out_off,

@@ -229,6 +229,27 @@ def test_compressed_index_through_the_decoded_view(comp):
         assert sum(g[2] for g in got[:len(keys)]) > len(keys) // 2
 
 
+@pytest.mark.parametrize("comp", [1, 2, 3])
+@pytest.mark.parametrize("tail", [b"\x91", b"\x91\x8d"])
+def test_compressed_index_ending_in_a_partial_marker(comp, tail):
+    """A compressed index.rio whose last bytes are a cut marker (0x91, or 91 8d): SeekNext from a probe
+    past the last record rewinds onto it and returns io.EOF (mmap_reader.go:88-124), so binarySearch
+    reports "not found" at the end; the decoded view's SeekNext map must say the same,
+    not hand the query back. Hits equal the oracle's binarySearch over the same bytes."""
+    rng = random.Random(90 + comp)
+    keys = sorted({bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 30))) for _ in range(300)})
+    idx = bytes(index_image(entries_for(keys), comp)) + tail
+    qs = queries_for(keys, rng, 60) + [b"\xff" * 41, keys[-1] + b"\x00"]
+    got = handle_hits(idx, qs)
+    for q, g in zip(qs, got):
+        o = orc.disk_index_search(idx, q, 4096)
+        if o[0] != 0:
+            assert g[0] == o[0], (comp, q, g, o)
+        else:
+            assert g == o, (comp, q, g, o)
+    assert all(g[0] != L.RIO_ERR_UNSUPPORTED for g in got)
+
+
 @pytest.mark.parametrize("version", [3, 2, 1])
 def test_older_version_indexes_match_oracle(version):
     """index.rio with the v3 / v2 / v1 header layouts: SeekNext-driven binarySearch on v3 / v2 as on v4;

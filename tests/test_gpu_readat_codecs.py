@@ -128,3 +128,35 @@ def test_empty_gzip_payload_past_the_break_continues_the_seek(tmp_path):
         st, ro, want = orc.seek_next(img, off, 4096)
         assert _seek_next(r._h, off) == (st, ro, want), k
     r.Close()
+
+
+def test_huge_claimed_lzw_record_past_the_break_is_a_status(tmp_path):
+    """An lzw record after a broken header whose u claims 4.6 GB (lzw allows 4096x its payload): the
+    expansion is sized from that claim, so it is capped like the ReadAtI index and answered with
+    RIO_ERR_CAPACITY, never an exception through the C-ABI (readat_expand)."""
+    import random
+
+    from recordio import NewMemoryMappedReaderWithPath
+    from recordio import _lib as L
+
+    recs = _records(3, 80)
+    items = [(len(r), orc.lzw_encode(r)) for r in recs]
+    rng = random.Random(81)
+    junk = bytes(rng.getrandbits(8) for _ in range(1_200_000))
+    items.append((4_600_000_000, junk))
+    img = corpus.lzw_file(items)
+    # record offsets from the same file with a 2-byte payload in the last record (the oracle would
+    # reserve the claimed 4.6 GB); records 0..3 start at the same offsets
+    o = orc.file_reader_decode(corpus.lzw_file(items[:3] + [(4_600_000_000, b"ab")]))
+    b = bytearray(img)
+    b[int(o["rec_off"][1]) + 3] ^= 0x02  # FileReader stops at record 1
+    img = bytes(b)
+    p = tmp_path / "f.rio"
+    p.write_bytes(img)
+    r, err = NewMemoryMappedReaderWithPath(str(p))
+    assert err is None and r.Open() is None
+    rc, got = _read_next_at(r._h, int(o["rec_off"][3]))
+    assert rc == L.RIO_ERR_CAPACITY and got is None
+    rc, got = _read_next_at(r._h, int(o["rec_off"][2]))  # an ordinary record past the break still reads
+    assert rc == 0 and got == recs[2]
+    r.Close()

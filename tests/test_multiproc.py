@@ -153,3 +153,39 @@ def test_bench_run_decode_world2(config, files_per_rank):
         assert line["n_gpus"] == 2 and line["config"]["files_this_rank"] == files_per_rank
         assert line["config"]["records"] == 150 * files_per_rank
     assert got[0][2]["value"] == got[1][2]["value"] > 0
+
+
+def _bench_cli(args, env_extra=None, timeout=300):
+    import subprocess
+
+    env = dict(os.environ, RIO_BENCH_TEST_SIZES="150,2048", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "tests", "bench_cli_oracle.py")] + args,
+                          env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("config,files_per_rank", [("c4", 4), ("c2", 1)])
+def test_bench_gpus2_without_launcher_self_launches(config, files_per_rank):
+    """`bench.py --gpus 2` started bare (the way the driver starts `--gpus 1`) runs 2 ranks, not a silent
+    1-rank job: the line reports n_gpus 2, each rank its own share of the files (C4: 4 of the 8)."""
+    import json
+
+    r = _bench_cli(["--gpus", "2", "--config", config, "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                    "--no-e2e", "--traffic-json", "/nonexistent"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints the one line
+    line = lines[0]
+    assert line["n_gpus"] == 2
+    assert line["config"]["files_this_rank"] == files_per_rank
+    assert line["config"]["records"] == 150 * files_per_rank
+    assert line["value"] > 0
+
+
+def test_bench_world_size_mismatch_refused():
+    """A launcher's WORLD_SIZE that disagrees with --gpus is refused (non-zero exit), not reported."""
+    r = _bench_cli(["--gpus", "4", "--steps", "1", "--warmup", "0"],
+                   env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
