@@ -452,7 +452,13 @@ __device__ __forceinline__ void coop_file(const FrameParams& P, CoopLds& S, uint
 // decode C2 1.19 -> 1.13 ms, C3 0.86 -> 0.80, C4 13.9 -> 13.6 (gpurun_out/r3k).
 // ------------------------------------------------------------------------------------------
 namespace {
-constexpr uint32_t kColRows = 64;                  // history rows per lane: 256 bytes
+// RIO_EXP_OCC (timing-only experiment, WRONG output): a 32-row history ring, so three 4-wave
+// workgroups fit a CU (12 waves) with the same instruction stream: the upper bound of what a third
+// wave per SIMD buys
+#ifndef RIO_EXP_OCC
+#define RIO_EXP_OCC 0
+#endif
+constexpr uint32_t kColRows = RIO_EXP_OCC ? 32 : 64;  // history rows per lane: 256 bytes
 constexpr uint32_t kColInRows = 16;                // input rows per lane: 64 bytes = kInCh chunks
 constexpr uint32_t kColWaves = kSnappyBlock / 64;
 constexpr uint32_t kColRow = kColWaves * 256;      // bytes per row of the four waves (1 KiB)
@@ -460,12 +466,12 @@ constexpr uint32_t kColH = kColRows * kColRow;     // history image (64 KiB: 16-
 constexpr uint32_t kColI = kColInRows * kColRow;   // input image (16 KiB)
 constexpr uint32_t kColLds = kColH + kColI;
 constexpr uint32_t kCoopSlice = kColH / kColWaves; // a wave's contiguous slice for the wave decoder
-static_assert(kColH == 65536, "history addresses wrap at 16 bits");
+static_assert(RIO_EXP_OCC || kColH == 65536, "history addresses wrap at 16 bits");
 static_assert(kColInRows == 4 * kInCh, "input image holds the input ring's chunks");
 static_assert(sizeof(CoopLds) <= kCoopSlice, "wave decoder LDS must fit a history slice");
 // live history: ring-copy sources reach kFarOff + 3 bytes below the destination, the emit writes
 // the 16 bytes from d - r; the flush reads complete blocks at most 127 bytes below d
-static_assert(kFarOff + 3 + 16 + 4 <= kColRows * 4, "history image must hold the copy reach");
+static_assert(RIO_EXP_OCC || kFarOff + 3 + 16 + 4 <= kColRows * 4, "history image must hold the copy reach");
 
 struct ColSlot {
     uint4 in;        // input chunk in_c (load in flight)
@@ -508,6 +514,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     auto hrow = [&](uint32_t b) __attribute__((always_inline)) { return ((b << 8) & (kColH - kColRow)) | wl; };
     // v_pk_add_u16: the low half wraps at 64 KiB, the high half (0) stays 0
     auto hnext = [&](uint32_t a) __attribute__((always_inline)) {
+        if (RIO_EXP_OCC) return (a + kColRow) & (kColH - 1u);
         const u16x2 v = __builtin_bit_cast(u16x2, a) + u16x2{(uint16_t)kColRow, 0};
         return __builtin_bit_cast(uint32_t, v);
     };

@@ -10,7 +10,8 @@
 constexpr uint64_t kRec = 1024;
 constexpr uint64_t kRecs = 1u << 20;  // 1 GiB
 
-// shape 0: lane streams, 1: quad streams, 2: coalesced
+// shape 0: lane streams, 1: quad streams, 2: coalesced, 3: pair streams (2 lanes x 16 B = 32 contiguous
+// bytes of 32 records per instruction), 4: octet streams (8 lanes x 16 B = 128 B of 8 records)
 template <int kShape, bool kStore>
 __global__ void __launch_bounds__(256) k_mem(uint4* buf, uint4* sink) {
     const uint32_t lane = threadIdx.x & 63;
@@ -27,6 +28,12 @@ __global__ void __launch_bounds__(256) k_mem(uint4* buf, uint4* sink) {
             } else if (kShape == 1) {
                 const uint32_t rec = (j & 3) * 16 + (lane >> 2), ch = (j >> 2) * 4 + (lane & 3);
                 idx = (r0 + rec) * (kRec / 16) + ch;  // 16 records x 64 B per instruction
+            } else if (kShape == 3) {
+                const uint32_t rec = (j & 1) * 32 + (lane >> 1), ch = (j >> 1) * 2 + (lane & 1);
+                idx = (r0 + rec) * (kRec / 16) + ch;  // 32 records x 32 B per instruction
+            } else if (kShape == 4) {
+                const uint32_t rec = (j & 7) * 8 + (lane >> 3), ch = (j >> 3) * 8 + (lane & 7);
+                idx = (r0 + rec) * (kRec / 16) + ch;  // 8 records x 128 B per instruction
             } else {
                 idx = r0 * (kRec / 16) + (uint64_t)j * 64 + lane;  // 1 KiB contiguous
             }
@@ -71,5 +78,8 @@ int main() {
     run<0, true>("store lane streams (64 rec)", buf, sink);
     run<1, true>("store quad streams (16 rec)", buf, sink);
     run<2, true>("store coalesced", buf, sink);
+    run<3, true>("store pair streams (32 rec)", buf, sink);
+    run<4, true>("store octet streams (8 rec)", buf, sink);
+    run<3, false>("load  pair streams (32 rec)", buf, sink);
     return 0;
 }
