@@ -19,12 +19,16 @@ constexpr uint32_t kFailLanes = 1024;
 // Snappy decode launch shape (k_snappy_pipe): every wave owns one 64-byte sink line that absorbs
 // the pipeline's placeholder loads and stores.
 constexpr unsigned kSnappyBlock = 256;
-// RIO_SNAPPY_GRID: experiment builds only (make variant VDEFS=-DRIO_SNAPPY_GRID=256); the sink is sized for 512
+// RIO_SNAPPY_GRID: the launch grid (experiment builds: make variant VDEFS=-DRIO_SNAPPY_GRID=768); the
+// sink is sized for up to kSnappyGridMax workgroups whatever the variant, so a build that changes the
+// grid in rio_snappy.hip alone stays inside the context's sink
 #ifndef RIO_SNAPPY_GRID
 #define RIO_SNAPPY_GRID 512
 #endif
 constexpr unsigned kSnappyGrid = RIO_SNAPPY_GRID;
-constexpr uint64_t kSinkBytes = (uint64_t)kSnappyBlock / 64 * kSnappyGrid * 64;
+constexpr unsigned kSnappyGridMax = 1024;
+static_assert(kSnappyGrid <= kSnappyGridMax, "sink sized for kSnappyGridMax workgroups");
+constexpr uint64_t kSinkBytes = (uint64_t)kSnappyBlock / 64 * kSnappyGridMax * 64;
 
 // Framing chunk: a byte range [cs, ce) of the file; a chunk OWNS the records whose header starts
 // in its range. Written by the walk kernel, consumed by the scan / place kernels.
