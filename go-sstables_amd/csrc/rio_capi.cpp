@@ -953,7 +953,9 @@ extern "C" void rio_reader_last_detail(rio_reader* r, uint64_t* d0, uint64_t* d1
     if (off) *off = tl_det.off;
 }
 
-constexpr uint64_t kAutoWindowFrom = 256ull << 20, kAutoWindow = 128ull << 20;
+// files past 32 MiB are read window by window (rio_stream_*): one window's H2D overlaps earlier windows'
+// decode and D2H, where the one-shot pair moves the whole file in, then all records out (round 4)
+constexpr uint64_t kAutoWindowFrom = 32ull << 20, kAutoWindow = 128ull << 20;
 
 static uint64_t reader_window(const rio_reader* r) {
     if (r->window == ~0ull) return 0;

@@ -497,8 +497,10 @@ struct rio_stream {
     uint64_t window = 0;
     uint32_t depth = 4;
     int device = 0;
-    static constexpr int kCtx = 2;
-    rio_ctx* ctx[kCtx] = {nullptr, nullptr};
+    // three contexts: window k+2 reads and frames while k and k+1 decode and copy out (VERDICT r3 #5:
+    // the D2H of consecutive windows runs back to back)
+    static constexpr int kCtx = 3;
+    rio_ctx* ctx[kCtx] = {nullptr, nullptr, nullptr};
     std::thread driver, worker[kCtx];
     std::mutex mu;
     std::condition_variable cv;
@@ -507,7 +509,7 @@ struct rio_stream {
         uint64_t k = 0, s = 0, first_record = 0;
         rio_file_info fi{};
     } job[kCtx];
-    bool busy[kCtx] = {false, false};
+    bool busy[kCtx] = {false, false, false};
     std::map<uint64_t, std::unique_ptr<Window>> ready;
     std::unique_ptr<Window> current;
     uint64_t next_out = 0;
@@ -538,7 +540,10 @@ struct rio_stream {
                 cv.wait(g, [&] { return stop || k > end_k || (!busy[c] && k < next_out + depth); });
                 if (stop || k > end_k) return;
             }
+            // ramp: the first windows are smaller, so the first D2H starts after a short H2D instead
+            // of a whole window's (windows of >= 8 MiB only; the ramp never changes what is decoded)
             uint64_t w = window, next_s = 0;
+            if (window >= (8ull << 20)) w = k == 0 ? window / 8 : (k == 1 ? window / 2 : window);
             rio_file_info fi{};
             bool terminal = false;
             for (;;) {

@@ -50,6 +50,7 @@ constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 // 209-232 into ring copies (A/B on MI355X, two rounds: C2 decode -0.6/-0.9 %, C4 -0.7/-0.9 %, C3 equal)
 constexpr uint32_t kFarOff = 232;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
+constexpr uint32_t kLitEff = ~0u;                // "offset" of a literal element (see snappy_lane)
 static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128 + 16, "far history must be flushed before the parser reads it");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
 
@@ -72,6 +73,25 @@ __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
 }
 __device__ __forceinline__ uint4 ld_far(const uint8_t* p) { return (RIO_NT & 2) ? ldu16_nt(p) : ldu16(p); }
+
+// RIO_BUF: the input prefetch and the flush store go through buffer descriptors (32-bit offsets from
+// the file / arena base, wave-uniform descriptors in SGPRs); a lane with nothing to load or store
+// passes an offset past the descriptor's range, which the range check drops (no sink line, no 64-bit
+// address arithmetic or pointer selects). The lane decoder only runs on files and arenas below
+// 0xFFFFFF00 bytes (snappy_wide), so every real offset fits 32 bits and kOob is out of range.
+#ifndef RIO_BUF
+#define RIO_BUF 1
+#endif
+constexpr uint32_t kOob = 0xFFFFFFC0u;
+typedef uint32_t v4u32b __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint64_t bytes) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bytes < 0xFFFFFF00ull ? bytes : 0xFFFFFF00ull));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, (int)n,
+                                             0x00020000);
+}
 }  // namespace
 
 // Files the 32-bit lane-stream positions cannot cover take the wave-per-record decoder.
@@ -507,8 +527,14 @@ __device__ __forceinline__ void col_hst(uint8_t* L, uint32_t a, uint32_t v) { co
 
 // Decode the record range [r0, r1) of this lane as one stream (as snappy_lane_t). L is the
 // workgroup's LDS base (input image, then history image).
+// kMulti = false: every lane holds at most one record (r1 <= r0 + 1; C2's shape), so the next-record
+// descriptor fetch, its latch and the record switch are compiled out. kLow = true: some lane's
+// first record starts in the arena's first 3 bytes (the caller passes it wave-uniform), so a far
+// copy there may need the kind-3 load from q (see the far-history load); every other wave has no
+// such lane and its far loads go through the arena descriptor.
+template <bool kMulti, bool kLow>
 __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* L,
-                                                uint32_t wave, uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
+                                            uint32_t wave, uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
     const uint32_t wl = wave * 256u + lane * 4u;  // row 0 of this lane (both images)
     // history / input row of a byte position (mod the ring), and the next row with wrap
     auto hrow = [&](uint32_t b) __attribute__((always_inline)) { return ((b << 8) & (kColH - kColRow)) | wl; };
@@ -549,12 +575,23 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     uint64_t k = r0;
     uint32_t s = (uint32_t)(start0 - base), s_end = s + d0.z;
     uint32_t pd = 0, rd_start = 0, rd_end = d0.w;
+    // eff: the current element's copy offset, or kLitEff for a literal (no copy offset is that large:
+    // a valid one is <= the bytes produced)
     uint32_t rem = 0, eff = 0;
-    bool islit = false, bad = false, pdone = !live;
+    bool bad = false, pdone = !live;
     uint4 nd = zero4();
-    uint32_t nds = (live && r0 + 1 < r1) ? 0u : 3u;
+    uint32_t nds = (kMulti && live && r0 + 1 < r1) ? 0u : 3u;
     uint32_t d = 0, fb = 0;
 
+#if RIO_BUF
+    const __amdgpu_buffer_rsrc_t rsrc_file = uniform_rsrc(P.file, P.len + RIO_DEVICE_PAD);
+    const __amdgpu_buffer_rsrc_t rsrc_out = uniform_rsrc(P.out, P.state->total_bytes + 16);
+    const uint32_t base32 = (uint32_t)base, o32 = (uint32_t)o0;
+    uint32_t obase[4];  // the flush owners' arena offsets
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; jj++)
+        obase[jj] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * jj + (lane >> 2)) * 4), (int)(uint32_t)o0);
+#else
     uint8_t* obase[4];
 #pragma unroll
     for (uint32_t jj = 0; jj < 4; jj++) {
@@ -563,6 +600,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
         obase[jj] = out + (((uint64_t)hi << 32) | lo);
     }
+#endif
 
     ColSlot S0 = col_empty_slot(), S1 = col_empty_slot(), S2 = col_empty_slot(), S3 = col_empty_slot();
     uint32_t drain = 0, qsrc = 0;
@@ -583,8 +621,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 
     auto step = [&](ColSlot& S, const ColSlot& N, const uint32_t j) __attribute__((always_inline)) {
         drain += pdone ? 1u : 0u;
-        nd = sel4(S.desc != 0, S.aux, nd);
-        nds = S.desc ? 2u : nds;
+        if constexpr (kMulti) {
+            nd = sel4(S.desc != 0, S.aux, nd);
+            nds = S.desc ? 2u : nds;
+        }
         const uint32_t pos = s;
 
         // 2. emit the piece parsed kD steps ago: destination dwords of bytes [d - r, d - r + 16)
@@ -602,7 +642,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             D3 = far ? S.aux.w : D3;
             // kind 3 (rare: a far source in the first bytes of the arena, lane of the file's first
             // record): aux holds bytes [q, q + 16), shifted up by r here
-            if (__builtin_expect(__any(S.kind == 3), 0)) {
+            if (kLow && __builtin_expect(__any(S.kind == 3), 0)) {
                 if (S.kind == 3) {
                     const uint32_t u = 4u - (d & 3u);
                     D0 = __builtin_amdgcn_alignbyte(S.aux.x, 0u, u);
@@ -672,7 +712,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t lit_hl = lng ? x - 58u : 1u;
             const uint32_t cp_hl = is1 ? 2u : (is2 ? 3u : 5u);
             const uint32_t hl = is0 ? lit_hl : cp_hl;
-            const uint32_t off = is1 ? c1_off : (is2 ? c2_off : W1);
+            const uint32_t off = is0 ? kLitEff : (is1 ? c1_off : (is2 ? c2_off : W1));
             const uint32_t sleft = s_end - s;
             const uint32_t lim = is0 ? sleft - hl : pd - rd_start;
             const uint32_t key = (is0 ? len : off) - 1u;
@@ -682,15 +722,17 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             bad = bad || badn;
             const uint32_t sh = ok ? hl : 0u;
             const uint32_t rem1 = ok ? len : rem, eff1 = ok ? off : eff;
-            const bool lit1 = ok ? t == 0 : islit;
+            const bool lit1 = eff1 == kLitEff;
             const bool go = !pdone && !badn && rem1 != 0 && (!lit1 || avail);
             // destination-aligned pieces: at most 16 - r bytes (r = pd & 3); a literal's bytes also
-            // stay inside the window [s, s + 16) the availability check covers
+            // stay inside the window [s, s + 16) the availability check covers, so a piece that starts
+            // with its element's header is capped at 16 - hl (copies too: only copies longer than
+            // 13 bytes ever take an extra piece for it); a copy's piece at most its offset
             const uint32_t r = pd & 3u;
-            const uint32_t cap = 16u - umax(lit1 ? sh : 0u, r);
-            const uint32_t n = go ? umin(rem1, lit1 ? cap : umin(cap, eff1)) : 0u;
+            const uint32_t cap = 16u - umax(sh, r);
+            const uint32_t n = go ? umin(rem1, umin(cap, eff1)) : 0u;
             S.n = n;
-            S.kind = n == 0 ? 1u : (lit1 ? 0u : (eff1 > kFarOff ? 2u : 1u));
+            S.kind = lit1 ? 0u : ((n != 0 && eff1 > kFarOff) ? 2u : 1u);
             qsrc = pd - eff1;
             // literal rows from (s + sh - r) & ~3 (the bytes below s + sh are masked at the emit)
             const uint32_t ls = s + sh - r;
@@ -704,8 +746,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
-            eff = (!lit1 && eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
-            islit = lit1;
+            eff = (eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
             s = badn ? s_end : s;
             uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
             pin_v(at_end);
@@ -713,9 +754,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
                 const bool bad_len = pd != rd_end;
                 bad = bad || bad_len;
                 rem = bad_len ? rd_end - pd : rem;
-                eff = bad_len ? 16u : eff;
-                islit = islit && !bad_len;
-                const bool more = k + 1 < r1;
+                eff = bad_len ? 16u : eff;  // the rest of the record: a ring copy (bytes unspecified)
+                const bool more = kMulti && k + 1 < r1;
                 const bool sw = !bad_len && more && nds == 2;
                 pdone = pdone || (!bad_len && !more);
                 k += sw ? 1u : 0u;
@@ -728,28 +768,51 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             }
         }
         // this step's owners' blocks (the far-history load below is issued after the store)
+#if RIO_BUF
+        {
+            const v4u32b w = {fv_now.x, fv_now.y, fv_now.z, fv_now.w};
+            __builtin_amdgcn_raw_buffer_store_b128(w, rsrc_out, (ofb_now >> 31) ? obase[j & 3u] + fpos_now : kOob, 0,
+                                                   (RIO_NT & 1) ? 2 : 0);
+        }
+#else
         st_out((ofb_now >> 31) ? obase[j & 3u] + fpos_now : sink, fv_now);
+#endif
         fb += ((lane >> 4) == (j & 3u) && ready_now) ? 64u : 0u;
 
         // far history (destination-aligned: from q - r), or the next record's descriptor, or a placeholder
         {
-            const bool want_desc = S.kind != 2 && nds == 0;
+            const bool want_desc = kMulti && S.kind != 2 && nds == 0;
             S.desc = want_desc ? 1u : 0u;
             nds = want_desc ? 1u : nds;
             const uint32_t r = (pd - S.n) & 3u;  // the piece's destination alignment
-            // 16 bytes from q - r would start below the arena: load from q, shift at the emit (kind 3)
-            const bool below = low_base && S.kind == 2 && qsrc < r;
-            S.kind = below ? 3u : S.kind;
-            const uint8_t* ap = S.kind >= 2 ? gout_m3 + (qsrc + 3u - (below ? 0u : r))
-                                            : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
-            S.aux = ld_far(ap);
+#if RIO_BUF
+            if constexpr (!kMulti && !kLow) {
+                // no descriptor to fetch and no source below the arena: the arena descriptor alone
+                const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, S.kind == 2 ? o32 + qsrc - r : kOob, 0,
+                                                                      (RIO_NT & 2) ? 2 : 0);
+                S.aux = make_uint4(v.x, v.y, v.z, v.w);
+            } else
+#endif
+            {
+                // 16 bytes from q - r would start below the arena: load from q, shift at the emit (kind 3)
+                const bool below = kLow && low_base && S.kind == 2 && qsrc < r;
+                S.kind = below ? 3u : S.kind;
+                const uint8_t* ap = S.kind >= 2 ? gout_m3 + (qsrc + 3u - (below ? 0u : r))
+                                                : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
+                S.aux = ld_far(ap);
+            }
         }
 
         // 5. input prefetch
         {
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn < a + kInCh;
+#if RIO_BUF
+            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, 0);
+            S.in = make_uint4(v.x, v.y, v.z, v.w);
+#else
             S.in = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
+#endif
             S.in_c = take ? cn : kNoChunk;
             cn += take ? 1u : 0u;
         }
@@ -844,7 +907,16 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     while (chunk < nchunks) {
         const uint64_t r0 = umin(chunk * per + lane * rpc, n), r1 = umin(r0 + rpc, n);
         uint64_t bad_rec = 0;
-        if (!snappy_lane(P, r0, r1, lds, wave, lane, sink, &bad_rec)) {
+        bool ok;
+        // lane 0 holds the wave's lowest arena offset: a wave whose lanes all start at >= 3 never needs kind 3
+        const bool low = __shfl(r0 < r1 ? P.out_off[r0] : ~0ull, 0) < 3;
+        if (rpc == 1)
+            ok = low ? snappy_lane<false, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
+                     : snappy_lane<false, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+        else
+            ok = low ? snappy_lane<true, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
+                     : snappy_lane<true, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+        if (!ok) {
             const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
             if (at < kFailLanes) {
                 P.fail_lanes[2 * at] = r0;
@@ -885,7 +957,15 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
             const uint64_t r0 = umin(t * rpl, n), r1 = umin(r0 + rpl, n);
             uint8_t* sink = P.sink + wg * 64;
             uint64_t bad_rec = 0;
-            if (!snappy_lane(P, r0, r1, lds, wave, lane, sink, &bad_rec)) {
+            bool ok;
+            const bool low = __shfl(r0 < r1 ? P.out_off[r0] : ~0ull, 0) < 3;
+            if (rpl == 1)
+                ok = low ? snappy_lane<false, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
+                         : snappy_lane<false, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+            else
+                ok = low ? snappy_lane<true, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
+                         : snappy_lane<true, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+            if (!ok) {
                 const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
                 if (at < kFailLanes) {
                     P.fail_lanes[2 * at] = r0;

@@ -138,7 +138,7 @@ class _Header:
 
 class FileReader(_Reader):
     """recordio.FileReader (ReaderI) backed by the device decode: the whole file at once, or, for
-    files larger than `window_bytes` (default: files over 256 MiB in 128 MiB windows; ~0 = never),
+    files larger than `window_bytes` (default: files over 32 MiB in 128 MiB windows; ~0 = never),
     window by window (rio_stream_*), with the same records and errors."""
 
     def __init__(self, path: str, device: int = 0, window_bytes: int | None = None):
