@@ -59,7 +59,9 @@ class HostPool {
   private:
     HostPool() {
         const char* v = getenv("RIO_COPY_THREADS");
-        const long t = v ? strtol(v, nullptr, 0) : 4;
+        // 8 copy threads (+ the caller): the staged H2D of a host image (rio_stream_open_host, rio_frame)
+        // ran at ~32 GB/s with 4, under PCIe's 57 GB/s (round 4); the GPU box gives a job 16 cores
+        const long t = v ? strtol(v, nullptr, 0) : 8;
         for (long i = 0; i < std::min(t, 32L); i++) workers_.emplace_back([this, i] { loop((size_t)i + 1); });
         for (auto& w : workers_) w.detach();
     }
