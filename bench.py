@@ -224,7 +224,7 @@ def e2e_rate(image, n_out_bytes: int) -> dict:
 
     def stream(open_fn, wbytes):
         best, nwin = None, 0
-        for _ in range(3):
+        for rep in range(6):  # the first run warms the context pool and the page-locked block cache
             h = ctypes.c_void_p()
             t0 = time.perf_counter()
             rc = open_fn(wbytes, h)
@@ -240,8 +240,10 @@ def e2e_rate(image, n_out_bytes: int) -> dict:
             lib.rio_stream_free(h)
             if rc != L.RIO_EOF or got != n:
                 raise RuntimeError(f"{L.strerror(rc)} after {got} records")
-            best = dt if best is None else min(best, dt)
-        return {"GiBps_input": round(image.shape[0] / 2**30 / best, 3), "windows": nwin, "seconds": round(best, 4)}
+            if rep:
+                best = dt if best is None else min(best, dt)
+        return {"GiBps_input": round(image.shape[0] / 2**30 / best, 3), "windows": nwin, "seconds": round(best, 4),
+                "runs": 5}
 
     def from_host(wbytes, h):
         return lib.rio_stream_open_host(dev, image.ctypes.data, image.shape[0], wbytes, 4, ctypes.byref(h))
