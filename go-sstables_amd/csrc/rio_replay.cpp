@@ -515,6 +515,7 @@ struct rio_stream {
     uint64_t next_out = 0;
     uint64_t end_k = ~0ull;  // index of the terminal window once known
     bool stop = false;
+    double t_origin = now_ms();  // RIO_REPLAY_TRACE timestamps are relative to the open
 
     void post_fatal(uint64_t k, int rc) {
         auto w = std::make_unique<Window>();
@@ -550,7 +551,11 @@ struct rio_stream {
                 const uint64_t e = whole ? len : s + std::min(w, len - s);
                 const uint64_t hl = whole ? 0 : RIO_FILE_HEADER_BYTES, n = hl + (e - s);
                 Fill f{&src, s, hdr, hl};
+                const double tf0 = kTrace ? now_ms() : 0.0;
                 if (int rc = rio::frame_fill(ctx[c], n, &Fill::fn, &f, &fi)) return post_fatal(k, rc);
+                if (kTrace)
+                    fprintf(stderr, "stream w%llu ctx%d: read+H2D+frame %llu B %.3f-%.3f ms\n", (unsigned long long)k, c,
+                            (unsigned long long)n, tf0 - t_origin, now_ms() - t_origin);
                 const uint64_t p = fi.status_offset + s - hl;  // file offset of the status
                 if (e == len) {
                     terminal = true;
@@ -590,7 +595,11 @@ struct rio_stream {
             w->k = j.k;
             w->first_record = j.first_record;
             w->d.info = j.fi;
+            const double td0 = kTrace ? now_ms() : 0.0;
             w->d.rc = decode_into(ctx[c], w->d);
+            if (kTrace)
+                fprintf(stderr, "stream w%llu ctx%d: decode+D2H %llu B out %.3f-%.3f ms\n", (unsigned long long)j.k, c,
+                        (unsigned long long)w->d.info.total_out_bytes, td0 - t_origin, now_ms() - t_origin);
             rio_file_info& fi = w->d.info;
             const uint64_t shift = j.s - RIO_FILE_HEADER_BYTES;  // window offset -> file offset
             for (uint64_t i = 0; !w->d.rc && shift && i < fi.n_records; i++) w->d.rec_off[i] += shift;
