@@ -157,13 +157,11 @@ namespace {
 // framing scratch + per-record decode descriptors of one file (a ctx has one set per file of a batch)
 struct FileArenas {
     DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, fail_lanes, chunks, block_runs, chunk_excl, place,
-        block_excl, state, info, lb, lb_ctl;
-    uint32_t lb_epoch = 0;  // tag of the last launch over lb (1 .. kLbTagMask; 0: lb must be zeroed first)
+        block_excl, state, info;
     void release() {
         for (DevBuf* b : {&scratch_off, &scratch_len, &scratch_pay, &rec_pay, &rec_desc, &fail_lanes, &chunks, &block_runs,
-                          &chunk_excl, &place, &block_excl, &state, &info, &lb, &lb_ctl})
+                          &chunk_excl, &place, &block_excl, &state, &info})
             b->release();
-        lb_epoch = 0;
     }
 };
 }  // namespace
@@ -176,7 +174,7 @@ struct rio_ctx {
     uint64_t ev_cursor = 0;
     uint64_t chunk_bytes = 32768;
     uint64_t coop_min = ~0ull >> 8;
-    uint32_t fused = 0;  // RIO_FUSED=1: device decodes place the records in the walk (look-back)
+    uint32_t walk_lanes = 0;  // RIO_WALK_LANES=1: k_walk_lanes frames
     hipEvent_t* next_events() {
         if (ev.empty()) return nullptr;
         return ev[ev_cursor++ % ev.size()].data();
@@ -230,6 +228,7 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     P.len = len;
     P.chunk_bytes = ctx->chunk_bytes;
     P.coop_min = ctx->coop_min;
+    P.walk_lanes = ctx->walk_lanes;
     P.comp_hint = RIO_COMP_UNKNOWN;
     P.zero_done = 0;
     P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + ctx->chunk_bytes - 1) / ctx->chunk_bytes : 0;
@@ -248,28 +247,6 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     HIP_TRY(A.info.ensure(sizeof(rio_file_info)));
     HIP_TRY(ctx->sink.ensure(kSinkBytes));
     HIP_TRY(A.fail_lanes.ensure(2 * kFailLanes * sizeof(uint64_t)));
-    P.fused = 0;
-    if (ctx->fused) {
-        // look-back words (fused walk): every launch tags its words with a new epoch, so a word from an
-        // earlier launch never matches; fresh buffers, and every kLbTagMask launches, are zeroed first
-        // (tag 0 is never used) once the previous call is done, with the host waiting, so no launch sees
-        // the old bytes
-        void* lb0 = A.lb.p;
-        void* ctl0 = A.lb_ctl.p;
-        HIP_TRY(A.lb.ensure(nc * kLbWords * sizeof(uint64_t)));
-        HIP_TRY(A.lb_ctl.ensure(8 * sizeof(uint64_t)));
-        if (A.lb.p != lb0 || A.lb_ctl.p != ctl0 || A.lb_epoch >= kLbTagMask) A.lb_epoch = 0;
-        if (A.lb_epoch == 0) {
-            if (ctx->order_valid) HIP_TRY(hipEventSynchronize(ctx->order_ev));
-            HIP_TRY(hipMemsetAsync(A.lb.p, 0, A.lb.cap, ctx->stream));
-            HIP_TRY(hipMemsetAsync(A.lb_ctl.p, 0, A.lb_ctl.cap, ctx->stream));
-            HIP_TRY(hipStreamSynchronize(ctx->stream));
-        }
-        A.lb_epoch++;
-        P.lb = A.lb.as<uint64_t>();
-        P.lb_ctl = A.lb_ctl.as<uint64_t>();
-        P.lb_epoch = A.lb_epoch;
-    }
     P.sink = ctx->sink.as<uint8_t>();
     P.fail_lanes = A.fail_lanes.as<uint64_t>();
     P.scratch_off = A.scratch_off.as<uint64_t>();
@@ -304,8 +281,7 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 32768);
     if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
     c->coop_min = env_u64("RIO_COOP_MIN", ~0ull >> 8);  // k_snappy_coop: wide files only
-    // look-back placement in the walk: opt-in until it has run on the GPU
-    c->fused = (uint32_t)env_u64("RIO_FUSED", 0);
+    c->walk_lanes = (uint32_t)env_u64("RIO_WALK_LANES", 0);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RIO_ERR_HIP;
@@ -404,12 +380,6 @@ extern "C" int rio_ctx_reserve(rio_ctx* ctx, uint64_t max_file_len, uint64_t max
     if (!ctx->order_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
     return RIO_OK;
 }
-// the walk places the records (look-back) when the decode follows in the same call and every value
-// fits the look-back words' 40 bits
-static uint32_t fused_ok(const rio_ctx* ctx, const FrameParams& P) {
-    return ctx->fused && P.lb && P.len < kLbMask && P.out_cap < kLbMask && P.rec_cap < kLbMask ? 1u : 0u;
-}
-
 extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                                  uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                                  uint64_t rec_cap, rio_file_info* d_info, void* stream) {
@@ -439,7 +409,6 @@ extern "C" int rio_device_decode_ex(rio_ctx* ctx, const uint8_t* d_file, uint64_
     HIP_TRY(ctx->fa.rec_desc.ensure((rec_cap + 1) * 16));
     P.rec_desc = ctx->fa.rec_desc.as<uint4>();
     P.comp_hint = compression;
-    P.fused = fused_ok(ctx, P);
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     if (int rc2 = order_before(ctx, s)) return rc2;
     hipEvent_t* ev = ctx->next_events();
@@ -488,7 +457,6 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
             P.rec_pay = A.rec_pay.as<uint64_t>();
             HIP_TRY(A.rec_desc.ensure((rec_cap[k] + 1) * 16));
             P.rec_desc = A.rec_desc.as<uint4>();
-            P.fused = fused_ok(ctx, P);
         }
         // stage events bracket the whole batch: [0] before the first file's framing, [1..2] after
         // the last file's walk / scan, [3] after placement, [4] after the decode kernels

@@ -13,6 +13,7 @@ constexpr uint64_t kNilBit = 1ull << 63;  // nil record
 constexpr uint64_t kBadBit = 1ull << 62;  // payload fails already at framing (codec preamble / size)
 constexpr uint64_t kEofBit = 1ull << 61;  // gzip: empty payload (gzip.NewReader's io.EOF)
 constexpr uint64_t kLenMask = kEofBit - 1;
+constexpr uint32_t kDescWide = 0xFFFFFFFFu;  // rec_desc z = w = kDescWide: sizes in rec_pay (rec_stream)
 // lanes of the Snappy lane decoder that met a corrupt record are listed for k_finish (re-checked there)
 constexpr uint32_t kFailLanes = 1024;
 
@@ -91,23 +92,7 @@ struct ScanState {
                             // size (its last member's ISIZE) does not cover: k_gz_resize sizes them;
                             // lzw: some record's output is not its header's u (k_lzw_resize)
     uint32_t gz_redo;       // k_gz_resize / k_lzw_resize ran: the scan, placement and decoders run again
-    uint32_t lb_fused;      // k_walk placed every record (look-back path, FrameParams::fused): k_scan_blocks
-                            // took the totals from its last chunk and k_place only merges the chunk flags
-    uint32_t pad_lb;
 };
-
-// Decoupled look-back of the fused walk (FrameParams::fused): per chunk kLbWords 8-byte words, each
-// written once per launch by one agent-scope (write-through) store and tagged with the launch's epoch
-// in its top 24 bits, so a reader needs no fence: a word is this launch's iff its tag matches.
-//   [0..4] the chunk's own run (key, out, cnt, bytes, term | broken << 1 | term_chunk << 2)
-//   [5..8] the inclusive prefix over chunks 0..c (out, cnt, bytes, flags; key is the file's first record)
-//   [9..11] placement flags for k_place (plain stores): first flagged record, flagged count, mixed | huge << 1
-// lb_ctl[0] = the walk's wave ticket (the last wave resets it to 0), [1..4] the whole file's run
-// (the last chunk's inclusive prefix).
-constexpr uint32_t kLbWords = 16;
-constexpr uint32_t kLbValBits = 40;
-constexpr uint64_t kLbMask = (1ull << kLbValBits) - 1;
-constexpr uint32_t kLbTagMask = (1u << 24) - 1;
 
 // Result of the single-record (ReadNextAt) kernel.
 struct ReadAtResult {
@@ -131,7 +116,8 @@ struct FrameParams {
     uint64_t* scratch_pay;   // [n_chunks * slots] payload descriptor (see rec_pay)
     // internal per-record payload descriptor [rec_cap]: bits 0..7 = bytes from the record header
     // start to the first payload byte the decoder consumes (header + snappy preamble), bits 8..63
-    // = length of the consumed payload stream (snappy element stream / raw payload)
+    // = length of the consumed payload stream (snappy element stream / raw payload). Written for
+    // gzip / lzw files and for records rec_desc cannot describe (see rec_stream)
     uint64_t* rec_pay;
     // internal per-record decode descriptor [rec_cap] (Snappy decode): x,y = file offset of the
     // element stream (lo, hi), z = stream length, w = decoded length
@@ -141,13 +127,9 @@ struct FrameParams {
     // Snappy: files whose mean decoded record is at least this many bytes (and files past 32-bit
     // lane positions) take the wave-per-record decoder k_snappy_coop instead of k_snappy_pipe
     uint64_t coop_min;
-    // 1: k_walk places the records itself (decoupled look-back over lb); only when the decode of the
-    // same FrameParams follows in the same call (rio_device_decode[_ex|_batch])
-    uint32_t fused;
-    uint64_t* lb;         // [n_chunks * kLbWords] look-back words (see kLbWords)
-    uint64_t* lb_ctl;     // [8] ticket + file totals
-    uint32_t lb_epoch;    // this launch's tag (1 .. kLbTagMask)
-    uint32_t pad1;
+    // 1: framing walks with k_walk_lanes (a lane per 1/64 of a chunk, header hops) instead of k_walk
+    uint32_t walk_lanes;
+    uint32_t pad_walk;
     // the file header's compression type as the host knows it (RIO_COMP_UNKNOWN: every decoder is
     // launched and exits unless the file is its own); k_finish rejects a file that contradicts it
     uint32_t comp_hint;
@@ -209,6 +191,20 @@ __device__ inline void mark_bad(const FrameParams& P, uint64_t i, uint8_t flag =
     P.flags[i] = (uint8_t)(P.flags[i] | flag);
     atomicMin((unsigned long long*)&P.state->first_bad, (unsigned long long)i);
     atomicAdd((unsigned long long*)&P.state->n_bad, 1ull);
+}
+// Record i's consumed stream (snappy element stream / raw payload): file offset and length. k_place
+// writes rec_pay only for gzip / lzw files (their kernels keep markers in it) and for records whose
+// sizes do not fit rec_desc's 32-bit fields (rec_desc then holds the kDescWide sentinel).
+__device__ inline void rec_stream(const FrameParams& P, uint64_t i, uint64_t& start, uint64_t& slen) {
+    const uint4 d = P.rec_desc[i];
+    if (d.z == kDescWide && d.w == kDescWide) {
+        const uint64_t pay = P.rec_pay[i];
+        start = P.rec_off[i] + (pay & 0xFF);
+        slen = pay >> 8;
+    } else {
+        start = ((uint64_t)d.y << 32) | d.x;
+        slen = d.z;
+    }
 }
 #endif
 

@@ -393,7 +393,7 @@ __device__ __forceinline__ int file_header_status(const FrameParams& P, uint32_t
     return RIO_OK;
 }
 
-__device__ void init_state(const FrameParams& P) {
+__device__ __forceinline__ void init_state(const FrameParams& P) {
     ScanState* st = P.state;
     const uint8_t* f = P.file;
     st->n_records = 0;
@@ -417,7 +417,6 @@ __device__ void init_state(const FrameParams& P) {
     st->pipe_next = 0;
     st->gz_resize = 0;
     st->gz_redo = 0;
-    st->lb_fused = 0;
     if (P.len < RIO_FILE_HEADER_BYTES) {
         st->hdr_status = RIO_ERR_SHORT_FILE_HEADER;
         st->version = st->compression = 0;
@@ -654,8 +653,6 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
     return mask;
 }
 
-__device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t lane, uint32_t comp, ChunkSum s);
-
 // minimum waves per SIMD for k_walk (0 = the compiler's choice, 4 waves). Round 1: 6 waves with 60 B
 // spilled to scratch beat 5 (walk 0.210 -> 0.185 ms on C2). With the packed DPP fill scans and the
 // 32-bit LEB128 packing the spills landed in the fill loop: 6 waves 0.413 ms on C3, 5 waves (96
@@ -673,20 +670,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
     if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
     crc32c_tab_init(crct);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
-    if (P.fused) {
-        // look-back path: chunks go to waves in the order the waves start (a ticket), so every chunk
-        // a wave waits for belongs to a wave that is already running; the wave taking the last ticket
-        // resets the counter for the next launch
-        uint32_t t = 0;
-        if (lane == 0) {
-            t = atomicAdd(reinterpret_cast<uint32_t*>(P.lb_ctl), 1u);
-            if (t == gridDim.x * kWalkWaves - 1)
-                __hip_atomic_store(reinterpret_cast<uint32_t*>(P.lb_ctl), 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(t, 0));
-    }
+    const uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
     uint32_t ver, comp;
     if (c >= P.n_chunks || file_header_status(P, ver, comp) != RIO_OK) return;  // wave-uniform
     WalkLds& L = W[wv];
@@ -821,9 +805,8 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         ws = we;
     }
     // 5. serial takeover where the chain left the candidates; the chunk summary
-    ChunkSum s;
     if (lane == 0) {
-        s = chunk_sum_empty(entry);
+        ChunkSum s = chunk_sum_empty(entry);
         s.count = (uint32_t)count;
         s.bytes = bytes;
         if (mode == 2)
@@ -832,14 +815,164 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
             s.exit = p;  // the chain left the chunk (or ended at the file end) cleanly
         P.chunks[c] = s;
     }
-    if (P.fused) {
-        // the summary to every lane (wave-uniform from here on)
-        s.entry = readlane64(s.entry, 0);
-        s.exit = readlane64(s.exit, 0);
-        s.bytes = readlane64(s.bytes, 0);
-        s.count = (uint32_t)__builtin_amdgcn_readlane((int)s.count, 0);
-        s.status = __builtin_amdgcn_readlane(s.status, 0);
-        walk_publish_place(P, c, lane, comp, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Lane-range walk (round 4, RIO_WALK_LANES=1): one wave per chunk, each lane one 1/64 range of it.
+//   1. every lane finds the first canonical magic in its range whose record frames (find_entry on
+//      the range) and walks the header chain from there to the range end (header-to-header hops:
+//      a record's payload bytes are never read);
+//   2. the wave follows the true chain from the chunk's entry over the lanes: the lane holding the
+//      chain position continues it if its own entry is that position, else it walks again from
+//      there (a speculative entry inside a payload, or none where the chain enters); a lane whose
+//      walk ended in an error ends the chunk's chain;
+//   3. the chain lanes' record counts are scanned into slot positions and those lanes walk their
+//      ranges again, writing the scratch slots.
+// Result and slots are identical to k_walk's (and to find_entry + walk_chunk). Where k_walk reads
+// every byte of the file (the candidate fill), this reads the headers: ~32 bytes per record.
+// ------------------------------------------------------------------------------------------
+struct LaneWalk {
+    uint64_t exit, bytes, err_off, det0, det1;
+    uint32_t count;
+    int32_t status;
+};
+
+// walk the chain from p while p < hi (FileReader order); slots from `slot` when `write`
+__device__ __forceinline__ LaneWalk lane_walk(const FrameParams& P, uint64_t c, uint64_t p, uint64_t hi, uint32_t ver,
+                                              uint32_t comp, const uint32_t* crct, bool write, uint64_t slot) {
+    LaneWalk w{p, 0, 0, 0, 0, 0, RIO_OK};
+    uint64_t* so = P.scratch_off + c * P.slots;
+    uint64_t* sl = P.scratch_len + c * P.slots;
+    uint64_t* sp = P.scratch_pay + c * P.slots;
+    while (p < hi) {
+        Hdr h;
+        uint64_t next = 0, olen = 0, pd = 0, lf = 0;
+        const int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd, lf, crct);
+        if (e) {
+            w.status = e;
+            w.err_off = p;
+            if (e == RIO_ERR_HEADER_CRC) {
+                w.det0 = h.exp_crc;
+                w.det1 = h.act_crc;
+            } else if (e == RIO_ERR_MAGIC) {
+                w.det0 = h.magic_len;
+            } else if (e == RIO_ERR_UNEXPECTED_EOF && h.hdr_len != 0) {
+                w.det0 = 1;  // raised by the payload read, not by a header varint
+            }
+            break;
+        }
+        if (write && slot < P.slots) {
+            so[slot] = p;
+            sl[slot] = olen | lf | (h.nil ? kNilBit : 0);
+            sp[slot] = pd;
+        }
+        slot++;
+        w.count++;
+        w.bytes += olen;
+        p = next;
+    }
+    w.exit = w.status ? w.err_off : p;
+    return w;
+}
+
+// first position in [lo, hi) holding the canonical magic whose record frames (find_entry's rule),
+// 64 bytes per round
+__device__ __forceinline__ uint64_t lane_entry(const FrameParams& P, uint64_t lo, uint64_t hi, uint32_t ver,
+                                               uint32_t comp, const uint32_t* crct) {
+    const uint8_t* f = P.file;
+    const uint32_t m3 = magic3(ver);
+    for (uint64_t q0 = lo & ~15ull; q0 < hi; q0 += 64) {
+        uint32_t masks[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint64_t q = q0 + 16 * j;
+            masks[j] = 0;
+            if (q < hi) {  // 16-B aligned; q + 20 <= len + RIO_DEVICE_PAD
+                const uint4 b = *reinterpret_cast<const uint4*>(f + q);
+                const uint32_t d[5] = {b.x, b.y, b.z, b.w, *reinterpret_cast<const uint32_t*>(f + q + 16)};
+                masks[j] = magic_mask(d, q, lo, hi, P.len, m3);
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            uint32_t m = masks[j];
+            while (m) {
+                const uint64_t p = q0 + 16 * j + (uint32_t)(__ffs(m) - 1);
+                m &= m - 1;
+                Hdr h;
+                uint64_t nx, ol, pd, lf;
+                if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd, lf, crct) == RIO_OK) return p;
+            }
+        }
+    }
+    return kNone;
+}
+
+__global__ void __launch_bounds__(64 * kWalkWaves) k_walk_lanes(FrameParams P) {
+    __shared__ uint32_t crct[1024];
+    if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
+    crc32c_tab_init(crct);
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
+    uint32_t ver, comp;
+    if (c >= P.n_chunks || file_header_status(P, ver, comp) != RIO_OK) return;  // wave-uniform
+    const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
+    const uint64_t sub = (((P.chunk_bytes + 63) >> 6) + 15) & ~15ull;  // a lane's range (16-B multiple)
+    const uint64_t lo = umin(cs + sub * lane, ce), hi = umin(lo + sub, ce);
+    // 1. speculative entry and walk of this lane's range (chunk 0 enters at the file header's end)
+    uint64_t ent = (c == 0 && lane == 0) ? (uint64_t)RIO_FILE_HEADER_BYTES
+                                         : (lo < hi ? lane_entry(P, lo, hi, ver, comp, crct) : kNone);
+    LaneWalk w{kNone, 0, 0, 0, 0, 0, RIO_OK};
+    if (ent != kNone) w = lane_walk(P, c, ent, hi, ver, comp, crct, false, 0);
+    // 2. the true chain over the lanes (wave-uniform)
+    uint64_t entry = kNone;
+    if (c == 0) {
+        entry = RIO_FILE_HEADER_BYTES;
+    } else {
+        const uint64_t m = __ballot(ent != kNone);
+        if (m) entry = readlane64(ent, (uint32_t)__builtin_ctzll(m));
+    }
+    uint64_t chain = 0, cur = entry;
+    int32_t st = RIO_OK;
+    uint64_t err_off = 0, det0 = 0, det1 = 0;
+    while (cur != kNone && cur < ce) {
+        const uint32_t k = (uint32_t)((cur - cs) / sub);
+        if (readlane64(ent, k) != cur) {  // the chain enters lane k elsewhere than its own entry
+            if (lane == k) {
+                ent = cur;
+                w = lane_walk(P, c, cur, hi, ver, comp, crct, false, 0);
+            }
+        }
+        chain |= 1ull << k;
+        st = __builtin_amdgcn_readlane(w.status, k);
+        if (st != RIO_OK) {
+            err_off = readlane64(w.err_off, k);
+            det0 = readlane64(w.det0, k);
+            det1 = readlane64(w.det1, k);
+            break;
+        }
+        cur = readlane64(w.exit, k);
+    }
+    // 3. slots: the chain lanes' records in order
+    const bool on = (chain >> lane) & 1ull;
+    const uint32_t cnt = on ? w.count : 0u;
+    const uint32_t inc = wave_incl_sum32(cnt);
+    const uint32_t total = lane63(inc);
+    uint64_t tb;
+    wave_excl_scan64(on ? w.bytes : 0ull, lane, tb);
+    if (on && cnt) lane_walk(P, c, ent, hi, ver, comp, crct, true, inc - cnt);
+    if (lane == 0) {
+        ChunkSum s = chunk_sum_empty(entry);
+        if (entry != kNone) {
+            s.count = total;
+            s.bytes = tb;
+            s.status = st;
+            s.err_off = err_off;
+            s.det0 = det0;
+            s.det1 = det1;
+            s.exit = st != RIO_OK ? err_off : cur;
+        }
+        P.chunks[c] = s;
     }
 }
 
@@ -902,40 +1035,6 @@ constexpr int kScanBlock = 256;
 
 __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]);
 
-// The fused walk's result (lb_ctl[1..4], this launch's tag): if the chain through the whole file held,
-// `write` (one thread) stores what scan_top would (record and byte totals, terminal status) and every
-// block skips the scan. A broken chain (a speculative entry that did not chain) takes the scan, whose
-// sequential repair then places the records again.
-__device__ bool fused_totals(const FrameParams& P, bool write) {
-    const uint64_t* T = P.lb_ctl + 1;
-    const uint32_t tag = P.lb_epoch;
-    for (int k = 0; k < 4; k++)
-        if ((uint32_t)(T[k] >> kLbValBits) != tag) return false;
-    auto val = [&](int k) {
-        const uint64_t v = T[k] & kLbMask;
-        return v == kLbMask ? kNone : v;
-    };
-    const uint64_t fl = val(3);
-    if (fl & 2) return false;  // broken
-    if (!write) return true;
-    ScanState* st = P.state;
-    st->n_records = val(1);
-    st->total_bytes = val(2);
-    if (fl & 1) {
-        const ChunkSum s = P.chunks[fl >> 2];
-        st->status = s.status;
-        st->status_offset = s.err_off;
-        st->det0 = s.det0;
-        st->det1 = s.det1;
-    } else {
-        st->status = RIO_EOF;  // chain ended exactly at the file end
-        st->status_offset = val(0);
-    }
-    if (st->status == RIO_ERR_MAGIC && st->version != RIO_VERSION1) st->zero_from = st->status_offset + st->det0;
-    st->lb_fused = 1;
-    return true;
-}
-
 // Level 1: inclusive scan of 256 chunk runs per block in LDS (Hillis-Steele, 8 steps). The last
 // block to finish (arrival ticket) runs level 2 over the block runs: one launch for the scan.
 __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
@@ -945,7 +1044,6 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
     const uint64_t c = (uint64_t)blockIdx.x * kScanBlock + t;
     if (P.state->hdr_status != RIO_OK) return;  // block-uniform
     if (P.redo && (!P.state->gz_redo || P.state->compression != P.redo)) return;  // another codec's redo round
-    if (P.fused && !P.redo && fused_totals(P, t == 0 && blockIdx.x == 0)) return;  // the walk placed everything
     RunSum v = c < P.n_chunks ? chunk_run(P, c) : run_identity();
     int cur = 0;
     buf[cur][t] = v;
@@ -1116,7 +1214,7 @@ struct PlaceFlags {
 };
 
 __device__ PlaceFlags place_chunk(const FrameParams& P, uint64_t c, uint64_t base_idx, uint64_t base_bytes,
-                                  uint64_t owned, bool snappy, uint32_t lane) {
+                                  uint64_t owned, bool snappy, bool pay_all, uint32_t lane) {
     PlaceFlags fl{kNone, 0, false, false};
     const uint64_t* so = P.scratch_off + c * P.slots;
     const uint64_t* sl = P.scratch_len + c * P.slots;
@@ -1146,15 +1244,19 @@ __device__ PlaceFlags place_chunk(const FrameParams& P, uint64_t c, uint64_t bas
         if (v) {
             const uint64_t i = base_idx + k;
             const uint64_t start = ro + (pay & 0xFF), slen = pay >> 8;
+            // rec_pay only where a consumer needs it (rec_stream): the stream position and length of a
+            // snappy / uncompressed record travel in rec_desc
+            const bool wide = slen >= kDescWide || len >= kDescWide;
             P.rec_off[i] = ro;
-            P.rec_pay[i] = pay;
+            if (pay_all || wide) P.rec_pay[i] = pay;
             P.out_off[i] = carry + excl;
             const uint8_t fg = ((l & kNilBit) ? RIO_FLAG_NIL : 0) | ((l & kBadBit) ? RIO_FLAG_CORRUPT : 0) |
                                ((l & kEofBit) ? RIO_FLAG_EOF : 0);
             P.flags[i] = fg;
             bad = (fg & (RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) != 0;  // failed at framing (stream length 0)
-            P.rec_desc[i] = make_uint4((uint32_t)start, (uint32_t)(start >> 32), (uint32_t)slen, (uint32_t)len);
-            huge = huge || (slen | len) > 0xFFFFFFFFull;
+            P.rec_desc[i] = make_uint4((uint32_t)start, (uint32_t)(start >> 32), wide ? kDescWide : (uint32_t)slen,
+                                       wide ? kDescWide : (uint32_t)len);
+            huge = huge || wide;  // (also a size of exactly 2^32 - 1: rec_desc holds the sentinel)
             // a snappy stream that is exactly one literal element of the record's whole length
             // (what golang/snappy emits for incompressible input) decodes as a copy
             if (snappy && fg == 0) mixed |= !snappy_single_literal(P.file + start, slen, len);
@@ -1184,183 +1286,9 @@ __device__ __forceinline__ void merge_place_flags(const FrameParams& P, const Pl
     if (f.mixed && st->compression == RIO_COMP_SNAPPY) st->any_mixed = 1u;
 }
 
-// ---- decoupled look-back (FrameParams::fused) -------------------------------------------------
-__device__ __forceinline__ uint64_t lb_word(uint32_t tag, uint64_t v) {
-    return ((uint64_t)tag << kLbValBits) | (v == kNone ? kLbMask : (v & kLbMask));
-}
-__device__ __forceinline__ uint64_t lb_val(uint64_t w) {
-    const uint64_t v = w & kLbMask;
-    return v == kLbMask ? kNone : v;
-}
-__device__ __forceinline__ bool lb_tagged(uint64_t w, uint32_t tag) { return (uint32_t)(w >> kLbValBits) == tag; }
-// agent-scope relaxed atomics: global_store / global_load with sc1 (write-through, L1 bypassed), so a
-// word another XCD stored is seen without a fence (MI355X_MICROARCH.md, inter-workgroup visibility)
-__device__ __forceinline__ void lb_st(uint64_t* p, uint64_t w) {
-    __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t lb_ld(uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t lb_flags(const RunSum& r) {
-    return (uint64_t)r.term | ((uint64_t)r.broken << 1) | (r.term_chunk << 2);
-}
-__device__ __forceinline__ void lb_unflag(RunSum& r, uint64_t f) {
-    r.term = (uint32_t)(f & 1);
-    r.broken = (uint32_t)((f >> 1) & 1);
-    r.term_chunk = f >> 2;
-}
-
-// bounded waits: a predecessor that never publishes (it cannot happen; a bug would hang the GPU) turns
-// into a broken chain after ~1 s, and the two-launch scan then frames the file
-#ifndef RIO_LB_SPIN_MAX
-#define RIO_LB_SPIN_MAX (1u << 22)
-#endif
-
-// Chunk c of the fused walk: publish its run, find the exclusive prefix over chunks 0..c-1 (the
-// nearest predecessor's inclusive prefix, composed with the runs of the chunks between, which lanes
-// read 64 at a time), publish the inclusive prefix, and place the chunk's records if the chain enters
-// it at its speculative entry; the last chunk publishes the file's run for k_scan_blocks.
-__device__ void walk_publish_place(const FrameParams& P, uint64_t c, uint32_t lane, uint32_t comp, ChunkSum s) {
-    const uint32_t tag = P.lb_epoch;
-    uint64_t* const me = P.lb + c * kLbWords;
-    RunSum A;  // this chunk's run (chunk_run)
-    A.key = s.entry;
-    A.out = s.exit;
-    A.cnt = s.count;
-    A.bytes = s.bytes;
-    A.ce = chunk_end(P, c);
-    A.term = s.status != RIO_OK;
-    // sizes the 40-bit words cannot carry (a header may announce far more output than the file holds)
-    // break the chain: the two-launch scan, in 64 bits, then frames the file
-    A.broken = A.bytes >= (kLbMask >> 1) ? 1u : 0u;
-    A.term_chunk = c;
-    {
-        const uint64_t v = lane == 0 ? A.key : lane == 1 ? A.out : lane == 2 ? A.cnt : lane == 3 ? A.bytes : lb_flags(A);
-        if (lane < 5) lb_st(me + lane, lb_word(tag, v));
-    }
-    RunSum E = run_identity();  // exclusive prefix
-    if (c > 0) {
-        RunSum acc = run_identity();  // runs of the chunks right of the current window, composed
-        uint64_t hi = c;              // window: chunks hi - 64 .. hi - 1 (lane l: chunk hi - 1 - l)
-        uint32_t spins = 0;
-        for (;;) {
-            const bool live = hi >= (uint64_t)lane + 1;
-            const uint64_t j = hi - 1 - lane;
-            uint64_t w[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) w[k] = 0;
-            bool hasA = false, hasP = !live;  // before chunk 0: the empty prefix
-            if (live) {
-                uint64_t* q = P.lb + j * kLbWords;
-#pragma unroll
-                for (int k = 0; k < 9; k++) w[k] = lb_ld(q + k);
-                hasA = lb_tagged(w[0], tag) && lb_tagged(w[1], tag) && lb_tagged(w[2], tag) && lb_tagged(w[3], tag) &&
-                       lb_tagged(w[4], tag);
-                hasP = lb_tagged(w[5], tag) && lb_tagged(w[6], tag) && lb_tagged(w[7], tag) && lb_tagged(w[8], tag);
-            }
-            const uint64_t pm = __ballot(hasP), am = __ballot(hasA);
-            const uint32_t kp = lane_ffs(pm);  // nearest lane with a prefix (64: none in the window)
-            const uint64_t need = kp >= 64 ? ~0ull : ((1ull << kp) - 1);
-            if ((am & need) != need) {  // a chunk between has not published its run yet
-                // wait for it with five loads per poll (lanes 0-4 read its run words), not the window's
-                // 576: thousands of waves re-reading whole windows saturated the memory system and
-                // starved the walks they were waiting for (C2 at 4406 chunks: 18 s per decode)
-                const uint64_t* q = P.lb + (hi - 1 - lane_ffs(need & ~am)) * kLbWords;
-                bool there = false;
-                while (!there && spins < RIO_LB_SPIN_MAX) {
-                    __builtin_amdgcn_s_sleep(8);
-                    spins++;
-                    there = __all(lane >= 5 || lb_tagged(lb_ld(const_cast<uint64_t*>(q) + lane), tag));
-                }
-                if (spins >= RIO_LB_SPIN_MAX) {
-                    E.ce = A.ce;
-                    E.key = RIO_FILE_HEADER_BYTES;
-                    E.broken = 1;
-                    break;
-                }
-                continue;
-            }
-            // lane kp's inclusive prefix (not the empty one), then the runs of lanes kp-1 .. 0 (later
-            // chunks at lower lanes), composed as a tree over the lanes: step k combines lane l + k's
-            // product (earlier chunks) with lane l's, so lane 0 ends with the window's composite
-            RunSum V = run_identity();
-            if (live && lane < kp) {
-                V.key = lb_val(w[0]);
-                V.out = lb_val(w[1]);
-                V.cnt = lb_val(w[2]);
-                V.bytes = lb_val(w[3]);
-                V.ce = chunk_end(P, j);
-                lb_unflag(V, lb_val(w[4]));
-            } else if (live && lane == kp) {
-                V.key = RIO_FILE_HEADER_BYTES;
-                V.out = lb_val(w[5]);
-                V.cnt = lb_val(w[6]);
-                V.bytes = lb_val(w[7]);
-                V.ce = chunk_end(P, j);
-                lb_unflag(V, lb_val(w[8]));
-            }
-#pragma unroll
-            for (uint32_t k = 1; k < 64; k <<= 1) {
-                RunSum U;
-                U.key = __shfl_down(V.key, k, 64);
-                U.out = __shfl_down(V.out, k, 64);
-                U.cnt = __shfl_down(V.cnt, k, 64);
-                U.bytes = __shfl_down(V.bytes, k, 64);
-                U.ce = __shfl_down(V.ce, k, 64);
-                const uint64_t f = __shfl_down(lb_flags(V), k, 64);
-                lb_unflag(U, f);
-                if (lane + k >= 64) U = run_identity();
-                V = combine(U, V);
-            }
-            RunSum X;
-            X.key = readlane64(V.key, 0);
-            X.out = readlane64(V.out, 0);
-            X.cnt = readlane64(V.cnt, 0);
-            X.bytes = readlane64(V.bytes, 0);
-            X.ce = readlane64(V.ce, 0);
-            lb_unflag(X, readlane64(lb_flags(V), 0));
-            acc = combine(X, acc);
-            if (kp < 64) break;
-            hi -= 64;
-        }
-        if (!E.broken) E = acc;
-    }
-    RunSum I = c > 0 ? combine(E, A) : A;  // inclusive prefix (chunk 0's run is keyed at 8)
-    if (I.bytes >= (kLbMask >> 1)) I.broken = 1;
-    {
-        const uint64_t v = lane == 5 ? I.out : lane == 6 ? I.cnt : lane == 7 ? I.bytes : lb_flags(I);
-        if (lane >= 5 && lane < 9) lb_st(me + lane, lb_word(tag, v));
-    }
-    // ownership as k_place decides it: the chain (unbroken, not terminated) enters chunk c at its entry
-    ChunkPlace pl;
-    pl.base_idx = E.cnt;
-    pl.base_bytes = E.bytes;
-    pl.owned = 0;
-    if (c == 0)
-        pl.owned = s.count;
-    else if (!E.broken && !E.term && s.entry != kNone && E.out == s.entry)
-        pl.owned = s.count;
-    if (lane == 0) P.place[c] = pl;
-    PlaceFlags f{kNone, 0, false, false};
-    if (pl.owned && pl.base_idx + pl.owned <= P.rec_cap) {
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's scratch stores before it reads them back
-        f = place_chunk(P, c, pl.base_idx, pl.base_bytes, pl.owned, comp == RIO_COMP_SNAPPY, lane);
-    }
-    if (lane == 0) {  // for k_place (next launch): plain stores
-        me[9] = f.first_bad;
-        me[10] = f.n_bad;
-        me[11] = (f.mixed ? 1u : 0u) | (f.huge ? 2u : 0u);
-    }
-    if (c + 1 == P.n_chunks) {  // the file's run
-        const uint64_t v = lane == 0 ? I.out : lane == 1 ? I.cnt : lane == 2 ? I.bytes : lb_flags(I);
-        if (lane < 4) lb_st(P.lb_ctl + 1 + lane, lb_word(tag, v));
-    }
-}
-
 // Placement: one wave per chunk (place_chunk). Its prologue also does what used to be two launches:
 // the capacity check + sentinel out_off[n] (block 0) and, on the device-resident path, the zero-tail
-// test of a magic mismatch (grid-stride). When the walk already placed the records (look-back path,
-// ScanState::lb_fused), a wave only merges its chunk's flags.
+// test of a magic mismatch (grid-stride).
 __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -1381,13 +1309,6 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
         if (__any(nz != 0) && lane == 0) atomicOr(&st->zero_nonzero, 1u);
     }
     if (c >= P.n_chunks) return;  // wave-uniform
-    if (st->lb_fused && !P.redo) {
-        if (lane == 0) {
-            const uint64_t* w = P.lb + c * kLbWords;
-            merge_place_flags(P, PlaceFlags{w[9], w[10], (w[11] & 1) != 0, (w[11] & 2) != 0});
-        }
-        return;
-    }
     ChunkPlace pl;
     if (st->slow) {
         pl = P.place[c];
@@ -1414,7 +1335,8 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     if (pl.base_idx + pl.owned > P.rec_cap || st->n_records > P.rec_cap) return;
     // once any wave has found a mixed record the file takes k_snappy_pipe: later waves skip the probe
     const bool snappy = st->compression == RIO_COMP_SNAPPY && !*(volatile const uint32_t*)&st->any_mixed;
-    const PlaceFlags f = place_chunk(P, c, pl.base_idx, pl.base_bytes, pl.owned, snappy, lane);
+    const bool pay_all = st->compression == RIO_COMP_GZIP || st->compression == RIO_COMP_LZW;
+    const PlaceFlags f = place_chunk(P, c, pl.base_idx, pl.base_bytes, pl.owned, snappy, pay_all, lane);
     if (lane == 0) merge_place_flags(P, f);
 }
 
@@ -1460,9 +1382,10 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
     for (uint64_t i = grp; i < n; i += ngrp) {
         const uint64_t o0 = P.out_off[i], len = P.out_off[i + 1] - o0;
         if (len == 0) continue;
-        const uint64_t pay = P.rec_pay[i];  // 64-bit stream position and length (any file size)
-        const uint8_t* s0 = P.file + P.rec_off[i] + (pay & 0xFF);
-        const uint8_t* src = none ? s0 : s0 + snappy_literal_hdr(s0, pay >> 8, len);
+        uint64_t start, slen;  // 64-bit stream position and length (any file size)
+        rec_stream(P, i, start, slen);
+        const uint8_t* s0 = P.file + start;
+        const uint8_t* src = none ? s0 : s0 + snappy_literal_hdr(s0, slen, len);
         uint8_t* dst = P.out + o0;
         for (uint64_t k = 16 * lane; k < len; k += 256) {
             const uint4 v = ldu16(src + k);
@@ -1547,8 +1470,10 @@ __global__ void __launch_bounds__(256) k_finish(FrameParams P) {
     if (st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_SNAPPY && st->n_fail_lanes) {
         auto verify = [&](uint64_t i) {
             if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) return;
-            const uint64_t pay = P.rec_pay[i], o0 = P.out_off[i], o1 = P.out_off[i + 1];
-            if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), pay >> 8, P.out + o0, o1 - o0))
+            const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
+            uint64_t start, slen;
+            rec_stream(P, i, start, slen);
+            if (!snappy_decode_thread(P.file + start, slen, P.out + o0, o1 - o0))
                 mark_bad(P, i);
         };
         if (st->n_fail_lanes > kFailLanes) {  // the list overflowed: every record
@@ -2132,7 +2057,10 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
 // Framing: k_walk (file header, state reset, chunk walk), k_scan_blocks (both scan levels).
 hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], s);
-    hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
+    if (P.walk_lanes)
+        hipLaunchKernelGGL(k_walk_lanes, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
+    else
+        hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
     if (ev) (void)hipEventRecord(ev[2], s);

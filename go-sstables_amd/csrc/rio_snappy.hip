@@ -434,9 +434,10 @@ __device__ __forceinline__ void coop_file(const FrameParams& P, CoopLds& S, uint
         // every record by one thread, byte loops straight to HBM
         for (uint64_t i = wave * 64 + lane; i < n; i += nw * 64) {
             if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
-            const uint64_t pay = P.rec_pay[i];
             const uint64_t o0 = P.out_off[i], o1 = P.out_off[i + 1];
-            if (!snappy_decode_thread(P.file + P.rec_off[i] + (pay & 0xFF), pay >> 8, P.out + o0, o1 - o0))
+            uint64_t start, slen;
+            rec_stream(P, i, start, slen);
+            if (!snappy_decode_thread(P.file + start, slen, P.out + o0, o1 - o0))
                 mark_bad(P, i);
         }
         return;
