@@ -174,7 +174,6 @@ struct rio_ctx {
     uint64_t ev_cursor = 0;
     uint64_t chunk_bytes = 32768;
     uint64_t coop_min = ~0ull >> 8;
-    uint32_t walk_lanes = 0;  // RIO_WALK_LANES=1: k_walk_lanes frames
     hipEvent_t* next_events() {
         if (ev.empty()) return nullptr;
         return ev[ev_cursor++ % ev.size()].data();
@@ -228,7 +227,6 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     P.len = len;
     P.chunk_bytes = ctx->chunk_bytes;
     P.coop_min = ctx->coop_min;
-    P.walk_lanes = ctx->walk_lanes;
     P.comp_hint = RIO_COMP_UNKNOWN;
     P.zero_done = 0;
     P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + ctx->chunk_bytes - 1) / ctx->chunk_bytes : 0;
@@ -281,7 +279,6 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 32768);
     if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
     c->coop_min = env_u64("RIO_COOP_MIN", ~0ull >> 8);  // k_snappy_coop: wide files only
-    c->walk_lanes = (uint32_t)env_u64("RIO_WALK_LANES", 0);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RIO_ERR_HIP;

@@ -127,9 +127,6 @@ struct FrameParams {
     // Snappy: files whose mean decoded record is at least this many bytes (and files past 32-bit
     // lane positions) take the wave-per-record decoder k_snappy_coop instead of k_snappy_pipe
     uint64_t coop_min;
-    // 1: framing walks with k_walk_lanes (a lane per 1/64 of a chunk, header hops) instead of k_walk
-    uint32_t walk_lanes;
-    uint32_t pad_walk;
     // the file header's compression type as the host knows it (RIO_COMP_UNKNOWN: every decoder is
     // launched and exits unless the file is its own); k_finish rejects a file that contradicts it
     uint32_t comp_hint;

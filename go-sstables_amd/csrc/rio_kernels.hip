@@ -818,165 +818,6 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Lane-range walk (round 4, RIO_WALK_LANES=1): one wave per chunk, each lane one 1/64 range of it.
-//   1. every lane finds the first canonical magic in its range whose record frames (find_entry on
-//      the range) and walks the header chain from there to the range end (header-to-header hops:
-//      a record's payload bytes are never read);
-//   2. the wave follows the true chain from the chunk's entry over the lanes: the lane holding the
-//      chain position continues it if its own entry is that position, else it walks again from
-//      there (a speculative entry inside a payload, or none where the chain enters); a lane whose
-//      walk ended in an error ends the chunk's chain;
-//   3. the chain lanes' record counts are scanned into slot positions and those lanes walk their
-//      ranges again, writing the scratch slots.
-// Result and slots are identical to k_walk's (and to find_entry + walk_chunk). Where k_walk reads
-// every byte of the file (the candidate fill), this reads the headers: ~32 bytes per record.
-// ------------------------------------------------------------------------------------------
-struct LaneWalk {
-    uint64_t exit, bytes, err_off, det0, det1;
-    uint32_t count;
-    int32_t status;
-};
-
-// walk the chain from p while p < hi (FileReader order); slots from `slot` when `write`
-__device__ __forceinline__ LaneWalk lane_walk(const FrameParams& P, uint64_t c, uint64_t p, uint64_t hi, uint32_t ver,
-                                              uint32_t comp, const uint32_t* crct, bool write, uint64_t slot) {
-    LaneWalk w{p, 0, 0, 0, 0, 0, RIO_OK};
-    uint64_t* so = P.scratch_off + c * P.slots;
-    uint64_t* sl = P.scratch_len + c * P.slots;
-    uint64_t* sp = P.scratch_pay + c * P.slots;
-    while (p < hi) {
-        Hdr h;
-        uint64_t next = 0, olen = 0, pd = 0, lf = 0;
-        const int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd, lf, crct);
-        if (e) {
-            w.status = e;
-            w.err_off = p;
-            if (e == RIO_ERR_HEADER_CRC) {
-                w.det0 = h.exp_crc;
-                w.det1 = h.act_crc;
-            } else if (e == RIO_ERR_MAGIC) {
-                w.det0 = h.magic_len;
-            } else if (e == RIO_ERR_UNEXPECTED_EOF && h.hdr_len != 0) {
-                w.det0 = 1;  // raised by the payload read, not by a header varint
-            }
-            break;
-        }
-        if (write && slot < P.slots) {
-            so[slot] = p;
-            sl[slot] = olen | lf | (h.nil ? kNilBit : 0);
-            sp[slot] = pd;
-        }
-        slot++;
-        w.count++;
-        w.bytes += olen;
-        p = next;
-    }
-    w.exit = w.status ? w.err_off : p;
-    return w;
-}
-
-// first position in [lo, hi) holding the canonical magic whose record frames (find_entry's rule),
-// 64 bytes per round
-__device__ __forceinline__ uint64_t lane_entry(const FrameParams& P, uint64_t lo, uint64_t hi, uint32_t ver,
-                                               uint32_t comp, const uint32_t* crct) {
-    const uint8_t* f = P.file;
-    const uint32_t m3 = magic3(ver);
-    for (uint64_t q0 = lo & ~15ull; q0 < hi; q0 += 64) {
-        uint32_t masks[4];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
-            const uint64_t q = q0 + 16 * j;
-            masks[j] = 0;
-            if (q < hi) {  // 16-B aligned; q + 20 <= len + RIO_DEVICE_PAD
-                const uint4 b = *reinterpret_cast<const uint4*>(f + q);
-                const uint32_t d[5] = {b.x, b.y, b.z, b.w, *reinterpret_cast<const uint32_t*>(f + q + 16)};
-                masks[j] = magic_mask(d, q, lo, hi, P.len, m3);
-            }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
-            uint32_t m = masks[j];
-            while (m) {
-                const uint64_t p = q0 + 16 * j + (uint32_t)(__ffs(m) - 1);
-                m &= m - 1;
-                Hdr h;
-                uint64_t nx, ol, pd, lf;
-                if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd, lf, crct) == RIO_OK) return p;
-            }
-        }
-    }
-    return kNone;
-}
-
-__global__ void __launch_bounds__(64 * kWalkWaves) k_walk_lanes(FrameParams P) {
-    __shared__ uint32_t crct[1024];
-    if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
-    crc32c_tab_init(crct);
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t c = (uint64_t)blockIdx.x * kWalkWaves + wv;
-    uint32_t ver, comp;
-    if (c >= P.n_chunks || file_header_status(P, ver, comp) != RIO_OK) return;  // wave-uniform
-    const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
-    const uint64_t sub = (((P.chunk_bytes + 63) >> 6) + 15) & ~15ull;  // a lane's range (16-B multiple)
-    const uint64_t lo = umin(cs + sub * lane, ce), hi = umin(lo + sub, ce);
-    // 1. speculative entry and walk of this lane's range (chunk 0 enters at the file header's end)
-    uint64_t ent = (c == 0 && lane == 0) ? (uint64_t)RIO_FILE_HEADER_BYTES
-                                         : (lo < hi ? lane_entry(P, lo, hi, ver, comp, crct) : kNone);
-    LaneWalk w{kNone, 0, 0, 0, 0, 0, RIO_OK};
-    if (ent != kNone) w = lane_walk(P, c, ent, hi, ver, comp, crct, false, 0);
-    // 2. the true chain over the lanes (wave-uniform)
-    uint64_t entry = kNone;
-    if (c == 0) {
-        entry = RIO_FILE_HEADER_BYTES;
-    } else {
-        const uint64_t m = __ballot(ent != kNone);
-        if (m) entry = readlane64(ent, (uint32_t)__builtin_ctzll(m));
-    }
-    uint64_t chain = 0, cur = entry;
-    int32_t st = RIO_OK;
-    uint64_t err_off = 0, det0 = 0, det1 = 0;
-    while (cur != kNone && cur < ce) {
-        const uint32_t k = (uint32_t)((cur - cs) / sub);
-        if (readlane64(ent, k) != cur) {  // the chain enters lane k elsewhere than its own entry
-            if (lane == k) {
-                ent = cur;
-                w = lane_walk(P, c, cur, hi, ver, comp, crct, false, 0);
-            }
-        }
-        chain |= 1ull << k;
-        st = __builtin_amdgcn_readlane(w.status, k);
-        if (st != RIO_OK) {
-            err_off = readlane64(w.err_off, k);
-            det0 = readlane64(w.det0, k);
-            det1 = readlane64(w.det1, k);
-            break;
-        }
-        cur = readlane64(w.exit, k);
-    }
-    // 3. slots: the chain lanes' records in order
-    const bool on = (chain >> lane) & 1ull;
-    const uint32_t cnt = on ? w.count : 0u;
-    const uint32_t inc = wave_incl_sum32(cnt);
-    const uint32_t total = lane63(inc);
-    uint64_t tb;
-    wave_excl_scan64(on ? w.bytes : 0ull, lane, tb);
-    if (on && cnt) lane_walk(P, c, ent, hi, ver, comp, crct, true, inc - cnt);
-    if (lane == 0) {
-        ChunkSum s = chunk_sum_empty(entry);
-        if (entry != kNone) {
-            s.count = total;
-            s.bytes = tb;
-            s.status = st;
-            s.err_off = err_off;
-            s.det0 = det0;
-            s.det1 = det1;
-            s.exit = st != RIO_OK ? err_off : cur;
-        }
-        P.chunks[c] = s;
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // Key-point run composition. combine(A, B): A's byte range precedes B's.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ RunSum run_identity() {
@@ -2057,10 +1898,7 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
 // Framing: k_walk (file header, state reset, chunk walk), k_scan_blocks (both scan levels).
 hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], s);
-    if (P.walk_lanes)
-        hipLaunchKernelGGL(k_walk_lanes, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
-    else
-        hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
+    hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
     if (ev) (void)hipEventRecord(ev[2], s);

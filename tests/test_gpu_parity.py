@@ -66,20 +66,16 @@ def test_repairs_happen_and_stay_exact():
         assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), name)
 
 
-@pytest.mark.parametrize("walk_lanes", [0, 1])
 @pytest.mark.parametrize("chunk", [64, 256, 1024, 4096, 65536])
-def test_chunk_size_independent(chunk, walk_lanes, monkeypatch):
+def test_chunk_size_independent(chunk, monkeypatch):
     """The result does not depend on the framing chunk size (speculation granularity): at 64-byte
-    chunks the files have thousands of chunks and speculations that break and are repaired. Both
-    walks: k_walk (candidate fill + chain votes) and k_walk_lanes (RIO_WALK_LANES=1: a lane per
-    1/64 of a chunk, header hops; at 64-byte chunks a lane's range is 16 bytes)."""
+    chunks the files have thousands of chunks and speculations that break and are repaired."""
     import ctypes
 
     from recordio import _lib as L
     from recordio.device import DeviceDecoder, to_device_file
 
     monkeypatch.setenv("RIO_CHUNK_BYTES", str(chunk))
-    monkeypatch.setenv("RIO_WALK_LANES", str(walk_lanes))
     h = ctypes.c_void_p()
     assert L.lib().rio_ctx_create(0, ctypes.byref(h)) == 0
     try:
