@@ -107,3 +107,37 @@ def test_wave_decoder_on_large_and_damaged_records(coop_ctx):
         g = dict(info, out=b.out[:info["total_out_bytes"]].cpu().numpy(), out_off=b.out_off[:kk + 1].cpu().numpy(),
                  rec_off=b.rec_off[:kk].cpu().numpy(), flags=b.flags[:kk].cpu().numpy())
         assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), f"coop {k}")
+
+
+def _crc32c(data: bytes) -> int:
+    c = 0xFFFFFFFF
+    for b in data:
+        c ^= b
+        for _ in range(8):
+            c = (c >> 1) ^ (0x82F63B78 & -(c & 1))
+    return c ^ 0xFFFFFFFF
+
+
+def _uvarint(x: int) -> bytes:
+    o = bytearray()
+    while x >= 0x80:
+        o.append((x & 0x7F) | 0x80)
+        x >>= 7
+    o.append(x)
+    return bytes(o)
+
+
+@pytest.mark.parametrize("size", [FOUR_GIB - 1, FOUR_GIB + 4096])
+def test_uncompressed_record_of_4gib(size):
+    """One uncompressed v4 record whose length does not fit rec_desc's 32-bit fields (2^32 - 1 is the
+    sentinel itself): its stream position and length come from rec_pay (k_place writes it for such a
+    record only, rio_device.h rec_stream), and k_copy_records moves it whole."""
+    head = b"\x91\x8d\x4c\x00" + _uvarint(size) + _uvarint(0)  # v4, not nil, u = size, c = 0 (uncompressed)
+    head += _uvarint(_crc32c(head))
+    fh = np.frombuffer(bytes.fromhex("0400000000000000"), dtype=np.uint8)  # v4, compression 0
+    payload = np.resize(np.arange(251, dtype=np.uint8), size)
+    img = np.concatenate([fh, np.frombuffer(head, dtype=np.uint8), payload])
+    g = gpu_decode_arrays(img)
+    assert g["status"] == STATUS["EOF"] and g["n_records"] == 1 and g["total_out_bytes"] == size
+    assert int(g["rec_off"][0]) == 8 and int(g["out_off"][1]) == size
+    assert np.array_equal(g["out"][:size], payload)
