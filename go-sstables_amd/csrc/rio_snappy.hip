@@ -82,10 +82,6 @@ __device__ __forceinline__ uint4 ld_far(const uint8_t* p) { return (RIO_NT & 2) 
 #ifndef RIO_BUF
 #define RIO_BUF 1
 #endif
-// RIO_V4: small VALU cuts (wave-uniform drain, shorter literal-length mask, q without the kind test)
-#ifndef RIO_V4
-#define RIO_V4 0
-#endif
 constexpr uint32_t kOob = 0xFFFFFFC0u;
 typedef uint32_t v4u32b __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint64_t bytes) {
@@ -608,19 +604,12 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 #endif
 
     ColSlot S0 = col_empty_slot(), S1 = col_empty_slot(), S2 = col_empty_slot(), S3 = col_empty_slot();
-#if RIO_V4
-    uint32_t qsrc = 0;
-#else
     uint32_t drain = 0, qsrc = 0;
-#endif
     // the next emit's source rows (ring copy) and shift, and the row holding bytes [d & ~3, d)
     uint32_t wL0 = 0, wL1 = 0, wL2 = 0, wL3 = 0, wL4 = 0, wSh = 0, wP = 0;
     uint32_t aD = hrow(0);  // history row of d
     // the flush in flight: this step's owners' blocks, read during the previous step
     uint4 pfv = zero4();
-#if RIO_V4 && RIO_BUF
-    v4u32b pfv4 = {0u, 0u, 0u, 0u};
-#endif
     uint32_t pofb = 0, pfpos = 0;
     bool pready = false;
     // the parser's window: rows s >> 2 and (s >> 2) + 1, read one step ahead
@@ -632,9 +621,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     }
 
     auto step = [&](ColSlot& S, const ColSlot& N, const uint32_t j) __attribute__((always_inline)) {
-#if !RIO_V4
         drain += pdone ? 1u : 0u;
-#endif
         if constexpr (kMulti) {
             nd = sel4(S.desc != 0, S.aux, nd);
             nds = S.desc ? 2u : nds;
@@ -757,7 +744,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.x3 = col_ld(L, c3);
             S.x4 = col_ld(L, c4);
             // literal: the shift (low 2 bits) of x0..x4; a far copy's q goes unused at the emit
-            S.q = RIO_V4 ? (lit1 ? ls : qsrc) : (S.kind == 1 ? qsrc : ls);
+            S.q = S.kind == 1 ? qsrc : ls;
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
@@ -785,15 +772,9 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         // this step's owners' blocks (the far-history load below is issued after the store)
 #if RIO_BUF
         {
-#if RIO_V4
-            // pfv / pfpos are not touched between the previous step's reads and here: store them in place
-            __builtin_amdgcn_raw_buffer_store_b128(pfv4, rsrc_out, (ofb_now >> 31) ? obase[j & 3u] + pfpos : kOob, 0,
-                                                   (RIO_NT & 1) ? 2 : 0);
-#else
             const v4u32b w = {fv_now.x, fv_now.y, fv_now.z, fv_now.w};
             __builtin_amdgcn_raw_buffer_store_b128(w, rsrc_out, (ofb_now >> 31) ? obase[j & 3u] + fpos_now : kOob, 0,
                                                    (RIO_NT & 1) ? 2 : 0);
-#endif
         }
 #else
         st_out((ofb_now >> 31) ? obase[j & 3u] + fpos_now : sink, fv_now);
@@ -856,12 +837,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t fo = 16u * ((j + 1) & 3u) + (lane >> 2);
             pfpos = (pofb & 0x7FFFFFFFu) + 16u * (lane & 3u);
             const uint32_t fa = ((pfpos << 8) & (kColH - kColRow)) | (wave * 256u + fo * 4u);
-#if RIO_V4 && RIO_BUF
-            pfv4 = v4u32b{col_hld(L, fa), col_hld(L, fa + kColRow), col_hld(L, fa + 2 * kColRow), col_hld(L, fa + 3 * kColRow)};
-#else
             pfv = make_uint4(col_hld(L, fa), col_hld(L, fa + kColRow), col_hld(L, fa + 2 * kColRow),
                              col_hld(L, fa + 3 * kColRow));
-#endif
             const uint32_t a = irow(s);
             Wa = col_ld(L, a);
             Wb = col_ld(L, inext(a));
@@ -869,22 +846,12 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     };
 
     static_assert(kD == 4, "unrolled for four slots");
-#if RIO_V4
-    uint32_t tail = 0;
-#endif
     do {
         step(S0, S1, 0);
         step(S1, S2, 1);
         step(S2, S3, 2);
         step(S3, S0, 3);
-#if RIO_V4
-        // every lane done: one more round of kD steps empties the last pieces' slots (a wave-uniform
-        // count instead of a per-lane drain counter)
-        tail = __any(!pdone) ? 0u : tail + 1u;
-    } while (tail < 2u);
-#else
     } while (__any(drain < kD));
-#endif
     // the stream's tail (< 128 bytes) from the lane's own rows
     for (uint32_t q = fb; q < d; q += 16) {
         const uint32_t a = hrow(q);
