@@ -117,3 +117,40 @@ def test_every_alignment_and_source_kind(seed):
 def test_long_records_with_far_copies():
     rng = random.Random(7)
     check(file_of([far_from_start(rng)] + [mixed(rng, 3000) for _ in range(40)]))
+
+
+def mutated_file(rng, n_rec):
+    """Valid streams (`mixed`) with seeded damage in about a third of the records, behind valid headers
+    (the v4 header CRC covers the header only, so framing keeps every record): flipped element bytes,
+    a wrong decoded-length preamble, a cut element stream, or a copy offset pushed past the bytes
+    produced. Records are written with the damaged payload's own length, as a writer would."""
+    img = bytearray(corpus.file_header(4, 2))
+    for _ in range(n_rec):
+        st = mixed(rng, rng.randrange(0, 300))
+        pre, els = corpus.uvarint(len(st.out)), bytearray(st.els)
+        k = rng.random()
+        if k < 0.15 and els:  # flipped bytes anywhere in the element stream
+            for _ in range(rng.randrange(1, 4)):
+                els[rng.randrange(len(els))] ^= 1 << rng.randrange(8)
+        elif k < 0.22:  # preamble one off, or far off
+            pre = corpus.uvarint(max(0, len(st.out) + rng.choice([-1, 1, 7, -len(st.out), 1 << 20])))
+        elif k < 0.30 and els:  # the stream cut inside its last elements
+            del els[len(els) - rng.randrange(1, min(6, len(els)) + 1):]
+        elif k < 0.35 and els:  # a 2-byte-offset copy reaching before the record start
+            els += bytes([2 | (3 << 2)]) + (len(st.out) + 1 + rng.randrange(100)).to_bytes(2, "little")
+        pay = pre + bytes(els)
+        img += corpus.header_v4(len(st.out), len(pay)) + pay
+    return bytes(img)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_damaged_streams_match_golang_snappy(seed):
+    """The lane decoder flags exactly the records golang/snappy's Decode rejects (decode_other.go:
+    ErrCorrupt on a tag past the stream, a literal or copy past the output, offset 0 or beyond the
+    bytes produced, a decoded length other than the preamble's), with identical bytes for the rest,
+    and ReadNext's status sequence is the reference loop's."""
+    rng = random.Random(1000 + seed)
+    img = mutated_file(rng, 400)
+    o = orc.file_reader_decode_arrays(img)
+    assert o["n_bad"] > 0  # the damage reaches the codec
+    assert_same_as_oracle(gpu_decode_arrays(img), o, f"seed {seed}")
