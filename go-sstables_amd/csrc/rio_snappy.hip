@@ -75,14 +75,21 @@ __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
 __device__ __forceinline__ uint4 ld_far(const uint8_t* p) { return (RIO_NT & 2) ? ldu16_nt(p) : ldu16(p); }
 
 // RIO_BUF: the input prefetch and the flush store go through buffer descriptors (32-bit offsets from
-// the file / arena base, wave-uniform descriptors in SGPRs); a lane with nothing to load or store
-// passes an offset past the descriptor's range, which the range check drops (no sink line, no 64-bit
-// address arithmetic or pointer selects). The lane decoder only runs on files and arenas below
-// 0xFFFFFF00 bytes (snappy_wide), so every real offset fits 32 bits and kOob is out of range.
+// the wave's own file / arena base, wave-uniform descriptors in SGPRs); a lane with nothing to load or
+// store passes an offset past the descriptor's range, which the range check drops (no sink line, no
+// 64-bit address arithmetic or pointer selects). A wave's records span less than 0xF0000000 bytes of
+// file and arena (snappy_lane checks; a wave past that decodes its records one thread each), so every
+// real offset fits 32 bits and kOob is out of range, whatever the file's size.
 #ifndef RIO_BUF
 #define RIO_BUF 1
 #endif
 constexpr uint32_t kOob = 0xFFFFFFC0u;
+// lane k's 64-bit value (k wave-uniform) into scalars
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t k) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
+    return ((uint64_t)hi << 32) | lo;
+}
 typedef uint32_t v4u32b __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint64_t bytes) {
     const uint64_t v = (uint64_t)p;
@@ -96,7 +103,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
 
 // Files the 32-bit lane-stream positions cannot cover take the wave-per-record decoder.
 __device__ __forceinline__ bool snappy_wide(const FrameParams& P, const ScanState* st) {
+#if RIO_BUF
+    return st->huge_streams;  // per-wave buffer bases: any file and arena size (snappy_lane)
+#else
     return st->huge_streams || P.len >= 0xFFFFFF00ull || st->total_bytes >= 0xFFFFFF00ull;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -561,6 +572,30 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     const uint64_t base = start0 & ~15ull;
     const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
     const uint32_t lastc = live && base < P.len ? (uint32_t)umin((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
+#if RIO_BUF
+    {
+        // the wave's input and output spans from its lowest record to the end of lane 63's last one
+        // (records are consecutive in the file and the arena); past what 32-bit offsets reach (a
+        // chunk of very large records), each lane decodes its records one thread each instead
+        const uint64_t n = P.state->n_records;
+        const uint64_t end_in = r1 < n ? P.rec_off[r1] : P.len, end_out = P.out_off[umin(r1, n)];
+        const uint64_t b_in = rl64(base, 0u), b_out = rl64(o0, 0u);
+        const uint64_t s_in = rl64(end_in, 63u) - umin(b_in, rl64(end_in, 63u));
+        const uint64_t s_out = rl64(end_out, 63u) - umin(b_out, rl64(end_out, 63u));
+        if (s_in >= 0xF0000000ull || s_out >= 0xF0000000ull) {  // wave-uniform
+            bool okw = true;
+            for (uint64_t i = r0; i < r1; i++) {
+                if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) continue;
+                uint64_t st, sl;
+                rec_stream(P, i, st, sl);
+                const uint64_t a = P.out_off[i], z = P.out_off[i + 1];
+                okw = snappy_decode_thread(P.file + st, sl, out + a, z - a) && okw;
+            }
+            *bad_rec = r0;
+            return okw;
+        }
+    }
+#endif
     // prime the input image with chunks [0, 4)
     uint32_t whi = live ? umin(kInCh, lastc + 1) : 0u;
     for (uint32_t c = 0; c < whi; c++) {
@@ -585,13 +620,21 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     uint32_t d = 0, fb = 0;
 
 #if RIO_BUF
-    const __amdgpu_buffer_rsrc_t rsrc_file = uniform_rsrc(P.file, P.len + RIO_DEVICE_PAD);
-    const __amdgpu_buffer_rsrc_t rsrc_out = uniform_rsrc(P.out, P.state->total_bytes + 16);
-    const uint32_t base32 = (uint32_t)base, o32 = (uint32_t)o0;
+    // the buffer descriptors start at the wave's lowest record (lane 0's: a wave takes consecutive
+    // records), so the 32-bit offsets are relative to it and any file or arena size works; the arena
+    // base stays 16 bytes below the wave's first output byte (a far copy reads from q - r, r <= 3),
+    // except within the arena's first 16 bytes, where it is the arena itself (kLow's kind 3 covers q - r
+    // below it, as before)
+    const uint64_t w_in = rl64(base, 0u);
+    const uint64_t o0l = rl64(o0, 0u);
+    const uint64_t w_out = o0l >= 16 ? o0l - 16 : 0;
+    const __amdgpu_buffer_rsrc_t rsrc_file = uniform_rsrc(P.file + w_in, P.len + RIO_DEVICE_PAD - umin(w_in, P.len));
+    const __amdgpu_buffer_rsrc_t rsrc_out = uniform_rsrc(P.out + w_out, P.state->total_bytes + 16 - umin(w_out, P.state->total_bytes));
+    const uint32_t base32 = (uint32_t)(base - w_in), o32 = (uint32_t)(o0 - w_out);
     uint32_t obase[4];  // the flush owners' arena offsets
 #pragma unroll
     for (uint32_t jj = 0; jj < 4; jj++)
-        obase[jj] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * jj + (lane >> 2)) * 4), (int)(uint32_t)o0);
+        obase[jj] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * jj + (lane >> 2)) * 4), (int)o32);
 #else
     uint8_t* obase[4];
 #pragma unroll
