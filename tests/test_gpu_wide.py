@@ -125,6 +125,20 @@ def test_snappy_file_past_4gib():
     assert_same_as_oracle(g, o, "snappy >4GiB file")
 
 
+@pytest.mark.timeout(900)
+def test_snappy_wave_span_past_32_bits():
+    """70 Snappy records of 64 MiB: the first wave's 64 records span 4 GiB of arena, more than its 32-bit
+    buffer offsets reach, so that wave decodes its records one thread each (snappy_lane's span guard);
+    the last 6 records take the lane decoder. Byte for byte against the oracle."""
+    from recordio import generate
+
+    n = 70
+    img = generate(n, 64 << 20, 2, kind=1, seed=5, threads=16)
+    g = gpu_decode_arrays(img)
+    assert g["status"] == STATUS["EOF"] and g["n_records"] == n and g["total_out_bytes"] == n << 26
+    assert_same_as_oracle(g, orc.file_reader_decode_arrays(img), "64 MiB records")
+
+
 def _crc32c(data: bytes) -> int:
     c = 0xFFFFFFFF
     for b in data:
