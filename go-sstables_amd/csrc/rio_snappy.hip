@@ -573,7 +573,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
     const uint32_t lastc = live && base < P.len ? (uint32_t)umin((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
 #if RIO_BUF
-    {
+    // (only a file or arena of 3.75 GiB or more can hold such a wave: the common case skips the loads)
+    if (P.len >= 0xF0000000ull || P.state->total_bytes >= 0xF0000000ull) {
         // the wave's input and output spans from its lowest record to the end of lane 63's last one
         // (records are consecutive in the file and the arena); past what 32-bit offsets reach (a
         // chunk of very large records), each lane decodes its records one thread each instead
