@@ -545,7 +545,7 @@ __device__ __forceinline__ void col_hst(uint8_t* L, uint32_t a, uint32_t v) { co
 // copy there may need the kind-3 load from q (see the far-history load); every other wave has no
 // such lane and its far loads go through the arena descriptor.
 template <bool kMulti, bool kLow>
-__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint8_t* L,
+__device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint4 d0, uint64_t o0, uint8_t* L,
                                             uint32_t wave, uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
     const uint32_t wl = wave * 256u + lane * 4u;  // row 0 of this lane (both images)
     // history / input row of a byte position (mod the ring), and the next row with wrap
@@ -561,8 +561,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 
     const bool live = r0 < r1;
     uint8_t* const out = P.out;
-    const uint4 d0 = live ? P.rec_desc[r0] : zero4();
-    const uint64_t o0 = live ? P.out_off[r0] : 0;
+    // d0 / o0: rec_desc and out_off of r0, loaded by the caller (zero when !live)
     uint8_t* const gout = out + o0;
     // a far copy's 16 bytes are loaded from q - r: below the arena for a source in its first
     // bytes (only the lane of a file's first record can meet this: kind 3)
@@ -955,13 +954,16 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
         uint64_t bad_rec = 0;
         bool ok;
         // lane 0 holds the wave's lowest arena offset: a wave whose lanes all start at >= 3 never needs kind 3
-        const bool low = __shfl(r0 < r1 ? P.out_off[r0] : ~0ull, 0) < 3;
+        const bool live0 = r0 < r1;
+        const uint4 d0 = live0 ? P.rec_desc[r0] : zero4();
+        const uint64_t o0 = live0 ? P.out_off[r0] : 0;
+        const bool low = rl64(live0 ? o0 : ~0ull, 0u) < 3;
         if (rpc == 1)
-            ok = low ? snappy_lane<false, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
-                     : snappy_lane<false, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+            ok = low ? snappy_lane<false, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
+                     : snappy_lane<false, false>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
         else
-            ok = low ? snappy_lane<true, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
-                     : snappy_lane<true, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+            ok = low ? snappy_lane<true, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
+                     : snappy_lane<true, false>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
         if (!ok) {
             const uint32_t at = atomicAdd(&st->n_fail_lanes, 1u);
             if (at < kFailLanes) {
@@ -1004,13 +1006,16 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
             uint8_t* sink = P.sink + wg * 64;
             uint64_t bad_rec = 0;
             bool ok;
-            const bool low = __shfl(r0 < r1 ? P.out_off[r0] : ~0ull, 0) < 3;
+            const bool live0 = r0 < r1;
+            const uint4 d0 = live0 ? P.rec_desc[r0] : zero4();
+            const uint64_t o0 = live0 ? P.out_off[r0] : 0;
+            const bool low = rl64(live0 ? o0 : ~0ull, 0u) < 3;
             if (rpl == 1)
-                ok = low ? snappy_lane<false, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
-                         : snappy_lane<false, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+                ok = low ? snappy_lane<false, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
+                         : snappy_lane<false, false>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
             else
-                ok = low ? snappy_lane<true, true>(P, r0, r1, lds, wave, lane, sink, &bad_rec)
-                         : snappy_lane<true, false>(P, r0, r1, lds, wave, lane, sink, &bad_rec);
+                ok = low ? snappy_lane<true, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
+                         : snappy_lane<true, false>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
             if (!ok) {
                 const uint32_t at = atomicAdd(&P.state->n_fail_lanes, 1u);
                 if (at < kFailLanes) {
