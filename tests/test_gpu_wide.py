@@ -171,3 +171,15 @@ def test_uncompressed_record_of_4gib(size):
     assert g["status"] == STATUS["EOF"] and g["n_records"] == 1 and g["total_out_bytes"] == size
     assert int(g["rec_off"][0]) == 8 and int(g["out_off"][1]) == size
     assert np.array_equal(g["out"][:size], payload)
+
+
+@pytest.mark.timeout(900)
+def test_batch_with_a_file_past_4gib():
+    """rio_device_decode_batch over a 4.6 GB Snappy file and two small ones: the batched lane decoder
+    takes the big file too (per-wave buffer bases), each file exactly the oracle's."""
+    from recordio import generate
+    from test_gpu_batch import check_batch
+
+    big = generate(9_000_000, 1024, 2, kind=1, seed=4, threads=16)
+    assert big.shape[0] > FOUR_GIB
+    check_batch([generate(3000, 1024, 2, kind=1, seed=6), big, generate(200, 65536, 2, kind=1, seed=8)], "batch >4GiB")
