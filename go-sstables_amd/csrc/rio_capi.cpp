@@ -573,15 +573,19 @@ static int h2d_fill(rio_ctx* c, void* dst, uint64_t n, rio::FillFn fill, void* u
     return RIO_OK;
 }
 
+// `prefix` (prefix_len bytes, host) then `file` (len - prefix_len bytes): a window of a larger file
+// behind its file header (rio::frame_direct)
 static int frame_common(rio_ctx* ctx, uint64_t len, rio_file_info* info, const uint8_t* file, rio::FillFn fill,
-                        void* user) {
+                        void* user, const uint8_t* prefix = nullptr, uint64_t prefix_len = 0) {
     HIP_TRY(hipSetDevice(ctx->device));
     // the host API shares the ctx arenas with the device API: wait for a device-API call still
     // running on another stream, and make the next device-API call wait for this one
     if (int rc = order_before(ctx, ctx->stream)) return rc;
     ctx->framed = false;
     HIP_TRY(ctx->file.ensure(len + RIO_DEVICE_PAD));
-    int rc = fill ? h2d_fill(ctx, ctx->file.p, len, fill, user) : h2d_staged(ctx, ctx->file.p, file, len);
+    if (prefix_len) HIP_TRY(hipMemcpyAsync(ctx->file.p, prefix, prefix_len, hipMemcpyHostToDevice, ctx->stream));
+    int rc = fill ? h2d_fill(ctx, ctx->file.p, len, fill, user)
+                  : h2d_staged(ctx, ctx->file.as<uint8_t>() + prefix_len, file, len - prefix_len);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(ctx->file.as<uint8_t>() + len, 0, RIO_DEVICE_PAD, ctx->stream));
     FrameParams P;
@@ -651,7 +655,26 @@ int frame_fill(rio_ctx* ctx, uint64_t len, FillFn fill, void* user, rio_file_inf
     if (!ctx || !fill || !info) return RIO_ERR_ARG;
     return frame_common(ctx, len, info, nullptr, fill, user);
 }
+int frame_direct(rio_ctx* ctx, const uint8_t* prefix, uint64_t prefix_len, const uint8_t* src, uint64_t n,
+                 rio_file_info* info) {
+    if (!ctx || !info || (n && !src) || (prefix_len && !prefix)) return RIO_ERR_ARG;
+    return frame_common(ctx, prefix_len + n, info, src, nullptr, nullptr, prefix, prefix_len);
+}
+bool is_host_pinned(const void* p, uint64_t n) { return host_pinned(p, n); }
 }  // namespace rio
+
+// page-lock a caller's host buffer (a file image it reuses): the H2D of rio_frame / rio_stream_open_host
+// then reads it by DMA in place instead of through the staging pieces
+extern "C" int rio_host_register(const void* p, uint64_t n) {
+    if (!p || !n) return RIO_ERR_ARG;
+    HIP_TRY(hipHostRegister(const_cast<void*>(p), n, hipHostRegisterDefault));
+    return RIO_OK;
+}
+extern "C" int rio_host_unregister(const void* p) {
+    if (!p) return RIO_ERR_ARG;
+    HIP_TRY(hipHostUnregister(const_cast<void*>(p)));
+    return RIO_OK;
+}
 
 extern "C" int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, uint64_t* rec_off,
                           uint8_t* flags, uint64_t rec_cap, rio_file_info* info) {

@@ -93,5 +93,9 @@ class HostPool {
 // the windows of rio_stream: a synthetic file header followed by a byte range of the file).
 typedef int (*FillFn)(void* user, uint8_t* dst, uint64_t off, uint64_t n);
 int frame_fill(rio_ctx* ctx, uint64_t len, FillFn fill, void* user, rio_file_info* info);
+// rio_frame of prefix[0, prefix_len) + src[0, n): src page-locked (rio_host_register) is copied by DMA in place
+int frame_direct(rio_ctx* ctx, const uint8_t* prefix, uint64_t prefix_len, const uint8_t* src, uint64_t n,
+                 rio_file_info* info);
+bool is_host_pinned(const void* p, uint64_t n);
 
 }  // namespace rio

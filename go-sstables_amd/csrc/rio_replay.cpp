@@ -497,6 +497,7 @@ struct rio_stream {
     uint64_t window = 0;
     uint32_t depth = 4;
     int device = 0;
+    bool pinned = false;  // a host image the caller page-locked (rio_host_register): windows go by DMA in place
     // three contexts: window k+2 reads and frames while k and k+1 decode and copy out (VERDICT r3 #5:
     // the D2H of consecutive windows runs back to back)
     static constexpr int kCtx = 3;
@@ -552,7 +553,9 @@ struct rio_stream {
                 const uint64_t hl = whole ? 0 : RIO_FILE_HEADER_BYTES, n = hl + (e - s);
                 Fill f{&src, s, hdr, hl};
                 const double tf0 = kTrace ? now_ms() : 0.0;
-                if (int rc = rio::frame_fill(ctx[c], n, &Fill::fn, &f, &fi)) return post_fatal(k, rc);
+                if (int rc = pinned ? rio::frame_direct(ctx[c], hdr, hl, src.mem + s, e - s, &fi)
+                                    : rio::frame_fill(ctx[c], n, &Fill::fn, &f, &fi))
+                    return post_fatal(k, rc);
                 if (kTrace)
                     fprintf(stderr, "stream w%llu ctx%d: read+H2D+frame %llu B %.3f-%.3f ms\n", (unsigned long long)k, c,
                             (unsigned long long)n, tf0 - t_origin, now_ms() - t_origin);
@@ -667,6 +670,7 @@ extern "C" int rio_stream_open_host(int device, const uint8_t* data, uint64_t le
     auto* r = new rio_stream();
     r->src = Source{-1, data};
     r->len = len;
+    r->pinned = len && rio::is_host_pinned(data, len);
     return stream_start(r, device, window_bytes, depth, out);
 }
 

@@ -112,6 +112,8 @@ _SIGS = {
     "rio_ctx_release": (None, [c_void_p]),
     "rio_device_count": (c_int, [POINTER(c_int)]),
     "rio_frame": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(FileInfo)]),
+    "rio_host_register": (c_int, [c_void_p, c_uint64]),
+    "rio_host_unregister": (c_int, [c_void_p]),
     "rio_decode": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, POINTER(FileInfo)]),
     "rio_device_decode": (
         c_int,

@@ -170,6 +170,12 @@ void rio_ctx_release(rio_ctx* ctx);
 int rio_frame(rio_ctx* ctx, const uint8_t* file, uint64_t len, rio_file_info* info);
 int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, uint64_t* rec_off,
                uint8_t* flags, uint64_t rec_cap, rio_file_info* info);
+/* rio_host_register / rio_host_unregister: page-lock a host buffer the caller reuses for file images
+ * (hipHostRegister). rio_frame and rio_stream_open_host then copy such an image to the device by DMA
+ * in place instead of through the pinned staging pieces; results are the same either way. No
+ * reference counterpart: the cgo adapter would register its read buffer pool once. */
+int rio_host_register(const void* p, uint64_t n);
+int rio_host_unregister(const void* p);
 
 /* ---- device-resident API: the file is already in HBM; everything runs on `stream` with no host
  * synchronisation (graph-capturable). Outputs are device pointers with the layout above; the

@@ -27,12 +27,23 @@ GOLDEN = [os.path.join(HERE, "golden", d, f) for d in ("v4_compat", "v3_compat",
 NEVER = (1 << 64) - 1
 
 
-def stream_all(data: bytes, window: int, depth: int = 2, path: str | None = None):
+def stream_all(data: bytes, window: int, depth: int = 2, path: str | None = None, register: bool = False):
     """Every window of rio_stream over `data` (host memory) or `path`: records, file offsets, the
-    first_record of each window and the terminal info."""
+    first_record of each window and the terminal info. `register`: the host image is page-locked
+    (rio_host_register), so windows of 1 MiB and more are copied by DMA from it in place."""
     lib = L.lib()
     h = ctypes.c_void_p()
     buf = ctypes.create_string_buffer(data, len(data) + 1)
+    if register:
+        assert lib.rio_host_register(buf, len(data) + 1) == 0
+    try:
+        return _stream_all(lib, h, buf, data, window, depth, path)
+    finally:
+        if register:
+            assert lib.rio_host_unregister(buf) == 0
+
+
+def _stream_all(lib, h, buf, data, window, depth, path):
     if path:
         rc = lib.rio_stream_open(0, path.encode(), window, depth, ctypes.byref(h))
     else:
@@ -146,6 +157,46 @@ def test_path_source_and_depth(tmp_path):
     assert a == b
     exp = orc.file_reader_decode(data)
     assert a[0] == exp["records"]
+
+
+@pytest.mark.parametrize("window", [1 << 20, (3 << 20) + 17, 16 << 20, NEVER])
+def test_registered_host_image(window):
+    """A page-locked host image (rio_host_register): each window's bytes go to the device by DMA from
+    the image in place, behind the file header copied separately (rio::frame_direct). Same records,
+    offsets and status as the oracle and as the staged path."""
+    data = bytes(generate(40_000, 1024, 2, kind=1, seed=31))
+    check_stream(data, window, register=True)
+    damaged = bytearray(data)
+    damaged[len(data) // 2 + 5] ^= 0x40
+    check_stream(bytes(damaged), window, register=True)
+
+
+def test_registered_image_one_shot():
+    """rio_frame + rio_decode of a page-locked image equal those of the same bytes unregistered."""
+    import numpy as np
+
+    lib = L.lib()
+    img = generate(20_000, 1024, 2, kind=1, seed=32)
+    ctx = L.default_ctx(0)
+
+    def one_shot():
+        fi = L.FileInfo()
+        assert lib.rio_frame(ctx, img.ctypes.data, img.shape[0], ctypes.byref(fi)) == 0
+        n, nb = fi.n_records, fi.total_out_bytes
+        out, out_off = np.empty(nb + 16, np.uint8), np.empty(n + 1, np.uint64)
+        rec_off, flags = np.empty(n + 1, np.uint64), np.empty(n + 1, np.uint8)
+        assert lib.rio_decode(ctx, out.ctypes.data, out.shape[0], out_off.ctypes.data, rec_off.ctypes.data,
+                              flags.ctypes.data, n, ctypes.byref(fi)) == 0
+        return out[:nb].tobytes(), out_off.tobytes(), rec_off[:n].tobytes(), flags[:n].tobytes(), fi.status
+
+    plain = one_shot()
+    assert lib.rio_host_register(img.ctypes.data, img.shape[0]) == 0
+    try:
+        assert one_shot() == plain
+    finally:
+        assert lib.rio_host_unregister(img.ctypes.data) == 0
+    exp = orc.file_reader_decode_arrays(img)
+    assert plain[0] == exp["out"].tobytes() and plain[4] == exp["status"]
 
 
 def test_whole_file_when_smaller_than_window():

@@ -51,6 +51,8 @@ def test_stream_and_replay_argument_errors():
     assert lib.rio_stream_open(0, REPO.encode(), 0, 0, ctypes.byref(h)) == L.RIO_ERR_IO  # not a regular file
     assert not h.value
     assert lib.rio_stream_open_host(0, None, 5, 0, 0, ctypes.byref(h)) == L.RIO_ERR_ARG
+    assert lib.rio_host_register(None, 5) == L.RIO_ERR_ARG
+    assert lib.rio_host_unregister(None) == L.RIO_ERR_ARG
     assert lib.rio_stream_next(None, None, None, None, None, None, None) == L.RIO_ERR_ARG
     lib.rio_stream_free(None)
     assert lib.rio_replay_next(None, None, None, None, None, None) == L.RIO_ERR_ARG
