@@ -130,6 +130,141 @@ def host_cores() -> int:
     return max(1, min(n, share) if share else n)
 
 
+def device_digest(t) -> str:
+    """Position-sensitive digest of a device tensor's bytes, computed on the device (int64 word sums per
+    4096-word row, the row sums weighted by their index; the tail words and bytes separately). Used to
+    show that the timed steps rebuilt exactly the bytes the warmup produced."""
+    import torch
+
+    u8 = t.contiguous().view(torch.uint8).flatten()
+    n = u8.numel()
+    n8 = n // 8 * 8
+    w = u8[:n8].view(torch.int64)
+    rows = 4096
+    m = w.numel() // rows * rows
+    parts = [n]
+    if m:
+        rs = w[:m].view(-1, rows).sum(dim=1)
+        wt = torch.arange(1, rs.numel() + 1, device=t.device, dtype=torch.int64) * 2654435761
+        parts += [int(rs.sum().item()), int((rs * wt).sum().item())]
+    if w.numel() > m:
+        tail = w[m:]
+        wt = torch.arange(1, tail.numel() + 1, device=t.device, dtype=torch.int64) * 40503
+        parts += [int(tail.sum().item()), int((tail * wt).sum().item())]
+    if n > n8:
+        parts += [int(x) for x in u8[n8:].cpu().tolist()]
+    return "%x" % (hash(tuple(parts)) & (2**64 - 1))
+
+
+def source_tree_hash(root: str = HERE) -> str:
+    """sha1 of the product sources (go-sstables_amd/csrc/*.hip|*.cpp|*.h and include/*.h): the tree a
+    traffic file was measured on, recorded in it by scripts/traffic.py and compared here."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha1()
+    files = sorted(glob.glob(os.path.join(root, "go-sstables_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(root, "go-sstables_amd", "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(root, "go-sstables_amd", "csrc", "*.h")) +
+                   glob.glob(os.path.join(root, "include", "*.h")))
+    for f in files:
+        h.update(os.path.relpath(f, root).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def dominant_kernel(config: str, rec_len: int | None = None) -> str:
+    """The decode kernel the roofline is taken on for a decode config (rec_len: a test's override)."""
+    _, rl, comp, kind, _ = CONFIGS[config]
+    rec_len = rl if rec_len is None else rec_len
+    batch = config in MULTI_FILE
+    if comp == 2 and kind == 0:
+        return "k_copy_records"  # ref-random records are each one literal: the copy path decodes them
+    if comp == 2 and rec_len >= int(os.environ.get("RIO_COOP_MIN", str(1 << 56)), 0):
+        return "k_snappy_coop_batch" if batch else "k_snappy_coop"  # wave-per-record decoder (opt-in)
+    if comp == 2 and batch:
+        return "k_snappy_pipe_batch"
+    return DECODE_KERNEL[comp]
+
+
+def pmc_counter(root: str, name: str, kernel: str) -> tuple[float, int]:
+    """(max over dispatches, dispatch count) of one rocprofv3 counter for kernels whose name contains
+    `kernel` (the first decode launch is a capacity probe that decodes nothing: the max is a real one)."""
+    import csv
+    import glob
+
+    vals = []
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["Kernel_Name"] and row["Counter_Name"] == name:
+                    vals.append(float(row["Counter_Value"]))
+    return (max(vals), len(vals)) if vals else (float("nan"), 0)
+
+
+def live_traffic(config: str, timeout_s: float = 300.0) -> dict:
+    """HBM traffic of the dominant kernel measured now, on this box and this tree: two child runs of this
+    script (2 timed steps) under `rocprofv3 --kernel-trace --pmc <one counter>`, FETCH_SIZE and
+    WRITE_SIZE in separate passes (MI355X_MICROARCH.md, HBM / rocprofv3: KiB at the L2's memory side,
+    FETCH_SIZE doubled on gfx950). Started before this process touches the GPU. Returns the traffic
+    fields for `roofline`, or {"error": ...} when the profiler is missing or a pass fails."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return {"error": "rocprofv3 not found"}
+    kernel = dominant_kernel(config)
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="rio_pmc_", dir="/tmp")
+        cmd = [prof, "--kernel-trace", "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--config", config, "--steps", "2", "--warmup", "1",
+               "--no-cpu-baseline", "--no-e2e", "--traffic", "none"]
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env, cwd="/tmp",
+                             start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            shutil.rmtree(d, ignore_errors=True)
+            return {"error": f"{ctr} pass timed out after {timeout_s:.0f} s"}
+        v, k = pmc_counter(d, ctr, kernel)
+        shutil.rmtree(d, ignore_errors=True)
+        if rc != 0 or k == 0:
+            return {"error": f"{ctr} pass rc={rc}, {k} dispatches of {kernel}"}
+        vals[ctr] = v
+    read_b, write_b = 2.0 * vals["FETCH_SIZE"] * 1024, vals["WRITE_SIZE"] * 1024
+    return {"traffic": read_b + write_b, "traffic_read": read_b, "traffic_write": write_b,
+            "traffic_source": {"kind": "live", "tree": source_tree_hash(), "kernel": kernel,
+                               "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), max over dispatches, two "
+                                         "rocprofv3 --pmc passes of this script run by this bench invocation"}}
+
+
+def file_traffic(config: str, path: str | None) -> dict:
+    """Traffic from a committed PMC file (scripts/traffic.py output), with the tree it was measured on and
+    whether that is this tree."""
+    for tpath in ([path] if path else [os.path.join(HERE, "profiles", f"traffic_{config}.json"),
+                                       os.path.join(HERE, "profiles", "traffic_latest.json")]):
+        if tpath and os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath))
+            except (OSError, ValueError):
+                continue
+            if tj.get("config") == config:
+                now = source_tree_hash()
+                return {"traffic": tj.get("decode_kernel_bytes_per_launch"),
+                        "traffic_source": {"kind": "file", "path": os.path.relpath(tpath, HERE),
+                                           "tree": tj.get("tree"), "tree_now": now,
+                                           "same_tree": tj.get("tree") == now}}
+    return {"traffic": None}
+
+
 def cpu_baseline(images, rec_offs=None, n_records=None, budget_s: float = 20.0) -> dict:
     """The oracle (oracle/rio_oracle.c, a C restatement of the reference reader) on host cores, timed
     on a bounded sample of the same workload:
@@ -892,6 +1027,17 @@ class DeviceBackend:
     def infos(self):
         return [self.dec.info(b) for b in self.bufs]
 
+    def checksums(self):
+        """Device digests of every file's decoded arrays (out, out_off, rec_off, flags)."""
+        res = []
+        for b in self.bufs:
+            i = self.dec.info(b)
+            n, nb = i["n_records"], i["total_out_bytes"]
+            res.append((device_digest(b.out[:nb]), device_digest(b.out_off[:n + 1]), device_digest(b.rec_off[:n]),
+                        device_digest(b.flags[:n])))
+        self.sync()
+        return res
+
     def set_timing(self, slots: int):
         from recordio import _lib as L
 
@@ -948,6 +1094,8 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     for info in infos:
         if info["status"] != L.RIO_EOF or info["n_records"] != n_rec:
             raise RuntimeError(f"decode failed: {info}")
+    # the warmup's result: every later pass must rebuild exactly these bytes
+    digests = backend.checksums()
     length = sum(lengths)  # input bytes of this rank per step
     n = sum(i["n_records"] for i in infos)
     nb = sum(i["total_out_bytes"] for i in infos)
@@ -968,6 +1116,16 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     stage = backend.stage_ms()  # per-stage HIP-event means over the timed steps
     backend.set_timing(1)
 
+    def verify(what: str) -> None:
+        """The decode's result struct and a device-side digest of out / out_off / rec_off / flags after
+        `what`, against the warmup's: a step that went wrong fails the bench loudly."""
+        now_infos, now_dig = backend.infos(), backend.checksums()
+        if now_infos != infos or now_dig != digests:
+            raise RuntimeError(f"bench: the {what} decoded different results from the warmup: "
+                               f"{now_infos} / {now_dig} vs {infos} / {digests}")
+
+    verify("timed steps")
+
     value, ms_per_step, dt_max = job_throughput(dt, length, args.steps, world)
 
     # SURVEY §8d: when input + output fit the 256 MB MALL (C1), back-to-back steps re-read a warm
@@ -984,6 +1142,7 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
             backend.sync()
             cold = backend.stage_ms()
             backend.set_timing(1)
+            verify("MALL-flushed steps")
         cold_ms = sum(cold) if len(cold) == 4 else 0.0
         # whole job: every rank's bytes over the slowest rank's cold step
         cold_value, cold_step_ms, _ = job_throughput(cold_ms * 1e-3, length, 1, world)
@@ -1008,27 +1167,20 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     alg_bytes = length + nb + 8 * (n + len(lengths)) + 8 * n + n
     decode_ms = stage[3] if len(stage) == 4 else float("nan")
     achieved = alg_bytes / (decode_ms * 1e-3) / 1e9
-    traffic = None
-    # the config's own PMC file (profiles/traffic_<config>.json), else traffic_latest.json if it is this config's
-    for tpath in ([args.traffic_json] if args.traffic_json else
-                  [os.path.join(HERE, "profiles", f"traffic_{args.config}.json"),
-                   os.path.join(HERE, "profiles", "traffic_latest.json")]):
-        if traffic is None and os.path.exists(tpath):
-            try:
-                tj = json.load(open(tpath))
-                if tj.get("config") == args.config:
-                    traffic = tj.get("decode_kernel_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
-    pipe_ms = sum(stage) if stage else float("nan")
-    if comp == 2 and kind == 0:
-        kernel = "k_copy_records"  # ref-random records are each one literal: the copy path decodes them
-    elif comp == 2 and rec_len >= int(os.environ.get("RIO_COOP_MIN", str(1 << 56)), 0):
-        kernel = "k_snappy_coop_batch" if batch else "k_snappy_coop"  # wave-per-record decoder (opt-in)
-    elif comp == 2 and batch:
-        kernel = "k_snappy_pipe_batch"
+    # HBM traffic of the dominant kernel: measured by this invocation (main() ran the PMC passes before
+    # the GPU was touched), else the committed PMC file with the tree it was measured on, else none
+    live = getattr(args, "live_traffic", None)
+    if live and "traffic" in live:
+        tr = live
+    elif getattr(args, "traffic", "live") == "none":
+        tr = {"traffic": None}
     else:
-        kernel = DECODE_KERNEL[comp]
+        tr = file_traffic(args.config, args.traffic_json)
+        if live and "error" in live:
+            tr["traffic_live_error"] = live["error"]
+    traffic = tr.get("traffic")
+    pipe_ms = sum(stage) if stage else float("nan")
+    kernel = dominant_kernel(args.config, rec_len)
     total_files = MULTI_FILE[args.config][0] if batch else world
     line = {
         "metric": METRIC,
@@ -1051,7 +1203,14 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
                    "parallelism": f"file-sharded x{world} ({total_files} files), no data-path collectives"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": kernel,
-                     "kernel_ms": round(decode_ms, 4), "alg_bytes_per_launch": alg_bytes},
+                     "kernel_ms": round(decode_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                     **{k: v for k, v in tr.items() if k != "traffic"}},
+        # every pass after the warmup (the timed steps, the MALL-flushed steps) rebuilt the warmup's result
+        # struct and the same device-side digest of out / out_off / rec_off / flags (verify() above)
+        "verified": True,
+        "verify": {"method": "rio_file_info + device digest of out, out_off, rec_off, flags: warmup vs after "
+                             "the timed steps (and after the MALL-flushed pass)",
+                   "digest_out": digests[0][0] if digests else None},
         "stages_ms": {"walk": round(stage[0], 4), "scan": round(stage[1], 4), "place": round(stage[2], 4),
                       "decode": round(stage[3], 4)} if len(stage) == 4 else None,
         "pipeline_roofline_frac": round(alg_bytes / (pipe_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if stage else None,
@@ -1127,6 +1286,9 @@ def main(argv: list[str] | None = None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic file (default: profiles/traffic_<config>.json, then traffic_latest.json)")
+    ap.add_argument("--traffic", default="live", choices=["live", "file", "none"],
+                    help="roofline.traffic: measured by this run (two rocprofv3 --pmc passes, 1 GPU only), the "
+                         "committed PMC file, or none")
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
     rc = launch_contract(args.gpus, argv)
@@ -1137,6 +1299,13 @@ def main(argv: list[str] | None = None):
     assert world == args.gpus
     import numpy as np  # noqa: F401
     import torch
+
+    # the PMC passes run as child processes before this one touches the GPU (decode configs, one GPU;
+    # torch.cuda.device_count() does not initialise HIP on this image)
+    args.live_traffic = None
+    if (args.traffic == "live" and world == 1 and args.config not in ("c5", "wal", "idx", "enc", "readat")
+            and torch.cuda.device_count() > 0):
+        args.live_traffic = live_traffic(args.config)
 
     device = make_device(local)
     if world > 1:

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -277,7 +278,9 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     auto* c = new rio_ctx();
     c->device = device;
     c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 32768);
-    if (c->chunk_bytes < 64 || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
+    // k_walk's candidate bounds take 32-bit differences inside a chunk (magic_mask): chunks stay below
+    // 1 GiB; anything outside [64, 1 GiB] or not a multiple of 16 falls back to the default
+    if (c->chunk_bytes < 64 || c->chunk_bytes > (1ull << 30) || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
     c->coop_min = env_u64("RIO_COOP_MIN", ~0ull >> 8);  // k_snappy_coop: wide files only
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -483,13 +486,50 @@ static int ensure_pinned(rio_ctx* c) {
     return RIO_OK;
 }
 
-// true when [p, p + n) is page-locked host memory HIP knows (hipHostMalloc / hipHostRegister): the
-// copy then goes by DMA directly, without the staging pieces. The probe's error on pageable memory
-// is cleared so a later hipGetLastError (kernel launch check) does not see it.
+// Page-locked host ranges this library knows: rio_host_register's ranges and PinnedPool's
+// blocks, base -> bytes. A DMA straight from host memory needs ALL of [p, p + n) page-locked; a
+// pointer attribute only describes p itself.
+namespace {
+std::mutex g_pin_mu;
+std::map<uintptr_t, uint64_t> g_pin;
+bool pinned_known(uintptr_t a, uint64_t n) {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pin.upper_bound(a);
+    if (it == g_pin.begin()) return false;
+    --it;
+    return a >= it->first && a - it->first <= it->second && n <= it->second - (a - it->first);
+}
+}  // namespace
+namespace rio {
+void note_pinned(const void* p, uint64_t n) {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pin[reinterpret_cast<uintptr_t>(p)] = n;
+}
+void forget_pinned(const void* p) {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pin.erase(reinterpret_cast<uintptr_t>(p));
+}
+}  // namespace rio
+
+// true when all of [p, p + n) is page-locked host memory: a range this library registered or
+// allocated, or one allocation HIP reports (hipHostMalloc / hipHostRegister by the caller) that
+// covers the whole range. The copy then goes by DMA directly, without the staging pieces; anything
+// else (a partly registered image, a range running past its registration) takes the staging path.
+// The probes' errors on pageable memory are cleared so a later hipGetLastError (kernel launch
+// check) does not see them.
 static bool host_pinned(const void* p, uint64_t n) {
     if (!p || n < (1u << 20)) return false;  // small copies: staging costs nothing
-    hipPointerAttribute_t a{};
-    const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if (pinned_known(a, n)) return true;
+    hipPointerAttribute_t at{};
+    bool ok = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+    if (ok) {
+        void* base = nullptr;
+        size_t sz = 0;
+        ok = hipMemGetAddressRange(&base, &sz, const_cast<void*>(p)) == hipSuccess && base &&
+             reinterpret_cast<uintptr_t>(base) <= a && a - reinterpret_cast<uintptr_t>(base) <= sz &&
+             n <= sz - (a - reinterpret_cast<uintptr_t>(base));
+    }
     (void)hipGetLastError();
     return ok;
 }
@@ -668,10 +708,12 @@ bool is_host_pinned(const void* p, uint64_t n) { return host_pinned(p, n); }
 extern "C" int rio_host_register(const void* p, uint64_t n) {
     if (!p || !n) return RIO_ERR_ARG;
     HIP_TRY(hipHostRegister(const_cast<void*>(p), n, hipHostRegisterDefault));
+    rio::note_pinned(p, n);
     return RIO_OK;
 }
 extern "C" int rio_host_unregister(const void* p) {
     if (!p) return RIO_ERR_ARG;
+    rio::forget_pinned(p);
     HIP_TRY(hipHostUnregister(const_cast<void*>(p)));
     return RIO_OK;
 }

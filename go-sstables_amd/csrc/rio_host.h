@@ -97,5 +97,8 @@ int frame_fill(rio_ctx* ctx, uint64_t len, FillFn fill, void* user, rio_file_inf
 int frame_direct(rio_ctx* ctx, const uint8_t* prefix, uint64_t prefix_len, const uint8_t* src, uint64_t n,
                  rio_file_info* info);
 bool is_host_pinned(const void* p, uint64_t n);
+// page-locked host ranges the library itself knows (rio_host_register, PinnedPool blocks)
+void note_pinned(const void* p, uint64_t n);
+void forget_pinned(const void* p);
 
 }  // namespace rio

@@ -635,7 +635,8 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
     if (c) {
         // positions [a, b) of the 16 are inside [lo, hi): lo and hi lie within 2^31 bytes of q (one
         // chunk's window, lo < hi), so 32-bit differences clamped to [0, 16] give a <= b; the three
-        // magic bytes must lie in the file: i + 2 < len - q (64-bit: the file may extend far past q)
+        // magic bytes must lie in the file: i + 2 < len - q (64-bit: the file may extend far past q);
+        // rio_ctx_create caps chunks at 1 GiB, which keeps lo and hi that close
         auto clamp16 = [](int32_t x) { return (uint32_t)(x < 0 ? 0 : (x > 16 ? 16 : x)); };
         const uint32_t a = clamp16((int32_t)((uint32_t)lo - (uint32_t)q));
         const uint32_t b = clamp16((int32_t)((uint32_t)hi - (uint32_t)q));

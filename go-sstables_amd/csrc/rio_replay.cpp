@@ -69,6 +69,7 @@ class PinnedPool {
             (void)hipGetLastError();
             return nullptr;
         }
+        rio::note_pinned(p, n);
         cap = n;
         return p;
     }
@@ -76,6 +77,7 @@ class PinnedPool {
         if (!p) return;
         std::lock_guard<std::mutex> g(mu_);
         if (cached_ + cap > kMaxCached) {
+            rio::forget_pinned(p);
             (void)hipHostFree(p);
             return;
         }

@@ -490,6 +490,17 @@ namespace {
 #ifndef RIO_EXP_OCC
 #define RIO_EXP_OCC 0
 #endif
+#if RIO_EXP_OCC && !defined(RIO_TIMING_ONLY_BUILD)
+#error "RIO_EXP_OCC produces wrong output: build it only as a timing experiment (-DRIO_TIMING_ONLY_BUILD)"
+#endif
+// RIO_EXP_MEM (timing-only, WRONG output; the control flow does not depend on output bytes): bit 0 sends the
+// flush stores out of range, bit 1 the far-history loads (measures what each stream costs the decoder)
+#ifndef RIO_EXP_MEM
+#define RIO_EXP_MEM 0
+#endif
+#if RIO_EXP_MEM && !defined(RIO_TIMING_ONLY_BUILD)
+#error "RIO_EXP_MEM produces wrong output: build it only as a timing experiment (-DRIO_TIMING_ONLY_BUILD)"
+#endif
 constexpr uint32_t kColRows = RIO_EXP_OCC ? 32 : 64;  // history rows per lane: 256 bytes
 constexpr uint32_t kColInRows = 16;                // input rows per lane: 64 bytes = kInCh chunks
 constexpr uint32_t kColWaves = kSnappyBlock / 64;
@@ -627,6 +638,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     // below it, as before)
     const uint64_t w_in = rl64(base, 0u);
     const uint64_t o0l = rl64(o0, 0u);
+    // lane 0 is the wave's lowest record (see the INVARIANT at k_snappy_pipe)
+#ifdef RIO_DEBUG_LANES
+    if (live && (base < w_in || o0 < o0l)) __builtin_trap();
+#endif
     const uint64_t w_out = o0l >= 16 ? o0l - 16 : 0;
     const __amdgpu_buffer_rsrc_t rsrc_file = uniform_rsrc(P.file + w_in, P.len + RIO_DEVICE_PAD - umin(w_in, P.len));
     const __amdgpu_buffer_rsrc_t rsrc_out = uniform_rsrc(P.out + w_out, P.state->total_bytes + 16 - umin(w_out, P.state->total_bytes));
@@ -816,7 +831,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 #if RIO_BUF
         {
             const v4u32b w = {fv_now.x, fv_now.y, fv_now.z, fv_now.w};
-            __builtin_amdgcn_raw_buffer_store_b128(w, rsrc_out, (ofb_now >> 31) ? obase[j & 3u] + fpos_now : kOob, 0,
+            __builtin_amdgcn_raw_buffer_store_b128(w, rsrc_out, ((ofb_now >> 31) && !(RIO_EXP_MEM & 1)) ? obase[j & 3u] + fpos_now : kOob, 0,
                                                    (RIO_NT & 1) ? 2 : 0);
         }
 #else
@@ -833,7 +848,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 #if RIO_BUF
             if constexpr (!kMulti && !kLow) {
                 // no descriptor to fetch and no source below the arena: the arena descriptor alone
-                const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, S.kind == 2 ? o32 + qsrc - r : kOob, 0,
+                const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, (S.kind == 2 && !(RIO_EXP_MEM & 2)) ? o32 + qsrc - r : kOob, 0,
                                                                       (RIO_NT & 2) ? 2 : 0);
                 S.aux = make_uint4(v.x, v.y, v.z, v.w);
             } else
@@ -930,6 +945,12 @@ __device__ __forceinline__ bool pipe_active(const FrameParams& P) {
            !snappy_wide(P, st) && !(st->n_records && st->total_bytes / st->n_records >= P.coop_min);
 }
 
+// INVARIANT (both launch sites, k_snappy_pipe and k_snappy_pipe_batch): the lanes of a wave
+// take consecutive, ascending records (lane l's first record = the wave's first + l * records per lane),
+// so lane 0 holds the wave's lowest file offset (base) and arena offset (o0), and lane 63's last record
+// ends the wave's spans. snappy_lane's kLow choice (rl64(o0, 0) < 3), its buffer bases (rl64(base, 0),
+// rl64(o0, 0)) and its span guard all rely on it: a strided or load-balanced record-to-lane mapping
+// would need the minimum over the live lanes instead. RIO_DEBUG_LANES checks it at run time.
 __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kColLds];
     ScanState* st = P.state;
@@ -953,7 +974,8 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
         const uint64_t r0 = umin(chunk * per + lane * rpc, n), r1 = umin(r0 + rpc, n);
         uint64_t bad_rec = 0;
         bool ok;
-        // lane 0 holds the wave's lowest arena offset: a wave whose lanes all start at >= 3 never needs kind 3
+        // lane 0 holds the wave's lowest arena offset (consecutive ascending records per lane, the
+        // INVARIANT above): a wave whose lanes all start at >= 3 never needs kind 3
         const bool live0 = r0 < r1;
         const uint4 d0 = live0 ? P.rec_desc[r0] : zero4();
         const uint64_t o0 = live0 ? P.out_off[r0] : 0;
@@ -1001,6 +1023,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
         if (!pipe_active(P)) continue;
         const uint64_t n = P.state->n_records, wf = (n + per_wave - 1) / per_wave;
         if (wg < w0 + wf) {
+            // consecutive ascending records per lane (the INVARIANT at k_snappy_pipe)
             const uint64_t t = ((wg - w0) << 6) | lane;
             const uint64_t r0 = umin(t * rpl, n), r1 = umin(r0 + rpl, n);
             uint8_t* sink = P.sink + wg * 64;

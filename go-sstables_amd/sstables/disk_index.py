@@ -42,8 +42,8 @@ def _error(status: int, version: int = 0) -> GoError:
     if status == L.RIO_ERR_UNSUPPORTED:
         if version < 2:  # a v1 index: every probe's SeekNext fails (mmap_reader.go:62-64)
             return GoError("unsupported on files with version lower than v2")
-        # v2+ compressed index: a probe whose SeekNext walk ends at a trial outside the decoded
-        # sequence is handed back by the device search
+        # (v2+: DiskKeyIndex.lookups answers these probes on the host reader; this text is reached
+        # only if that reader itself hands a probe back)
         return GoError("rio: SeekNext probe ends outside the decoded record sequence (unsupported on the device)")
     from recordio.reader import _base_error
 
@@ -99,12 +99,59 @@ class DiskKeyIndex:
             raise GoError(f"rio_index_search: {L.strerror(rc)}")
         return [(h.offset, bool(h.found), h.value_offset, h.checksum, h.status) for h in hits]
 
+    def lookups(self, keys) -> list:
+        """(offset, found, value_offset, checksum, err) per key: the device search, except that a key
+        whose probe the device hands back (RIO_ERR_UNSUPPORTED on a v2+ compressed index: a SeekNext
+        walk that ends outside the decoded record sequence) is searched again on the host
+        reader with the reference's own loop, so Get / Contains / the iterators answer
+        where the reference answers."""
+        keys = [bytes(k) for k in keys]
+        out = []
+        for k, (off, found, vo, cs, st) in zip(keys, self.search(keys)):
+            if st == L.RIO_ERR_UNSUPPORTED and self.version >= 2:
+                out.append(self._host_search(k))
+            else:
+                out.append((off, found, vo, cs, _error(st, self.version) if st else None))
+        return out
+
+    def _host_search(self, target: bytes):
+        """DiskKeyIndex.binarySearch + findAt (disk_key_index.go:88-139) with every probe a SeekNext of
+        the MMapReader mirror and proto.Unmarshal of its record (mmap_proto_reader.go:26-38), as a
+        freshly loaded index (no offsetCache)."""
+        from .proto import decode_index_entry
+
+        n = self.size
+
+        def find_at(h):
+            _, rec, err = self._reader.SeekNext(h)
+            if err is not None:
+                return None, err
+            try:
+                return decode_index_entry(rec or b""), None
+            except ValueError:
+                return None, GoError("proto: cannot parse invalid wire-format data")
+
+        i, j = 0, n
+        while i < j:
+            h = (i + j) >> 1
+            at, err = find_at(h)
+            if err is not None:
+                return (n, False, 0, 0, None) if errors_is(err, EOF) else (0, False, 0, 0, err)
+            if at[0] < target:
+                i = h + 1
+            else:
+                j = h
+        at, err = find_at(i)
+        if err is not None:
+            return (n, False, 0, 0, None) if errors_is(err, EOF) else (0, False, 0, 0, err)
+        return i, i < n and at[0] == target, at[1], at[2], None
+
     def GetBatch(self, keys):  # noqa: N802
         """[(IndexVal, err)] per key, Get's semantics."""
         out = []
-        for off, found, vo, cs, st in self.search(keys):
-            if st:
-                out.append((IndexVal(), _error(st, self.version)))
+        for off, found, vo, cs, err in self.lookups(keys):
+            if err is not None:
+                out.append((IndexVal(), err))
             elif not found:
                 out.append((IndexVal(), NotFound))
             else:
@@ -115,24 +162,24 @@ class DiskKeyIndex:
         return self.GetBatch([key])[0]
 
     def Contains(self, key):  # noqa: N802
-        off, found, _, _, st = self.search([key])[0]
-        return (False, _error(st, self.version)) if st else (found, None)
+        off, found, _, _, err = self.lookups([key])[0]
+        return (False, err) if err is not None else (found, None)
 
     def Iterator(self):  # noqa: N802
         return _DiskKeyIndexIterator(self._reader, 8, self.size), None
 
     def IteratorStartingAt(self, key):  # noqa: N802
-        off, _, _, _, st = self.search([key])[0]
-        if st:
-            return None, _error(st, self.version)
+        off, _, _, _, err = self.lookups([key])[0]
+        if err is not None:
+            return None, err
         return _DiskKeyIndexIterator(self._reader, off, self.size), None
 
     def IteratorBetween(self, lo, hi):  # noqa: N802
         if bytes(lo) > bytes(hi):
             return None, GoError("keyHigher is lower than keyLower")
-        (s, _, _, _, st1), (e, found, _, _, st2) = self.search([lo, hi])
-        if st1 or st2:
-            return None, _error(st1 or st2, self.version)
+        (s, _, _, _, e1), (e, found, _, _, e2) = self.lookups([lo, hi])
+        if e1 is not None or e2 is not None:
+            return None, e1 if e1 is not None else e2
         if not found:
             e -= 1  # keyHigher is inclusive
         return _DiskKeyIndexIterator(self._reader, s, e), None

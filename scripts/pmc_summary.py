@@ -1,4 +1,6 @@
-"""Summarise rocprofv3 counter CSVs: per kernel (substring match), mean counter value per dispatch.
+"""Summarise rocprofv3 counter CSVs: per kernel (substring match), mean counter value per dispatch, and the mean
+over the real launches (the smallest dispatch dropped when there are 3 or more: bench.py's decode runs one
+capacity-probe dispatch of ~no work before its timed launches).
 usage: python scripts/pmc_summary.py <dir> [kernel-substring ...]"""
 import collections, csv, glob, sys
 
@@ -13,5 +15,7 @@ for path in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=Tru
                 acc[p][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for p, ctrs in acc.items():
     print(p)
+    print(f"  {'counter':32s} {'mean':>16s} {'real-launch mean':>18s}")
     for c, v in sorted(ctrs.items()):
-        print(f"  {c:32s} {sum(v) / len(v):16.4g}  (n={len(v)})")
+        real = sorted(v)[1:] if len(v) >= 3 else v
+        print(f"  {c:32s} {sum(v) / len(v):16.4g} {sum(real) / len(real):18.4g}  (n={len(v)})")

@@ -10,7 +10,11 @@ usage: python scripts/traffic.py <fetch_pass_dir> <write_pass_dir> <config> <ker
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_tree_hash  # noqa: E402  (the tree this file was measured on)
 
 
 def counter(root, name, kernel):
@@ -40,6 +44,7 @@ def main():
         "hbm_write_bytes": write_bytes,
         "decode_kernel_bytes_per_launch": read_bytes + write_bytes,
         "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), max over dispatches, separate --pmc passes",
+        "tree": source_tree_hash(),
     }
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(doc))

@@ -250,6 +250,43 @@ def test_compressed_index_ending_in_a_partial_marker(comp, tail):
     assert all(g[0] != L.RIO_ERR_UNSUPPORTED for g in got)
 
 
+@pytest.mark.parametrize("comp", [1, 2, 3])
+def test_handed_back_probes_answered_on_the_host(tmp_path, comp):
+    """A compressed index whose record 200 has a damaged header (its CRC no longer matches): FileReader,
+    and so the handle's decoded view, stops there, while the reference's SeekNext steps over it and reads
+    on (mmap_reader.go:105-110). The device hands back the probes that land past it
+    (RIO_ERR_UNSUPPORTED); DiskKeyIndex answers them with the reference's binarySearch on the host
+    reader, so Get / Contains / IteratorStartingAt agree with the oracle for every query."""
+    rng = random.Random(40 + comp)
+    keys = [be(3 * i) for i in range(400)]
+    img = bytearray(index_image(entries_for(keys), comp))
+    ro = orc.file_reader_decode(bytes(img))["rec_off"]
+    img[ro[200] + 4] ^= 0x01  # record 200's u: its header CRC no longer matches
+    img = bytes(img)
+    qs = queries_for(keys, rng, 60)
+    assert any(g[0] == L.RIO_ERR_UNSUPPORTED for g in handle_hits(img, qs))
+    p = tmp_path / "index.rio"
+    p.write_bytes(img)
+    idx, err = DiskIndexLoader().Load(str(p), None)
+    assert err is None and idx.Open() is None
+    try:
+        got = idx.lookups(qs)
+        for q, (off, found, vo, cs, err), (v, gerr) in zip(qs, got, idx.GetBatch(qs)):
+            o = orc.disk_index_search(img, q, 4096)  # (status, offset, found, value offset, checksum)
+            if o[0] != 0:
+                assert err is not None and "rio:" not in str(err), (q, o, err)
+                continue
+            assert err is None and (off, found) == (o[1], o[2]), (q, o, off, found)
+            if found:
+                assert gerr is None and v == IndexVal(o[3], o[4])
+                assert idx.Contains(q) == (True, None)
+            else:
+                assert gerr is NotFound
+        assert sum(1 for g in got if g[1]) >= 300
+    finally:
+        idx.Close()
+
+
 @pytest.mark.parametrize("version", [3, 2, 1])
 def test_older_version_indexes_match_oracle(version):
     """index.rio with the v3 / v2 / v1 header layouts: SeekNext-driven binarySearch on v3 / v2 as on v4;

@@ -97,6 +97,12 @@ class OracleBackend:
     def set_timing(self, slots):
         pass
 
+    def checksums(self):
+        import hashlib
+
+        return [tuple(hashlib.sha1(r[k].tobytes()).hexdigest()[:16] for k in ("out", "out_off", "rec_off", "flags"))
+                for r in self.res]
+
     def stage_ms(self):
         return [0.01, 0.01, 0.01, 0.1] if self.images else []
 
@@ -152,7 +158,32 @@ def test_bench_run_decode_world2(config, files_per_rank):
         assert steps == 1 + 1 + 3 + 3 and "mall_flushed" in line
         assert line["n_gpus"] == 2 and line["config"]["files_this_rank"] == files_per_rank
         assert line["config"]["records"] == 150 * files_per_rank
+        assert line["verified"] is True and line["verify"]["digest_out"]
     assert got[0][2]["value"] == got[1][2]["value"] > 0
+
+
+class _DriftingBackend(OracleBackend):
+    """An oracle backend whose timed steps produce different bytes (a decode that went wrong)."""
+
+    def step(self):
+        super().step()
+        if self.steps > 2:
+            self.res[0]["out"][0] ^= 0xFF
+
+
+def test_bench_fails_when_timed_steps_diverge():
+    """The headline is self-verifying: a timed step whose output differs from the
+    warmup's makes run_decode raise instead of reporting a line."""
+    import argparse
+
+    import bench
+
+    args = argparse.Namespace(config="c2", steps=3, warmup=1, no_cpu_baseline=True, no_e2e=True,
+                              traffic_json="/nonexistent")
+    with pytest.raises(RuntimeError, match="different results"):
+        bench.run_decode(args, 1, 0, _DriftingBackend(), sizes=(150, 2048))
+    line = bench.run_decode(args, 1, 0, OracleBackend(), sizes=(150, 2048))
+    assert line["verified"] is True and line["roofline"]["traffic"] is None
 
 
 def _bench_cli(args, env_extra=None, timeout=300):
