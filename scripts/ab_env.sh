@@ -9,7 +9,7 @@ for r in 1 2; do
     v=0
     for e in "$@"; do
       v=$((v + 1))
-      env $e timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-e2e \
+      env $e timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --traffic none \
           > "$OUT/b_${c}_v${v}_$r.log" 2>&1
       rc=$?; [ $rc -ne 0 ] && { echo "bench $c [$e] rc=$rc"; tail -5 "$OUT/b_${c}_v${v}_$r.log"; exit $rc; }
       grep '^{' "$OUT/b_${c}_v${v}_$r.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$c [$e]', d['value'], d['stages_ms'])"

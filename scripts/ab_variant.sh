@@ -12,7 +12,7 @@ for r in 1 2; do
   for c in $CFGS; do
     for v in base $V; do
       if [ $v = base ]; then LIBP=$PWD/go-sstables_amd/librio.so; else LIBP=$VLIB; fi
-      RIO_LIB_PATH=$LIBP timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > "$OUT/b_${c}_${v}_$r.log" 2>&1
+      RIO_LIB_PATH=$LIBP timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --traffic none > "$OUT/b_${c}_${v}_$r.log" 2>&1
       rc=$?; [ $rc -ne 0 ] && { echo "bench $c $v rc=$rc"; tail -5 "$OUT/b_${c}_${v}_$r.log"; exit $rc; }
       grep '^{' "$OUT/b_${c}_${v}_$r.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$c $v', d['value'], d['stages_ms'])"
     done

@@ -3,7 +3,7 @@
 set -u
 for c in $1; do
   for k in $2; do
-    out=$(RIO_CHUNK_BYTES=$k timeout -k 10 180 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-e2e 2>&1 | grep '^{')
+    out=$(RIO_CHUNK_BYTES=$k timeout -k 10 180 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --traffic none 2>&1 | grep '^{')
     echo "$c $k $(echo "$out" | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['stages_ms'], d['value'])")"
   done
 done

@@ -8,7 +8,7 @@ i=0
 for set in "$@"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d "$OUT/pmc$i" -o run --output-format csv -- \
-      python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > "$OUT/pmc$i.log" 2>&1
+      python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none > "$OUT/pmc$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && tail -20 "$OUT/pmc$i.log" && exit $rc
 done
 echo done

@@ -29,20 +29,20 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --config "$CFG"
 grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
 step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python bench.py --config "$CFG" --no-cpu-baseline --no-e2e
+    python bench.py --config "$CFG" --no-cpu-baseline --no-e2e --traffic none
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 python scripts/kstats.py "$OUT/prof" "$OUT/kernel_launches.json" > /dev/null  # per launch, probe dispatch excluded
 step pmc_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-    python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 step pmc_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-    python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config "$CFG" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 python scripts/traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$CFG" k_snappy_pipe "$OUT/traffic.json"
 # C4's decode-kernel traffic (roofline.traffic of the c4 line: profiles/traffic_c4.json)
 if [ -z "${SKIP_C4_PMC:-}" ]; then
 step pmc_fetch_c4 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch_c4" -o run --output-format csv -- \
-    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 step pmc_write_c4 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write_c4" -o run --output-format csv -- \
-    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 python scripts/traffic.py "$OUT/pmc_fetch_c4" "$OUT/pmc_write_c4" c4 k_snappy_pipe_batch "$OUT/traffic_c4.json"
 fi
 # the SSTable line (SURVEY config 5) and its kernel trace

@@ -13,18 +13,18 @@ step() {
 step bench 600 python bench.py --config c2
 grep '^{' "$OUT/bench.log" > "$OUT/bench.json" || true
 step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python bench.py --config c2 --no-cpu-baseline --no-e2e
+    python bench.py --config c2 --no-cpu-baseline --no-e2e --traffic none
 find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 python scripts/kstats.py "$OUT/prof" "$OUT/kernel_launches.json" > /dev/null
 step pmc_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-    python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 step pmc_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-    python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 python scripts/traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" c2 k_snappy_pipe "$OUT/traffic.json"
 step pmc_fetch_c4 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch_c4" -o run --output-format csv -- \
-    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 step pmc_write_c4 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_write_c4" -o run --output-format csv -- \
-    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e
+    python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --traffic none
 python scripts/traffic.py "$OUT/pmc_fetch_c4" "$OUT/pmc_write_c4" c4 k_snappy_pipe_batch "$OUT/traffic_c4.json"
 for c in ${PROFILE_LINES:-c3 c4 c1 c2r}; do
     step bench_$c 600 python bench.py --config $c

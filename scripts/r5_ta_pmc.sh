@@ -28,7 +28,7 @@ for v in $LIBS; do
     echo "$v pass $i:$ctr" | tee -a "$OUT/passes.txt"
     [ -z "$ctr" ] && continue
     RIO_LIB_PATH=$LIBP timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctr -d "$OUT/$v/pmc$i" -o run --output-format csv -- \
-        python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > "$OUT/${v}_pmc$i.log" 2>&1
+        python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none > "$OUT/${v}_pmc$i.log" 2>&1
     rc=$?; echo "$v pass $i rc=$rc"; [ $rc -ne 0 ] && tail -20 "$OUT/${v}_pmc$i.log" && exit $rc
   done
   python3 scripts/pmc_summary.py "$OUT/$v" k_snappy_pipe k_walk > "$OUT/${v}_summary.txt" 2>&1; echo "== $v"; cat "$OUT/${v}_summary.txt"
