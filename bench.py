@@ -989,11 +989,13 @@ class DeviceBackend:
     """The device call of a decode step: rio_device_decode (one file) or rio_device_decode_batch
     (a file set) on this rank's GPU, files resident in HBM, outputs preallocated."""
 
-    def __init__(self, local: int, device):
+    def __init__(self, local: int, device, own: bool = False):
+        """own: a context and a stream of its own (in-process multi-device mode, where host threads
+        drive the backends concurrently and a device may be listed twice)."""
         from recordio.device import DeviceDecoder
 
-        self.local, self.device = local, device
-        self.dec = DeviceDecoder(local)
+        self.local, self.device, self.own = local, device, own
+        self.dec = DeviceDecoder(local, own_ctx=own)
 
     def load(self, images, batch: bool):
         import torch
@@ -1004,7 +1006,7 @@ class DeviceBackend:
         self.batch = batch
         # the header's compression type (the host has the image): only that codec's kernels launch
         self.comp = int(images[0][4]) if images and len(images[0]) >= 8 else None
-        self.stream = torch.cuda.current_stream(self.device)
+        self.stream = torch.cuda.Stream(self.device) if self.own else torch.cuda.current_stream(self.device)
         if batch:
             self.bufs = [b for b, _ in self.dec.decode_batch(self.files)] if self.files else []
         else:
@@ -1022,7 +1024,10 @@ class DeviceBackend:
     def sync(self):
         import torch
 
-        torch.cuda.synchronize(self.device)
+        if self.own:
+            self.stream.synchronize()
+        else:
+            torch.cuda.synchronize(self.device)
 
     def infos(self):
         return [self.dec.info(b) for b in self.bufs]
@@ -1229,6 +1234,108 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     return line
 
 
+def lpt_assign(sizes: list[int], n_dev: int) -> list[list[int]]:
+    """Longest processing time first: file indices per device, each file (largest first) to the device
+    with the fewest bytes so far (ties: the lower device slot). rio_fileset_decode's rule (rio.h)."""
+    load = [0] * n_dev
+    out: list[list[int]] = [[] for _ in range(n_dev)]
+    for i in sorted(range(len(sizes)), key=lambda k: (-sizes[k], k)):
+        d = min(range(n_dev), key=lambda k: (load[k], k))
+        out[d].append(i)
+        load[d] += sizes[i]
+    return [sorted(x) for x in out]
+
+
+def run_decode_inproc(args, devices: list[int], make_be, sizes=None) -> dict:
+    """The in-process multi-device shape a Go caller has (rio_fileset_*): ONE process,
+    one host thread and one backend (its own context and stream) per listed device, the config's files
+    assigned longest-first (lpt_assign). Files are resident in HBM before the timed region, as in
+    run_decode; the threads start each timed loop together (a barrier) and value = all files' bytes x
+    steps / the wall time until the last thread's device is idle. Every backend's result is verified
+    after the timed loop as in run_decode. A device may be listed twice (one-GPU rehearsal)."""
+    import threading
+
+    from recordio import _lib as L
+    from recordio import generate
+
+    n_rec, rec_len, comp, kind, desc = CONFIGS[args.config]
+    if sizes:
+        n_rec, rec_len = sizes
+    threads = min(16, os.cpu_count() or 1)
+    batch = args.config in MULTI_FILE
+    nd = len(devices)
+    seeds = ([MULTI_FILE[args.config][1] + f for f in range(MULTI_FILE[args.config][0])] if batch
+             else [rank_seed(i) for i in range(nd)])
+    images = [generate(n_rec, rec_len, comp, kind=kind, seed=sd, threads=threads) for sd in seeds]
+    plan = lpt_assign([len(img) for img in images], nd)
+    bes = [make_be(devices[k]) for k in range(nd)]
+    lengths = [sum(be.load([images[i] for i in plan[k]], batch) or [0]) if plan[k] else 0 for k, be in enumerate(bes)]
+    for be, part in zip(bes, plan):
+        if part:
+            for _ in range(args.warmup):
+                be.step()
+            be.sync()
+    infos = [be.infos() if part else [] for be, part in zip(bes, plan)]
+    for inf in infos:
+        for i in inf:
+            if i["status"] != L.RIO_EOF or i["n_records"] != n_rec:
+                raise RuntimeError(f"decode failed: {i}")
+    digests = [be.checksums() if part else [] for be, part in zip(bes, plan)]
+    for be, part in zip(bes, plan):
+        if part:
+            be.set_timing(args.steps)
+    bar = threading.Barrier(nd + 1)
+    ends = [0.0] * nd
+    errs: list = []
+
+    def drive(k):
+        try:
+            bar.wait()
+            if plan[k]:
+                for _ in range(args.steps):
+                    bes[k].step()
+                bes[k].sync()
+            ends[k] = time.perf_counter()
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+            ends[k] = time.perf_counter()
+
+    ths = [threading.Thread(target=drive, args=(k,)) for k in range(nd)]
+    for t in ths:
+        t.start()
+    bar.wait()
+    t0 = time.perf_counter()
+    for t in ths:
+        t.join()
+    if errs:
+        raise errs[0]
+    dt = max(ends) - t0
+    stage = bes[0].stage_ms() if plan[0] else []
+    for k, (be, part) in enumerate(zip(bes, plan)):
+        if part:
+            be.set_timing(1)
+            if be.infos() != infos[k] or be.checksums() != digests[k]:
+                raise RuntimeError(f"bench: device slot {k}'s timed steps decoded different results from its warmup")
+    total = sum(lengths)
+    value = total * args.steps / 2**30 / dt
+    n = sum(i["n_records"] for inf in infos for i in inf)
+    nb = sum(i["total_out_bytes"] for inf in infos for i in inf)
+    return {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": nd, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong" if batch else "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: seeded text-like Zipf-word records (snappy ratio ~0.55)",
+        "config": {"workload": desc, "records": n, "record_bytes": rec_len, "file_bytes": total, "decoded_bytes": nb,
+                   "parallelism": f"in-process: one host thread + context + stream per device, {len(images)} files "
+                                  f"assigned longest-first, no collectives",
+                   "devices": devices, "files_per_device": [len(p) for p in plan]},
+        "stages_ms_device0": ({"walk": round(stage[0], 4), "scan": round(stage[1], 4), "place": round(stage[2], 4),
+                               "decode": round(stage[3], 4)} if len(stage) == 4 else None),
+        "verified": True,
+        "mode": "inproc" + (" (rehearsal: a device listed more than once)" if len(set(devices)) < nd else ""),
+    }
+
+
 def _free_port() -> int:
     import socket
 
@@ -1271,9 +1378,16 @@ def make_device(local: int):
     return torch.device(f"cuda:{local}")
 
 
-def make_backend(local: int, device):
+def make_backend(local: int, device, own: bool = False):
     """The decode configs' device call (tests/bench_cli_oracle.py substitutes the CPU oracle)."""
-    return DeviceBackend(local, device)
+    return DeviceBackend(local, device, own=own)
+
+
+def make_inproc_device(local: int):
+    """A device of the in-process mode (no set_device: the threads share the process)."""
+    import torch
+
+    return torch.device(f"cuda:{local}")
 
 
 def main(argv: list[str] | None = None):
@@ -1286,6 +1400,9 @@ def main(argv: list[str] | None = None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic file (default: profiles/traffic_<config>.json, then traffic_latest.json)")
+    ap.add_argument("--inproc-devices", default=None,
+                    help="in-process multi-device mode: a device list (\"0,1,2,3\", or N for 0..N-1); one process, "
+                         "one host thread per device (the Go caller's shape, INTEGRATION.md §2.2)")
     ap.add_argument("--traffic", default="live", choices=["live", "file", "none"],
                     help="roofline.traffic: measured by this run (two rocprofv3 --pmc passes, 1 GPU only), the "
                          "committed PMC file, or none")
@@ -1299,6 +1416,13 @@ def main(argv: list[str] | None = None):
     assert world == args.gpus
     import numpy as np  # noqa: F401
     import torch
+
+    if args.inproc_devices:
+        spec = args.inproc_devices
+        devices = [int(x) for x in spec.split(",")] if "," in spec else list(range(int(spec)))
+        line = run_decode_inproc(args, devices, lambda d: make_backend(d, make_inproc_device(d), own=True))
+        print(json.dumps(line), flush=True)
+        return
 
     # the PMC passes run as child processes before this one touches the GPU (decode configs, one GPU;
     # torch.cuda.device_count() does not initialise HIP on this image)

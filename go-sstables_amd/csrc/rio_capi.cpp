@@ -174,6 +174,9 @@ struct rio_ctx {
     std::vector<std::array<hipEvent_t, 5>> ev;
     uint64_t ev_cursor = 0;
     uint64_t chunk_bytes = 32768;
+    // framing by k_walk_lane (RIO_WALK_LANE=1): one lane per chunk of lane_chunk_bytes (RIO_LANE_CHUNK_BYTES)
+    uint32_t walk_lane = 0;
+    uint64_t lane_chunk_bytes = 4096;
     uint64_t coop_min = ~0ull >> 8;
     hipEvent_t* next_events() {
         if (ev.empty()) return nullptr;
@@ -226,12 +229,14 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     memset(&P, 0, sizeof P);
     P.file = d_file;
     P.len = len;
-    P.chunk_bytes = ctx->chunk_bytes;
+    const uint64_t cb = ctx->walk_lane ? ctx->lane_chunk_bytes : ctx->chunk_bytes;
+    P.walk_lane = ctx->walk_lane;
+    P.chunk_bytes = cb;
     P.coop_min = ctx->coop_min;
     P.comp_hint = RIO_COMP_UNKNOWN;
     P.zero_done = 0;
-    P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + ctx->chunk_bytes - 1) / ctx->chunk_bytes : 0;
-    P.slots = ctx->chunk_bytes / 5 + 1;  // records starting in a chunk: the smallest is v2's 5 bytes
+    P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + cb - 1) / cb : 0;
+    P.slots = cb / 5 + 1;  // records starting in a chunk: the smallest is v2's 5 bytes
     P.n_blocks = (P.n_chunks + 255) / 256;
     const uint64_t nc = std::max<uint64_t>(P.n_chunks, 1), nb = std::max<uint64_t>(P.n_blocks, 1);
     HIP_TRY(A.scratch_off.ensure(nc * P.slots * 8));
@@ -281,6 +286,10 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     // k_walk's candidate bounds take 32-bit differences inside a chunk (magic_mask): chunks stay below
     // 1 GiB; anything outside [64, 1 GiB] or not a multiple of 16 falls back to the default
     if (c->chunk_bytes < 64 || c->chunk_bytes > (1ull << 30) || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
+    c->walk_lane = env_u64("RIO_WALK_LANE", 0) ? 1u : 0u;
+    c->lane_chunk_bytes = env_u64("RIO_LANE_CHUNK_BYTES", 4096);
+    if (c->lane_chunk_bytes < 64 || c->lane_chunk_bytes > (1ull << 30) || (c->lane_chunk_bytes & 15))
+        c->lane_chunk_bytes = 4096;
     c->coop_min = env_u64("RIO_COOP_MIN", ~0ull >> 8);  // k_snappy_coop: wide files only
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;

@@ -480,7 +480,8 @@ __device__ uint64_t find_entry(const FrameParams& P, uint64_t cs, uint64_t ce, u
 
 // Continue walking chunk c from record start p (count/bytes already in s), filling its scratch
 // slots; sets s.exit / s.status. Serial header-to-header hops (FileReader order).
-__device__ void walk_from(const FrameParams& P, uint64_t c, uint64_t p, uint32_t ver, uint32_t comp, ChunkSum& s) {
+__device__ void walk_from(const FrameParams& P, uint64_t c, uint64_t p, uint32_t ver, uint32_t comp, ChunkSum& s,
+                          const uint32_t* crct = nullptr) {
     const uint64_t ce = chunk_end(P, c);
     uint64_t* so = P.scratch_off + c * P.slots;
     uint64_t* sl = P.scratch_len + c * P.slots;
@@ -488,7 +489,7 @@ __device__ void walk_from(const FrameParams& P, uint64_t c, uint64_t p, uint32_t
     while (p < ce) {
         Hdr h;
         uint64_t next = 0, olen = 0, pd = 0, lf = 0;
-        int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd, lf);
+        int e = frame_record(P.file, P.len, p, ver, comp, h, next, olen, pd, lf, crct);
         if (e) {
             s.status = e;
             s.err_off = p;
@@ -816,6 +817,64 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
             s.exit = p;  // the chain left the chunk (or ended at the file end) cleanly
         P.chunks[c] = s;
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Lane walk (round 5, RIO_WALK_LANE): one LANE per chunk (small chunks, 4 KiB by default), the serial
+// FileReader walk of find_entry + walk_chunk with the memory access shaped for a lane:
+//   * entry search: 64 bytes per step as four aligned 16-byte loads issued together (plus the next
+//     dword), candidates from magic_mask (0x91 bytes, then the 3-byte test), each framed by
+//     frame_record; the first that frames is the chunk's speculative entry (as find_entry);
+//   * then header to header: each hop is ONE round trip (frame_record's two 16-byte loads, header
+//     parsed in registers, CRC-32C from the LDS slice-by-4 table) and the payload is never read.
+// Slots and ChunkSum are the serial walk's, so the scan, the repair and the placement are unchanged.
+// Against the wave-per-chunk walk (k_walk) it reads ~64 bytes per record instead of every byte, and
+// its framing work is per record, not per candidate window; its cost is one dependent round trip per
+// record per lane, covered by the lanes of ~2 waves per SIMD.
+// ------------------------------------------------------------------------------------------
+__device__ uint64_t find_entry_lane(const FrameParams& P, uint64_t cs, uint64_t ce, uint32_t ver, uint32_t comp,
+                                    const uint32_t* crct) {
+    const uint8_t* f = P.file;
+    const uint32_t m3 = magic3(ver);
+    for (uint64_t q0 = cs & ~15ull; q0 < ce; q0 += 64) {
+        // 64 + 4 bytes from q0 (16-B aligned: the 64 lie inside the padded file, q0 < len, pad 64; the
+        // next dword only when it starts inside the file)
+        const uint4 a = *reinterpret_cast<const uint4*>(f + q0);
+        const uint4 b = *reinterpret_cast<const uint4*>(f + q0 + 16);
+        const uint4 cc = *reinterpret_cast<const uint4*>(f + q0 + 32);
+        const uint4 d = *reinterpret_cast<const uint4*>(f + q0 + 48);
+        const uint32_t t = q0 + 64 < P.len ? *reinterpret_cast<const uint32_t*>(f + q0 + 64) : 0u;
+        const uint32_t w0[5] = {a.x, a.y, a.z, a.w, b.x}, w1[5] = {b.x, b.y, b.z, b.w, cc.x};
+        const uint32_t w2[5] = {cc.x, cc.y, cc.z, cc.w, d.x}, w3[5] = {d.x, d.y, d.z, d.w, t};
+        const uint64_t m = (uint64_t)magic_mask(w0, q0, cs, ce, P.len, m3) |
+                           ((uint64_t)magic_mask(w1, q0 + 16, cs, ce, P.len, m3) << 16) |
+                           ((uint64_t)magic_mask(w2, q0 + 32, cs, ce, P.len, m3) << 32) |
+                           ((uint64_t)magic_mask(w3, q0 + 48, cs, ce, P.len, m3) << 48);
+        uint64_t mm = m;
+        while (mm) {
+            const uint64_t p = q0 + (uint64_t)__builtin_ctzll(mm);
+            mm &= mm - 1;
+            Hdr h;
+            uint64_t nx, ol, pd, lf;
+            if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd, lf, crct) == RIO_OK) return p;
+        }
+    }
+    return kNone;
+}
+
+constexpr uint32_t kWalkLaneBlock = 256;
+__global__ void __launch_bounds__(kWalkLaneBlock) k_walk_lane(FrameParams P) {
+    __shared__ uint32_t crct[1024];
+    if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
+    crc32c_tab_init(crct);
+    const uint64_t c = (uint64_t)blockIdx.x * kWalkLaneBlock + threadIdx.x;
+    uint32_t ver, comp;
+    if (c >= P.n_chunks || file_header_status(P, ver, comp) != RIO_OK) return;
+    const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
+    const uint64_t from = c == 0 ? (uint64_t)RIO_FILE_HEADER_BYTES : find_entry_lane(P, cs, ce, ver, comp, crct);
+    ChunkSum s = chunk_sum_empty(from);
+    if (from != kNone) walk_from(P, c, from, ver, comp, s, crct);
+    P.chunks[c] = s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1899,7 +1958,10 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
 // Framing: k_walk (file header, state reset, chunk walk), k_scan_blocks (both scan levels).
 hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], s);
-    hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
+    if (P.walk_lane)
+        hipLaunchKernelGGL(k_walk_lane, dim3(blocks_for(P.n_chunks, kWalkLaneBlock)), dim3(kWalkLaneBlock), 0, s, P);
+    else
+        hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
     if (ev) (void)hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
     if (ev) (void)hipEventRecord(ev[2], s);

@@ -54,9 +54,23 @@ def header_codec(img) -> int | None:
 
 
 class DeviceDecoder:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, own_ctx: bool = False):
+        """own_ctx: a context of its own (rio_ctx_create) instead of the device's shared default one, so
+        several decoders on one device can be driven from different host threads."""
         self.device = device
-        self.ctx = L.default_ctx(device)
+        if own_ctx:
+            h = ctypes.c_void_p()
+            rc = L.lib().rio_ctx_create(device, ctypes.byref(h))
+            if rc != L.RIO_OK:
+                raise RuntimeError(f"rio_ctx_create(device={device}): {L.strerror(rc)}")
+            self.ctx, self._own = h.value, True
+        else:
+            self.ctx, self._own = L.default_ctx(device), False
+
+    def __del__(self):
+        if getattr(self, "_own", False) and self.ctx:
+            L.lib().rio_ctx_destroy(self.ctx)
+            self.ctx = None
 
     def alloc(self, n_records: int, total_bytes: int) -> DecodeBuffers:
         dev = f"cuda:{self.device}"

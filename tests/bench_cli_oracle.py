@@ -26,7 +26,9 @@ def main():
 
     sizes = tuple(int(x) for x in os.environ.get("RIO_BENCH_TEST_SIZES", "150,2048").split(","))
     bench.make_device = lambda local: torch.device("cpu")
-    bench.make_backend = lambda local, device: OracleBackend()
+    bench.make_backend = lambda local, device, own=False: OracleBackend()
+    bench.make_inproc_device = lambda local: torch.device("cpu")
+    bench.run_decode_inproc = functools.partial(bench.run_decode_inproc, sizes=sizes)
     bench.run_decode = functools.partial(bench.run_decode, sizes=sizes)
     bench.main()
 

@@ -215,6 +215,35 @@ def test_bench_gpus2_without_launcher_self_launches(config, files_per_rank):
     assert line["value"] > 0
 
 
+def test_lpt_assign():
+    """Longest-first assignment (rio_fileset_decode's rule): equal files alternate, a big file gets a
+    device of its own, ties go to the lower slot."""
+    import bench
+
+    assert bench.lpt_assign([10] * 8, 2) == [[0, 2, 4, 6], [1, 3, 5, 7]]
+    assert bench.lpt_assign([100, 10, 10, 10, 10, 60], 2) == [[0], [1, 2, 3, 4, 5]]
+    assert bench.lpt_assign([5, 5, 5], 4) == [[0], [1], [2], []]
+    assert sorted(sum(bench.lpt_assign([7, 3, 9, 1, 4], 3), [])) == [0, 1, 2, 3, 4]
+
+
+@pytest.mark.parametrize("config,per_dev", [("c4", [4, 4]), ("c2", [1, 1])])
+def test_bench_inproc_devices(config, per_dev):
+    """`bench.py --inproc-devices 0,0`: one process, one thread and backend per listed device (the Go
+    caller's shape), C4's 8 files split 4 / 4, the line verified; device 0 listed twice is the
+    one-GPU rehearsal and says so."""
+    import json
+
+    r = _bench_cli(["--inproc-devices", "0,0", "--config", config, "--steps", "2", "--warmup", "1",
+                    "--no-cpu-baseline", "--no-e2e"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["config"]["devices"] == [0, 0]
+    assert line["config"]["files_per_device"] == per_dev
+    assert line["verified"] is True and "rehearsal" in line["mode"] and line["value"] > 0
+
+
 def test_bench_world_size_mismatch_refused():
     """A launcher's WORLD_SIZE that disagrees with --gpus is refused (non-zero exit), not reported."""
     r = _bench_cli(["--gpus", "4", "--steps", "1", "--warmup", "0"],
