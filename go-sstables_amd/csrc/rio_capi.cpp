@@ -174,9 +174,13 @@ struct rio_ctx {
     std::vector<std::array<hipEvent_t, 5>> ev;
     uint64_t ev_cursor = 0;
     uint64_t chunk_bytes = 32768;
-    // framing by k_walk_lane (RIO_WALK_LANE=1): one lane per chunk of lane_chunk_bytes (RIO_LANE_CHUNK_BYTES)
-    uint32_t walk_lane = 0;
-    uint64_t lane_chunk_bytes = 4096;
+    // framing walk (RIO_WALK_LANE): 0 k_walk (one wave per chunk_bytes chunk), 1 k_walk_lane (one lane per
+    // lane_chunk_bytes chunk, RIO_LANE_CHUNK_BYTES), 2 auto (default): the lane walk when the context's
+    // previous decode had records of kLaneWalkMin..kLaneWalkMax bytes on average (walk_hint, written by
+    // that decode's finalize_info into page-locked host memory: no host synchronisation), else the wave walk
+    uint32_t walk_mode = 2;
+    uint64_t lane_chunk_bytes = 16384;
+    uint64_t* walk_hint = nullptr;
     uint64_t coop_min = ~0ull >> 8;
     hipEvent_t* next_events() {
         if (ev.empty()) return nullptr;
@@ -225,12 +229,28 @@ struct rio_ctx {
     rio_file_info frame_info{};
 };
 
+// mean bytes per record for which the auto walk takes k_walk_lane (round 5 A/B on MI355X, 16 KiB lane chunks:
+// 1 KiB incompressible records walk 0.269 -> 0.142 ms; 560-byte records even; 48-byte and 36 KiB records
+// slower, so those keep k_walk)
+constexpr uint64_t kLaneWalkMin = 768, kLaneWalkMax = 8192, kLaneWalkChunks = 32768;
+
 static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P, FileArenas& A) {
     memset(&P, 0, sizeof P);
     P.file = d_file;
     P.len = len;
-    const uint64_t cb = ctx->walk_lane ? ctx->lane_chunk_bytes : ctx->chunk_bytes;
-    P.walk_lane = ctx->walk_lane;
+    // the lane walk reads ~64 bytes per record and is latency-bound per lane; the wave walk reads every
+    // byte (HBM-bound on records of ~1 KiB and more) and frames candidates 64 at a time (the better one for
+    // small records, and for very large ones, whose chunks hold no header and the lane walk scans)
+    // (and only with lanes to fill the chip: a file of fewer than kLaneWalkChunks lane chunks leaves the lane
+    // walk's one-chain-per-lane latency exposed, C1's 103 MB: walk 0.076 -> 0.179 ms)
+    bool lane = ctx->walk_mode == 1;
+    if (ctx->walk_mode == 2 && ctx->walk_hint && len / ctx->lane_chunk_bytes >= kLaneWalkChunks) {
+        const uint64_t m = *reinterpret_cast<volatile uint64_t*>(ctx->walk_hint);
+        lane = m >= kLaneWalkMin && m <= kLaneWalkMax;
+    }
+    const uint64_t cb = lane ? ctx->lane_chunk_bytes : ctx->chunk_bytes;
+    P.walk_lane = lane ? 1u : 0u;
+    P.walk_hint = ctx->walk_hint;
     P.chunk_bytes = cb;
     P.coop_min = ctx->coop_min;
     P.comp_hint = RIO_COMP_UNKNOWN;
@@ -286,10 +306,16 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     // k_walk's candidate bounds take 32-bit differences inside a chunk (magic_mask): chunks stay below
     // 1 GiB; anything outside [64, 1 GiB] or not a multiple of 16 falls back to the default
     if (c->chunk_bytes < 64 || c->chunk_bytes > (1ull << 30) || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
-    c->walk_lane = env_u64("RIO_WALK_LANE", 0) ? 1u : 0u;
-    c->lane_chunk_bytes = env_u64("RIO_LANE_CHUNK_BYTES", 4096);
+    c->walk_mode = (uint32_t)std::min<uint64_t>(env_u64("RIO_WALK_LANE", 2), 2);
+    c->lane_chunk_bytes = env_u64("RIO_LANE_CHUNK_BYTES", 16384);
     if (c->lane_chunk_bytes < 64 || c->lane_chunk_bytes > (1ull << 30) || (c->lane_chunk_bytes & 15))
-        c->lane_chunk_bytes = 4096;
+        c->lane_chunk_bytes = 16384;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->walk_hint), sizeof(uint64_t), hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        c->walk_hint = nullptr;  // no hint: the wave walk
+    } else {
+        *c->walk_hint = 0;
+    }
     c->coop_min = env_u64("RIO_COOP_MIN", ~0ull >> 8);  // k_snappy_coop: wide files only
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -322,6 +348,7 @@ extern "C" void rio_ctx_destroy(rio_ctx* c) {
         if (c->pin_ev[i]) hipEventDestroy(c->pin_ev[i]);
     }
     c->set_ring(0);
+    if (c->walk_hint) hipHostFree(c->walk_hint);
     hipStreamDestroy(c->stream);
     delete c;
 }

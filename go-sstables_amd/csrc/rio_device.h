@@ -132,6 +132,8 @@ struct FrameParams {
     uint32_t comp_hint;
     uint32_t zero_done;  // the zero-tail check already ran (host API phase A): k_place skips it
     uint32_t walk_lane;  // framing by k_walk_lane (one lane per chunk) instead of k_walk (one wave per chunk)
+    uint64_t* walk_hint; // page-locked host word: the decode's mean bytes per record (finalize_info), read by
+                         // the context when it picks the next decode's walk (null: not recorded)
     uint32_t redo;       // redo round of this codec (RIO_COMP_GZIP: k_gz_resize onwards, RIO_COMP_LZW:
                          // k_lzw_resize onwards; 0: first round): the kernel exits unless the file is
                          // that codec's and its resize kernel ran

@@ -239,21 +239,14 @@ __device__ void crc32c_tab_init(uint32_t* T) {
 // at most 4096 bytes (oracle ORC_LZW_MAX_RATIO). k_lzw_decode counts and re-places any other size.
 __device__ __forceinline__ uint64_t lzw_size(uint64_t u, uint64_t plen) { return u <= 4096ull * plen ? u : 0; }
 
-// FileReader sequential semantics at record start p: header + payload availability + decoded
-// size. next = start of the following record; pay = rec_pay descriptor (rio_device.h).
-// Common records (canonical magic, header + preamble inside 32 bytes, valid) are parsed from two
-// 16-byte loads; everything else (and every failure, for its exact classification) takes the
-// byte-wise ReadUvarint restatement.
-// A payload whose codec preamble / size already fails (snappy: unusable preamble; gzip: empty, too
-// short, or an ISIZE no DEFLATE stream reaches) frames normally: FileReader consumed it, and its
-// ReadNext fails without ending the file. `lflags` then carries kBadBit / kEofBit and out_len 0.
-__device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t ver, uint32_t comp,
-                            Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay, uint64_t& lflags,
-                            const uint32_t* crct = nullptr) {
-    lflags = 0;
-    if (p + 32 <= len) {
-        const uint4 a = ldu16(f + p), b = ldu16(f + p + 16);
-        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+// The fast path of frame_record on the 32 bytes at p already in registers (w; p + 32 <= len): RIO_OK
+// with the record framed (lflags 0), or kFrameSlow when the record needs the byte-wise path below.
+constexpr int kFrameSlow = -1000;
+__device__ __forceinline__ int frame_fast(const uint32_t (&w)[8], uint64_t len, uint64_t p, uint32_t ver, uint32_t comp,
+                                          Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay,
+                                          const uint32_t* crct) {
+    const uint4 a = make_uint4(w[0], w[1], w[2], w[3]), b = make_uint4(w[4], w[5], w[6], w[7]);
+    {
         if (ver == RIO_VERSION1 ? a.x == RIO_MAGIC : (a.x & 0xFFFFFFu) == 0x4C8D91u) {
             // v3 / v4: the nil byte at 3, the sizes from 4; v2: no nil byte (readRecordHeaderV2)
             // v1: fixed 20 bytes, LE u64 sizes at 4 and 12 (readRecordHeaderV1)
@@ -322,6 +315,14 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
             }
         }
     }
+    return kFrameSlow;
+}
+
+// The byte-wise path of frame_record (ReadUvarint restatement): every record the fast path does not take,
+// and every failure's exact classification.
+__device__ int frame_slow(const uint8_t* f, uint64_t len, uint64_t p, uint32_t ver, uint32_t comp, Hdr& h,
+                          uint64_t& next, uint64_t& out_len, uint64_t& pay, uint64_t& lflags) {
+    lflags = 0;
     uint64_t cap = ver == RIO_VERSION4 ? RIO_RECORD_HEADER_V4_MAX : ~0ull;
     int e = parse_header(f, p, len - p, cap, ver, h);
     if (e) return e;
@@ -375,6 +376,26 @@ __device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t
     }
     pay = ((plen - k) << 8) | (h.hdr_len + k);
     return RIO_OK;
+}
+
+// FileReader sequential semantics at record start p: header + payload availability + decoded
+// size. next = start of the following record; pay = rec_pay descriptor (rio_device.h).
+// Common records (canonical magic, header + preamble inside 32 bytes, valid) are parsed from two
+// 16-byte loads; everything else (and every failure, for its exact classification) takes the
+// byte-wise ReadUvarint restatement.
+// A payload whose codec preamble / size already fails (snappy: unusable preamble; gzip: empty, too
+// short, or an ISIZE no DEFLATE stream reaches) frames normally: FileReader consumed it, and its
+// ReadNext fails without ending the file. `lflags` then carries kBadBit / kEofBit and out_len 0.
+__device__ int frame_record(const uint8_t* f, uint64_t len, uint64_t p, uint32_t ver, uint32_t comp,
+                            Hdr& h, uint64_t& next, uint64_t& out_len, uint64_t& pay, uint64_t& lflags,
+                            const uint32_t* crct = nullptr) {
+    lflags = 0;
+    if (p + 32 <= len) {
+        const uint4 a = ldu16(f + p), b = ldu16(f + p + 16);
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        if (frame_fast(w, len, p, ver, comp, h, next, out_len, pay, crct) == RIO_OK) return RIO_OK;
+    }
+    return frame_slow(f, len, p, ver, comp, h, next, out_len, pay, lflags);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -836,21 +857,32 @@ __device__ uint64_t find_entry_lane(const FrameParams& P, uint64_t cs, uint64_t 
                                     const uint32_t* crct) {
     const uint8_t* f = P.file;
     const uint32_t m3 = magic3(ver);
-    for (uint64_t q0 = cs & ~15ull; q0 < ce; q0 += 64) {
-        // 64 + 4 bytes from q0 (16-B aligned: the 64 lie inside the padded file, q0 < len, pad 64; the
-        // next dword only when it starts inside the file)
-        const uint4 a = *reinterpret_cast<const uint4*>(f + q0);
-        const uint4 b = *reinterpret_cast<const uint4*>(f + q0 + 16);
-        const uint4 cc = *reinterpret_cast<const uint4*>(f + q0 + 32);
-        const uint4 d = *reinterpret_cast<const uint4*>(f + q0 + 48);
-        const uint32_t t = q0 + 64 < P.len ? *reinterpret_cast<const uint32_t*>(f + q0 + 64) : 0u;
+    // 64 + 4 bytes from q0 (16-B aligned: the 64 lie inside the padded file, q0 < len, pad 64; the next
+    // dword only when it starts inside the file); the next step's bytes are loaded before this step's
+    // candidates are tested, so the scan has two steps of loads in flight
+    auto fetch = [&](uint64_t q, uint4& a, uint4& b, uint4& c, uint4& d, uint32_t& t) __attribute__((always_inline)) {
+        a = *reinterpret_cast<const uint4*>(f + q);
+        b = *reinterpret_cast<const uint4*>(f + q + 16);
+        c = *reinterpret_cast<const uint4*>(f + q + 32);
+        d = *reinterpret_cast<const uint4*>(f + q + 48);
+        t = q + 64 < P.len ? *reinterpret_cast<const uint32_t*>(f + q + 64) : 0u;
+    };
+    uint64_t q0 = cs & ~15ull;
+    if (q0 >= ce) return kNone;
+    uint4 a, b, cc, d;
+    uint32_t t;
+    fetch(q0, a, b, cc, d, t);
+    for (;;) {
+        const uint64_t q1 = q0 + 64;
+        uint4 na = zero4(), nb = zero4(), nc = zero4(), nd = zero4();
+        uint32_t nt = 0;
+        if (q1 < ce) fetch(q1, na, nb, nc, nd, nt);
         const uint32_t w0[5] = {a.x, a.y, a.z, a.w, b.x}, w1[5] = {b.x, b.y, b.z, b.w, cc.x};
         const uint32_t w2[5] = {cc.x, cc.y, cc.z, cc.w, d.x}, w3[5] = {d.x, d.y, d.z, d.w, t};
-        const uint64_t m = (uint64_t)magic_mask(w0, q0, cs, ce, P.len, m3) |
-                           ((uint64_t)magic_mask(w1, q0 + 16, cs, ce, P.len, m3) << 16) |
-                           ((uint64_t)magic_mask(w2, q0 + 32, cs, ce, P.len, m3) << 32) |
-                           ((uint64_t)magic_mask(w3, q0 + 48, cs, ce, P.len, m3) << 48);
-        uint64_t mm = m;
+        uint64_t mm = (uint64_t)magic_mask(w0, q0, cs, ce, P.len, m3) |
+                      ((uint64_t)magic_mask(w1, q0 + 16, cs, ce, P.len, m3) << 16) |
+                      ((uint64_t)magic_mask(w2, q0 + 32, cs, ce, P.len, m3) << 32) |
+                      ((uint64_t)magic_mask(w3, q0 + 48, cs, ce, P.len, m3) << 48);
         while (mm) {
             const uint64_t p = q0 + (uint64_t)__builtin_ctzll(mm);
             mm &= mm - 1;
@@ -858,8 +890,69 @@ __device__ uint64_t find_entry_lane(const FrameParams& P, uint64_t cs, uint64_t 
             uint64_t nx, ol, pd, lf;
             if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd, lf, crct) == RIO_OK) return p;
         }
+        if (q1 >= ce) return kNone;
+        q0 = q1;
+        a = na;
+        b = nb;
+        cc = nc;
+        d = nd;
+        t = nt;
     }
-    return kNone;
+}
+
+// walk_from for one lane: the same records, slots and summary, with the next record's header loads
+// issued before this record's slot stores (on CDNA vmcnt retires loads and stores in issue order: a
+// load issued after the stores would wait for them too), so each hop costs one load round trip.
+__device__ void walk_from_lane(const FrameParams& P, uint64_t c, uint64_t p, uint32_t ver, uint32_t comp, ChunkSum& s,
+                               const uint32_t* crct) {
+    const uint8_t* f = P.file;
+    const uint64_t ce = chunk_end(P, c);
+    uint64_t* so = P.scratch_off + c * P.slots;
+    uint64_t* sl = P.scratch_len + c * P.slots;
+    uint64_t* sp = P.scratch_pay + c * P.slots;
+    bool have = p < ce && p + 32 <= P.len;
+    uint4 a = zero4(), b = zero4();
+    if (have) {
+        a = ldu16(f + p);
+        b = ldu16(f + p + 16);
+    }
+    while (p < ce) {
+        Hdr h;
+        uint64_t next = 0, olen = 0, pd = 0, lf = 0;
+        int e = kFrameSlow;
+        if (have) {
+            const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            e = frame_fast(w, P.len, p, ver, comp, h, next, olen, pd, crct);
+        }
+        if (e != RIO_OK) e = frame_slow(f, P.len, p, ver, comp, h, next, olen, pd, lf);
+        if (e) {
+            s.status = e;
+            s.err_off = p;
+            if (e == RIO_ERR_HEADER_CRC) {
+                s.det0 = h.exp_crc;
+                s.det1 = h.act_crc;
+            } else if (e == RIO_ERR_MAGIC) {
+                s.det0 = h.magic_len;
+            } else if (e == RIO_ERR_UNEXPECTED_EOF && h.hdr_len != 0) {
+                s.det0 = 1;  // raised by the payload read, not by a header varint
+            }
+            break;
+        }
+        have = next < ce && next + 32 <= P.len;
+        if (have) {
+            a = ldu16(f + next);
+            b = ldu16(f + next + 16);
+        }
+        if (s.count < P.slots) {
+            so[s.count] = p;
+            sl[s.count] = olen | lf | (h.nil ? kNilBit : 0);
+            sp[s.count] = pd;
+        }
+        s.count++;
+        s.bytes += olen;
+        p = next;
+    }
+    s.exit = s.status ? s.err_off : p;
 }
 
 constexpr uint32_t kWalkLaneBlock = 256;
@@ -873,7 +966,7 @@ __global__ void __launch_bounds__(kWalkLaneBlock) k_walk_lane(FrameParams P) {
     const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
     const uint64_t from = c == 0 ? (uint64_t)RIO_FILE_HEADER_BYTES : find_entry_lane(P, cs, ce, ver, comp, crct);
     ChunkSum s = chunk_sum_empty(from);
-    if (from != kNone) walk_from(P, c, from, ver, comp, s, crct);
+    if (from != kNone) walk_from_lane(P, c, from, ver, comp, s, crct);
     P.chunks[c] = s;
 }
 
@@ -1299,6 +1392,9 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
 }
 
 __device__ void finalize_info(const FrameParams& P) {
+    // the file's mean bytes per record, for the context's choice of walk on its next decode (ctx_frame_params)
+    if (P.walk_hint && P.state->n_records && P.len > RIO_FILE_HEADER_BYTES)
+        *reinterpret_cast<volatile uint64_t*>(P.walk_hint) = (P.len - RIO_FILE_HEADER_BYTES) / P.state->n_records;
     ScanState* st = P.state;
     rio_file_info info;
     info.version = st->version;

@@ -4,7 +4,7 @@
 #   e.g. scripts/ab_env.sh r3g "c2 c3" "RIO_FUSED=0" "RIO_FUSED=1"
 set -u
 TAG=$1; CFGS=$2; shift 2; OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
-for r in 1 2; do
+for r in $(seq 1 ${R:-2}); do
   for c in $CFGS; do
     v=0
     for e in "$@"; do

@@ -96,3 +96,26 @@ def test_older_layouts_full_size(version, monkeypatch):
     img = corpus.to_version(bytes(corpus.generate(200_000, 1024, 2, kind=1, seed=5)), version)
     g = _check(dec, f"C2 v{version}", img)
     assert g["n_records"] == 200_000
+
+
+def test_auto_walk_follows_the_previous_decode(monkeypatch):
+    """RIO_WALK_LANE unset (auto): a context's decode takes the lane walk (16 KiB chunks, info.n_chunks shows
+    which) when its previous decode had records of 768 B .. 8 KiB on average and the file fills 32768 lane
+    chunks, else the wave walk (32 KiB chunks). DeviceDecoder.decode runs a capacity probe first, which records the file's mean for the real
+    decode: a fresh context's first file is framed by the wave walk in the probe only. Every decode is the
+    oracle's."""
+    from recordio.device import DeviceDecoder
+
+    monkeypatch.delenv("RIO_WALK_LANE", raising=False)
+    monkeypatch.delenv("RIO_LANE_CHUNK_BYTES", raising=False)
+    dec = DeviceDecoder(0, own_ctx=True)
+    big = corpus.generate(600_000, 1024, 2, kind=0, seed=7)  # incompressible 1 KiB records, >= 32768 lane chunks
+    small = corpus.generate(200_000, 64, 2, kind=1, seed=8)
+    chunks = lambda img, cb: (len(img) - 8 + cb - 1) // cb  # noqa: E731
+    got = []
+    short = corpus.generate(40_000, 1024, 2, kind=0, seed=9)  # large records, too few lane chunks
+    for img in (big, big, small, small, big, short):
+        g = _check(dec, "auto", img)
+        got.append(g["n_chunks"])
+    assert got == [chunks(big, 16384), chunks(big, 16384), chunks(small, 32768), chunks(small, 32768),
+                   chunks(big, 16384), chunks(short, 32768)]
