@@ -51,7 +51,12 @@ constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 constexpr uint32_t kFarOff = 232;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
 constexpr uint32_t kLitEff = ~0u;                // "offset" of a literal element (see snappy_lane)
-static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128 + 16, "far history must be flushed before the parser reads it");
+// RIO_STORE_LATE: the flush store after the step's loads (one more step of flush lag for a far load to see)
+#ifndef RIO_STORE_LATE
+#define RIO_STORE_LATE 1
+#endif
+static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128 + 16 + (RIO_STORE_LATE ? 16 : 0),
+              "far history must be flushed before the parser reads it");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
 
 // materialize x in a VGPR here: the selects that use it can no longer be turned into branches that
@@ -62,12 +67,16 @@ __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
     return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
-// cache policy (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads. Default 1: the
-// arena stores no longer push the lanes' input lines out of L2 between their 16-byte reads (C2
-// decode: HBM reads 4.1 -> 3.4 GB and writes 1.12 -> 1.03 GB per launch, 0.9 % slower, because far
-// copies then miss L2 more often; C4: 3 % faster). 2 and 3 were slower (+5 %, +8 %).
+// cache policy (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads. Round 3 chose 1 (the
+// arena stores no longer pushed the lanes' input lines out of L2: C2 HBM reads 4.1 -> 3.4 GB per launch,
+// C2 0.9 % slower, C4 3 % faster). Round 5, after the paired input loads and the late flush store: plain
+// stores (0) C4 decode 13.21 -> 12.19 ms (-7.7 %: far copies find their sources written with plain stores
+// in L2 / MALL), C2 equal (+0.2 %). 2 and 3 were slower (+5 %, +8 %, round 3).
 #ifndef RIO_NT
-#define RIO_NT 1
+#define RIO_NT 0
+#endif
+#ifndef RIO_NT_MULTI
+#define RIO_NT_MULTI 1
 #endif
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
@@ -581,6 +590,9 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     auto inext = [&](uint32_t a) __attribute__((always_inline)) { return (a + kColRow) & (kColI - 1u); };
 
     constexpr bool kPair = RIO_IN_PAIR && RIO_BUF && !kMulti;  // paired input prefetch (RIO_IN_PAIR)
+    // flush stores non-temporal in the multi-record loop (C3: plain stores +1.8 % decode), plain in the
+    // single-record loop (C4: -7.7 %, C2 equal; RIO_NT above); RIO_NT_MULTI overrides
+    constexpr bool kStoreNT = kMulti ? (RIO_NT_MULTI & 1) : (RIO_NT & 1);
     const bool live = r0 < r1;
     uint8_t* const out = P.out;
     // d0 / o0: rec_desc and out_off of r0, loaded by the caller (zero when !live)
@@ -838,16 +850,19 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
                 nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
             }
         }
-        // this step's owners' blocks (the far-history load below is issued after the store)
+        // this step's owners' blocks (the far-history load below is issued after the store; with
+        // RIO_STORE_LATE after the input prefetch, so a wait for this step's loads three steps on does not
+        // also wait for this store: vmcnt retires stores and loads in issue order)
+        auto flush_store = [&]() __attribute__((always_inline)) {
 #if RIO_BUF
-        {
             const v4u32b w = {fv_now.x, fv_now.y, fv_now.z, fv_now.w};
             __builtin_amdgcn_raw_buffer_store_b128(w, rsrc_out, ((ofb_now >> 31) && !(RIO_EXP_MEM & 1)) ? obase[j & 3u] + fpos_now : kOob, 0,
-                                                   (RIO_NT & 1) ? 2 : 0);
-        }
+                                                   kStoreNT ? 2 : 0);
 #else
-        st_out((ofb_now >> 31) ? obase[j & 3u] + fpos_now : sink, fv_now);
+            st_out((ofb_now >> 31) ? obase[j & 3u] + fpos_now : sink, fv_now);
 #endif
+        };
+        if (!RIO_STORE_LATE) flush_store();
         fb += ((lane >> 4) == (j & 3u) && ready_now) ? 64u : 0u;
 
         // far history (destination-aligned: from q - r), or the next record's descriptor, or a placeholder
@@ -900,6 +915,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.in_c = take ? cn : kNoChunk;
             cn += take ? 1u : 0u;
         }
+
+        if (RIO_STORE_LATE) flush_store();
 
         // 6. land the next slot's input chunk(s), then read the next step's parser window
         if constexpr (kPair) {
