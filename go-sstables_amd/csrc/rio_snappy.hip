@@ -73,11 +73,10 @@ __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
 // stores (0) C4 decode 13.21 -> 12.19 ms (-7.7 %: far copies find their sources written with plain stores
 // in L2 / MALL), C2 equal (+0.2 %). 2 and 3 were slower (+5 %, +8 %, round 3).
 #ifndef RIO_NT
-#define RIO_NT 0
+#define RIO_NT 1
 #endif
-#ifndef RIO_NT_MULTI
-#define RIO_NT_MULTI 1
-#endif
+// mean decoded bytes per record from which a wave's flush stores are plain (snappy_lane's kPlain)
+constexpr uint64_t kPlainStoreMin = 4096;
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
     if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
 }
@@ -574,7 +573,7 @@ __device__ __forceinline__ void col_hst(uint8_t* L, uint32_t a, uint32_t v) { co
 // first record starts in the arena's first 3 bytes (the caller passes it wave-uniform), so a far
 // copy there may need the kind-3 load from q (see the far-history load); every other wave has no
 // such lane and its far loads go through the arena descriptor.
-template <bool kMulti, bool kLow>
+template <bool kMulti, bool kLow, bool kPlain = false>
 __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, uint64_t r1, uint4 d0, uint64_t o0, uint8_t* L,
                                             uint32_t wave, uint32_t lane, uint8_t* sink, uint64_t* bad_rec) {
     const uint32_t wl = wave * 256u + lane * 4u;  // row 0 of this lane (both images)
@@ -590,9 +589,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     auto inext = [&](uint32_t a) __attribute__((always_inline)) { return (a + kColRow) & (kColI - 1u); };
 
     constexpr bool kPair = RIO_IN_PAIR && RIO_BUF && !kMulti;  // paired input prefetch (RIO_IN_PAIR)
-    // flush stores non-temporal in the multi-record loop (C3: plain stores +1.8 % decode), plain in the
-    // single-record loop (C4: -7.7 %, C2 equal; RIO_NT above); RIO_NT_MULTI overrides
-    constexpr bool kStoreNT = kMulti ? (RIO_NT_MULTI & 1) : (RIO_NT & 1);
+    // flush stores: plain (kPlain) for records of kPlainStoreMin bytes and more (C4's 64 KiB records: far
+    // copies then find their sources in L2 / MALL, decode -7.7 %), non-temporal otherwise (C2 the same
+    // speed with 2.84 instead of 3.62 GB of reads per launch; C3 plain +1.8 %); RIO_NT overrides (bit 0)
+    constexpr bool kStoreNT = (RIO_NT & 1) && !kPlain;
     const bool live = r0 < r1;
     uint8_t* const out = P.out;
     // d0 / o0: rec_desc and out_off of r0, loaded by the caller (zero when !live)
@@ -1021,6 +1021,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
         return;
     }
     const uint64_t n = st->n_records;
+    const bool plain = n && st->total_bytes / n >= kPlainStoreMin;  // flush store policy (kPlainStoreMin)
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t g = (uint64_t)wave * gridDim.x + blockIdx.x;
     uint8_t* sink = P.sink + g * 64;
@@ -1038,7 +1039,10 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
         const uint4 d0 = live0 ? P.rec_desc[r0] : zero4();
         const uint64_t o0 = live0 ? P.out_off[r0] : 0;
         const bool low = rl64(live0 ? o0 : ~0ull, 0u) < 3;
-        if (rpc == 1)
+        if (rpc == 1 && plain)
+            ok = low ? snappy_lane<false, true, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
+                     : snappy_lane<false, false, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
+        else if (rpc == 1)
             ok = low ? snappy_lane<false, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
                      : snappy_lane<false, false>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
         else
@@ -1091,7 +1095,11 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe_batch(FrameBatch B
             const uint4 d0 = live0 ? P.rec_desc[r0] : zero4();
             const uint64_t o0 = live0 ? P.out_off[r0] : 0;
             const bool low = rl64(live0 ? o0 : ~0ull, 0u) < 3;
-            if (rpl == 1)
+            const bool plain = n && P.state->total_bytes / n >= kPlainStoreMin;  // wave-uniform (one file)
+            if (rpl == 1 && plain)
+                ok = low ? snappy_lane<false, true, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
+                         : snappy_lane<false, false, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
+            else if (rpl == 1)
                 ok = low ? snappy_lane<false, true>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec)
                          : snappy_lane<false, false>(P, r0, r1, d0, o0, lds, wave, lane, sink, &bad_rec);
             else
