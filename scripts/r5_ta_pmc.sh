@@ -2,10 +2,11 @@
 # Address-path / LDS / issue counters of k_snappy_pipe on C2: the stock build (2 waves per SIMD)
 # and the timing-only 3-wave build (librio_occ.so). One --pmc set per pass, kernel trace only, each pass under its
 # own timeout; counters the device does not list are dropped from a set before it runs.
-# usage: scripts/r5_ta_pmc.sh <tag> [libs...]   (libs: base occ ...; default "base occ")
+# usage: [CFG=c3] [PASSES="1 7"] scripts/r5_ta_pmc.sh <tag> [libs...]   (libs: base occ ...; default "base occ")
 set -u
 TAG=$1; shift
 LIBS=${*:-base occ}
+CFG=${CFG:-c2}; PASSES=${PASSES:-1 2 3 4 5 6 7 8}
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 have() { grep -qw "$1" "$OUT/counters_list.txt"; }
@@ -24,11 +25,12 @@ for v in $LIBS; do
   i=0
   for set in "${SETS[@]}"; do
     i=$((i+1))
+    case " $PASSES " in *" $i "*) ;; *) continue ;; esac
     ctr=""; for c in $set; do have "$c" && ctr="$ctr $c"; done
     echo "$v pass $i:$ctr" | tee -a "$OUT/passes.txt"
     [ -z "$ctr" ] && continue
     RIO_LIB_PATH=$LIBP timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctr -d "$OUT/$v/pmc$i" -o run --output-format csv -- \
-        python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none > "$OUT/${v}_pmc$i.log" 2>&1
+        python bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --traffic none > "$OUT/${v}_pmc$i.log" 2>&1
     rc=$?; echo "$v pass $i rc=$rc"; [ $rc -ne 0 ] && tail -20 "$OUT/${v}_pmc$i.log" && exit $rc
   done
   python3 scripts/pmc_summary.py "$OUT/$v" k_snappy_pipe k_walk > "$OUT/${v}_summary.txt" 2>&1; echo "== $v"; cat "$OUT/${v}_summary.txt"
