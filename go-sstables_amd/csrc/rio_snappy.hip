@@ -72,6 +72,14 @@ __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
 // C2 0.9 % slower, C4 3 % faster). Round 5, after the paired input loads and the late flush store: plain
 // stores (0) C4 decode 13.21 -> 12.19 ms (-7.7 %: far copies find their sources written with plain stores
 // in L2 / MALL), C2 equal (+0.2 %). 2 and 3 were slower (+5 %, +8 %, round 3).
+// RIO_LEAN (default 1): fewer VALU compares per step. On gfx950 two waves of a SIMD issue ~1.7 v_add / v_and /
+// v_or / v_xor / v_lshrrev per 4-cycle slot but ~1.15 of the 3-operand integer ops (v_cndmask_e64, v_bfi,
+// v_alignbyte ...) and ~0.95 v_cmp (scripts/op_probe.hip, profiles/r5/r5w_op_probe.txt): the record-end test as
+// one OR and one compare (was three compares), the offset doubling without its range compare, and the emit's
+// ring / far selects from the parse's masks instead of re-comparing the slot kind (C2 decode -2 %, r5x)
+#ifndef RIO_LEAN
+#define RIO_LEAN 1
+#endif
 #ifndef RIO_NT
 #define RIO_NT 1
 #endif
@@ -542,6 +550,7 @@ struct ColSlot {
     uint32_t kind;   // 0 literal, 1 ring copy, 2 far copy, 3 far copy loaded from q (see the emit)
     uint32_t q;      // ring copy: source output position; literal: byte shift of x0..x4
     uint32_t desc;   // aux carries the next record's descriptor
+    uint32_t ringm, farm;  // RIO_LEAN: kind 1 / kind 2 as all-ones masks (the emit selects by v_bfi, no compare)
 };
 __device__ __forceinline__ ColSlot col_empty_slot() {
     ColSlot S;
@@ -552,6 +561,8 @@ __device__ __forceinline__ ColSlot col_empty_slot() {
     S.in_c = kNoChunk;
     S.n = 0;
     S.kind = 1;
+    S.ringm = ~0u;
+    S.farm = 0;
     S.q = 0;
     S.desc = 0;
     return S;
@@ -711,6 +722,19 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 
         // 2. emit the piece parsed kD steps ago: destination dwords of bytes [d - r, d - r + 16)
         {
+#if RIO_LEAN
+            const uint32_t rm = S.ringm, fm = S.farm;
+            auto bsel = [](uint32_t m, uint32_t a, uint32_t b) __attribute__((always_inline)) { return (a & m) | (b & ~m); };
+            uint32_t X0 = bsel(rm, wL0, S.x0), X1 = bsel(rm, wL1, S.x1), X2 = bsel(rm, wL2, S.x2), X3 = bsel(rm, wL3, S.x3),
+                     X4 = bsel(rm, wL4, S.x4);
+            const uint32_t sh = bsel(rm, wSh, S.q);
+            uint32_t D0 = __builtin_amdgcn_alignbyte(X1, X0, sh), D1 = __builtin_amdgcn_alignbyte(X2, X1, sh),
+                     D2 = __builtin_amdgcn_alignbyte(X3, X2, sh), D3 = __builtin_amdgcn_alignbyte(X4, X3, sh);
+            D0 = bsel(fm, S.aux.x, D0);
+            D1 = bsel(fm, S.aux.y, D1);
+            D2 = bsel(fm, S.aux.z, D2);
+            D3 = bsel(fm, S.aux.w, D3);
+#else
             const bool ring = S.kind == 1;
             uint32_t X0 = ring ? wL0 : S.x0, X1 = ring ? wL1 : S.x1, X2 = ring ? wL2 : S.x2, X3 = ring ? wL3 : S.x3,
                      X4 = ring ? wL4 : S.x4;
@@ -722,6 +746,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             D1 = far ? S.aux.y : D1;
             D2 = far ? S.aux.z : D2;
             D3 = far ? S.aux.w : D3;
+#endif
             // kind 3 (rare: a far source in the first bytes of the arena, lane of the file's first
             // record): aux holds bytes [q, q + 16), shifted up by r here
             if (kLow && __builtin_expect(__any(S.kind == 3), 0)) {
@@ -814,7 +839,14 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t cap = 16u - umax(sh, r);
             const uint32_t n = go ? umin(rem1, umin(cap, eff1)) : 0u;
             S.n = n;
+#if RIO_LEAN
+            const bool farc = !lit1 && n != 0 && eff1 > kFarOff;
+            S.kind = lit1 ? 0u : (farc ? 2u : 1u);
+            S.ringm = (lit1 || farc) ? 0u : ~0u;
+            S.farm = farc ? ~0u : 0u;
+#else
             S.kind = lit1 ? 0u : ((n != 0 && eff1 > kFarOff) ? 2u : 1u);
+#endif
             qsrc = pd - eff1;
             // literal rows from (s + sh - r) & ~3 (the bytes below s + sh are masked at the emit)
             const uint32_t ls = s + sh - r;
@@ -825,15 +857,29 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.x3 = col_ld(L, c3);
             S.x4 = col_ld(L, c4);
             // literal: the shift (low 2 bits) of x0..x4; a far copy's q goes unused at the emit
+#if RIO_LEAN
+            S.q = (lit1 || farc) ? ls : qsrc;
+#else
             S.q = S.kind == 1 ? qsrc : ls;
+#endif
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
+#if RIO_LEAN
+            // a piece that covered its whole offset doubles it (the source is periodic in eff1; n <= 16,
+            // so eff stays <= 32, a ring copy); the record end tested as one OR (one compare, not three)
+            eff = eff1 + ((n == eff1) ? n : 0u);
+            s = badn ? s_end : s;
+            uint32_t at_z = rem | (s ^ s_end) | (uint32_t)pdone;
+            pin_v(at_z);
+            if (at_z == 0) {
+#else
             eff = (eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
             s = badn ? s_end : s;
             uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
             pin_v(at_end);
             if (at_end) {
+#endif
                 const bool bad_len = pd != rd_end;
                 bad = bad || bad_len;
                 rem = bad_len ? rd_end - pd : rem;
