@@ -680,6 +680,12 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
 // spilled to scratch beat 5 (walk 0.210 -> 0.185 ms on C2). With the packed DPP fill scans and the
 // 32-bit LEB128 packing the spills landed in the fill loop: 6 waves 0.413 ms on C3, 5 waves (96
 // VGPRs, no scratch) 0.300 ms, against 0.363 before (C2 0.183 -> 0.164 ms)
+// RIO_COPY2 (default 2): k_copy_records with the next record's sizes prefetched and 1 KiB in flight per
+// 16-lane group, non-temporal loads and stores (C2-ref-random copy 0.423 -> 0.370 ms, 5.8 TB/s; C1 +7 %,
+// C5 +4 %: profiles/r5/r5aa_copy_ab.txt); 1: the same with plain loads and stores; 0: the round-4 loop
+#ifndef RIO_COPY2
+#define RIO_COPY2 2
+#endif
 #ifndef RIO_WALK_OCC
 #define RIO_WALK_OCC 5
 #endif
@@ -1373,6 +1379,52 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
+#if RIO_COPY2
+    // each group's next record's sizes are loaded while the current one is copied, and a record moves in
+    // 1 KiB rounds (four 16-byte loads per lane in flight, then the four stores): the copy was a chain of
+    // dependent round trips (sizes, literal header byte, then 256 bytes at a time)
+    auto meta = [&](uint64_t i, uint64_t& o0, uint64_t& len, const uint8_t*& src) __attribute__((always_inline)) {
+        o0 = P.out_off[i];
+        len = P.out_off[i + 1] - o0;
+        uint64_t start, slen;
+        rec_stream(P, i, start, slen);
+        // a Snappy record here is one literal of its whole length (k_place checked every record with
+        // bytes): its header is the slen - len bytes in front of them, no byte to read
+        src = P.file + start + (none ? 0 : slen - len);
+    };
+    uint64_t o0 = 0, len = 0;
+    const uint8_t* src = P.file;
+    if (grp < n) meta(grp, o0, len, src);
+    for (uint64_t i = grp; i < n; i += ngrp) {
+        uint64_t no0 = 0, nlen = 0;
+        const uint8_t* nsrc = P.file;
+        if (i + ngrp < n) meta(i + ngrp, no0, nlen, nsrc);
+        uint8_t* dst = P.out + o0;
+        for (uint64_t k0 = 0; k0 < len; k0 += 1024) {
+            uint4 v[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint64_t k = k0 + 256 * j + 16 * lane;
+                v[j] = k < len ? (RIO_COPY2 == 2 ? ldu16_nt(src + k) : ldu16(src + k)) : zero4();
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint64_t k = k0 + 256 * j + 16 * lane;
+                if (k + 16 <= len) {
+                    if (RIO_COPY2 == 2)
+                        stu16_nt(dst + k, v[j]);
+                    else
+                        stu16(dst + k, v[j]);
+                } else if (k < len) {
+                    st_partial(dst + k, v[j], (uint32_t)(len - k));
+                }
+            }
+        }
+        o0 = no0;
+        len = nlen;
+        src = nsrc;
+    }
+#else
     for (uint64_t i = grp; i < n; i += ngrp) {
         const uint64_t o0 = P.out_off[i], len = P.out_off[i + 1] - o0;
         if (len == 0) continue;
@@ -1389,6 +1441,7 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
                 st_partial(dst + k, v, (uint32_t)(len - k));
         }
     }
+#endif
 }
 
 __device__ void finalize_info(const FrameParams& P) {
