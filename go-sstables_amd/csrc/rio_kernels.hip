@@ -686,6 +686,11 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
 #ifndef RIO_COPY2
 #define RIO_COPY2 2
 #endif
+// k_copy_records' grid (4096 x 256: C1's 100 k records over twice the groups, copy 0.067 -> 0.057 ms; C2-ref-random
+// -2 %; 1024: C1 +45 %; two records in flight per group: +10 %, r5ab)
+#ifndef RIO_COPY_GRID
+#define RIO_COPY_GRID 4096
+#endif
 #ifndef RIO_WALK_OCC
 #define RIO_WALK_OCC 5
 #endif
@@ -2160,7 +2165,7 @@ static void launch_decoders(const FrameParams& P, hipStream_t s, bool snappy_mai
     const uint32_t c = P.comp_hint;
     const bool any = c == RIO_COMP_UNKNOWN;
     if (any || c == RIO_COMP_NONE || c == RIO_COMP_SNAPPY)
-        hipLaunchKernelGGL(k_copy_records, dim3(2048), dim3(256), 0, s, P);
+        hipLaunchKernelGGL(k_copy_records, dim3(RIO_COPY_GRID), dim3(256), 0, s, P);
     if ((any || c == RIO_COMP_SNAPPY) && snappy_main) launch_snappy_decode(P, s, true);
     if (any || c == RIO_COMP_GZIP) {
         launch_gzip_decode(P, s);
