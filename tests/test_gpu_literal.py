@@ -9,6 +9,7 @@ import random
 import numpy as np
 import pytest
 
+import corpus
 import oracle_py as orc
 from gpu_util import assert_same_as_oracle, gpu_decode_arrays
 from recordio import encode_file
@@ -55,3 +56,37 @@ def test_one_compressible_record_uses_the_decoder(where):
 def test_multi_block_literal_is_not_single():
     rng = random.Random(9)
     check([rand_bytes(rng, 70000), rand_bytes(rng, 200000), rand_bytes(rng, 10)])
+
+
+def _literal_stream(data: bytes, nb: int) -> bytes:
+    """A Snappy stream that is one literal element: the decoded-length preamble, then the literal's tag with
+    nb extra length bytes (0: the 1-byte form, lengths 1..60; 1..4: tag values 60..63, which golang/snappy's
+    decoder accepts for any length they can hold, canonical or not), then the bytes."""
+    n = len(data)
+    tag = bytes([(n - 1) << 2]) if nb == 0 else bytes([(59 + nb) << 2]) + (n - 1).to_bytes(nb, "little")
+    return corpus.uvarint(n) + tag + data
+
+
+def test_non_canonical_literal_headers_take_the_copy():
+    """Single-literal records whose literal header is 1..5 bytes for lengths that need fewer (a writer other
+    than golang/snappy's): the copy path takes each record's header length from its sizes (stream length -
+    record length), so every form must land the same bytes as the oracle's decoder."""
+    rng = random.Random(11)
+    out = bytearray(corpus.file_header(4, 2))
+    for i in range(3000):
+        if i % 97 == 13:
+            out += corpus.header_for(4, 0, 1, nil=True)
+            continue
+        if i % 89 == 7:
+            pay = corpus.uvarint(0)  # an empty record: the preamble alone
+            out += corpus.header_for(4, 0, len(pay)) + pay
+            continue
+        n = rng.randint(1, 60) if i % 3 == 0 else rng.randint(61, 3000)
+        nb = rng.choice([k for k in (0, 1, 2, 3, 4) if (k == 0 and n <= 60) or (k > 0 and n - 1 < 256 ** k)])
+        pay = _literal_stream(rand_bytes(rng, n), nb)
+        out += corpus.header_for(4, n, len(pay)) + pay
+    img = bytes(out)
+    g = gpu_decode_arrays(np.frombuffer(img, dtype=np.uint8))
+    o = orc.file_reader_decode_arrays(img)
+    assert_same_as_oracle(g, o)
+    assert g["n_records"] == 3000
