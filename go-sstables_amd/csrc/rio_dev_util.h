@@ -57,14 +57,16 @@ __device__ __forceinline__ void stu16(uint8_t* p, uint4 v) { *reinterpret_cast<u
 #pragma clang diagnostic pop
 // non-temporal (streaming) 16-byte access: bytes touched once should not displace lines the
 // kernel comes back to (the decoder's input lines)
+// (p any byte address: the 1-aligned vector type, as u4u for the plain forms)
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u32u __attribute__((ext_vector_type(4), aligned(1)));
 __device__ __forceinline__ uint4 ldu16_nt(const uint8_t* p) {
-    const v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(p));
+    const v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32u*>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void stu16_nt(uint8_t* p, uint4 v) {
-    v4u32 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<v4u32*>(p));
+    v4u32u w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<v4u32u*>(p));
 }
 __device__ __forceinline__ uint4 zero4() { return make_uint4(0, 0, 0, 0); }
 __device__ __forceinline__ uint4 or4(uint4 a, uint4 b) { return make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w); }
