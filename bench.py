@@ -1052,12 +1052,21 @@ class DeviceBackend:
         return self.dec.stage_ms() if self.files else []
 
     def evict(self):
-        """Write 1 GiB of HBM (pushes the decode's working set out of the MALL)."""
+        """Write 1 GiB of HBM and read half of it back (pushes the decode's working set out of the MALL)."""
         import torch
 
         if not hasattr(self, "_evict"):
             self._evict = torch.empty(1 << 30, dtype=torch.uint8, device=self.device)
         self._evict.fill_(1)
+        if os.environ.get("RIO_BENCH_EVICT", "write_read") == "write_read":
+            # then read 512 MiB of it back: clean lines replace the fill's dirty ones, whose write-back would
+            # otherwise run under the next decode (C1 cold walk 0.069 -> 0.045 ms, profiles/r5/r5ai_evict_ab.txt);
+            # RIO_BENCH_EVICT=write: the fill alone (round 4's method)
+            self._evict_sum = self._evict[: 1 << 29].view(torch.int64).sum()
+        # the fill runs on torch's stream, the decode on the context's: without this wait the next decode ran
+        # beside the 1 GiB write (rocprofv3 trace, profiles/r5/r5af_c1_trace.txt) and its cold stage times
+        # priced the write's bandwidth in
+        torch.cuda.synchronize(self.device)
 
     def rec_offs(self, n):
         """Record offsets of every loaded file (the CPU baseline's ReadNextAt table)."""
@@ -1154,7 +1163,7 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
         if len(cold) == 4:
             mall_flushed = {"ms_per_step": round(cold_step_ms, 4), "value": round(cold_value, 3),
                             "unit": "GiB/s", "stages_ms": [round(x, 4) for x in cold],
-                            "note": "1 GiB device write between steps; per-stage HIP events, flush excluded"}
+                            "note": "1 GiB device write + 512 MiB read-back between steps, finished before the decode; per-stage HIP events, flush excluded"}
 
     # with the working set inside the MALL the warm loop would price cache hits as HBM;
     # the line then reports the cold pass (MALL evicted before every step, per-stage HIP events,

@@ -157,12 +157,11 @@ constexpr size_t kStage = 32ull << 20;  // pinned staging piece
 namespace {
 // framing scratch + per-record decode descriptors of one file (a ctx has one set per file of a batch)
 struct FileArenas {
-    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, fail_lanes, chunks, block_runs, chunk_excl, place,
-        block_excl, state, info;
+    // meta: the scan state, the file info, the lanes' failure list, the block and chunk summaries and the chunk
+    // placements of one call in one allocation (state and block summaries first, 256-byte aligned parts)
+    DevBuf scratch_off, scratch_len, scratch_pay, rec_pay, rec_desc, meta;
     void release() {
-        for (DevBuf* b : {&scratch_off, &scratch_len, &scratch_pay, &rec_pay, &rec_desc, &fail_lanes, &chunks, &block_runs,
-                          &chunk_excl, &place, &block_excl, &state, &info})
-            b->release();
+        for (DevBuf* b : {&scratch_off, &scratch_len, &scratch_pay, &rec_pay, &rec_desc, &meta}) b->release();
     }
 };
 }  // namespace
@@ -262,27 +261,26 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     HIP_TRY(A.scratch_off.ensure(nc * P.slots * 8));
     HIP_TRY(A.scratch_len.ensure(nc * P.slots * 8));
     HIP_TRY(A.scratch_pay.ensure(nc * P.slots * 8));
-    HIP_TRY(A.chunks.ensure(nc * sizeof(ChunkSum)));
-    HIP_TRY(A.chunk_excl.ensure(nc * sizeof(RunSum)));
-    HIP_TRY(A.place.ensure(nc * sizeof(ChunkPlace)));
-    HIP_TRY(A.block_runs.ensure(nb * sizeof(RunSum)));
-    HIP_TRY(A.block_excl.ensure(nb * sizeof(RunSum)));
-    HIP_TRY(A.state.ensure(sizeof(ScanState)));
-    HIP_TRY(A.info.ensure(sizeof(rio_file_info)));
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    const uint64_t o_info = al(sizeof(ScanState)), o_brun = o_info + al(sizeof(rio_file_info));
+    const uint64_t o_bexc = o_brun + al(nb * sizeof(RunSum)), o_fail = o_bexc + al(nb * sizeof(RunSum));
+    const uint64_t o_chk = o_fail + al(2 * kFailLanes * sizeof(uint64_t)), o_cexc = o_chk + al(nc * sizeof(ChunkSum));
+    const uint64_t o_place = o_cexc + al(nc * sizeof(RunSum)), meta_bytes = o_place + al(nc * sizeof(ChunkPlace));
+    HIP_TRY(A.meta.ensure(meta_bytes));
     HIP_TRY(ctx->sink.ensure(kSinkBytes));
-    HIP_TRY(A.fail_lanes.ensure(2 * kFailLanes * sizeof(uint64_t)));
+    uint8_t* const mb = A.meta.as<uint8_t>();
     P.sink = ctx->sink.as<uint8_t>();
-    P.fail_lanes = A.fail_lanes.as<uint64_t>();
+    P.fail_lanes = reinterpret_cast<uint64_t*>(mb + o_fail);
     P.scratch_off = A.scratch_off.as<uint64_t>();
     P.scratch_len = A.scratch_len.as<uint64_t>();
     P.scratch_pay = A.scratch_pay.as<uint64_t>();
-    P.chunks = A.chunks.as<ChunkSum>();
-    P.chunk_excl = A.chunk_excl.as<RunSum>();
-    P.place = A.place.as<ChunkPlace>();
-    P.block_runs = A.block_runs.as<RunSum>();
-    P.block_excl = A.block_excl.as<RunSum>();
-    P.state = A.state.as<ScanState>();
-    P.info = A.info.as<rio_file_info>();
+    P.chunks = reinterpret_cast<ChunkSum*>(mb + o_chk);
+    P.chunk_excl = reinterpret_cast<RunSum*>(mb + o_cexc);
+    P.place = reinterpret_cast<ChunkPlace*>(mb + o_place);
+    P.block_runs = reinterpret_cast<RunSum*>(mb + o_brun);
+    P.block_excl = reinterpret_cast<RunSum*>(mb + o_bexc);
+    P.state = reinterpret_cast<ScanState*>(mb);
+    P.info = reinterpret_cast<rio_file_info*>(mb + o_info);
     return RIO_OK;
 }
 
