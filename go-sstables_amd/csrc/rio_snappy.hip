@@ -77,6 +77,10 @@ __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
 // v_alignbyte ...) and ~0.95 v_cmp (scripts/op_probe.hip, profiles/r5/r5w_op_probe.txt): the record-end test as
 // one OR and one compare (was three compares), the offset doubling without its range compare, and the emit's
 // ring / far selects from the parse's masks instead of re-comparing the slot kind (C2 decode -2 %, r5x)
+// RIO_IN_CP (experiment): cache-policy bits of the input loads (0 default; 2 non-temporal)
+#ifndef RIO_IN_CP
+#define RIO_IN_CP 0
+#endif
 #ifndef RIO_LEAN
 #define RIO_LEAN 1
 #endif
@@ -940,8 +944,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
           if ((j & 1u) == 0) {  // a pair (cn, cn + 1) when the ring has room for both
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn + 1 < a + kInCh;
-            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, 0);
-            const v4u32b v2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn + 16u : kOob, 0, 0);
+            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, RIO_IN_CP);
+            const v4u32b v2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn + 16u : kOob, 0, RIO_IN_CP);
             S.in = make_uint4(v.x, v.y, v.z, v.w);
             S.in2 = make_uint4(v2.x, v2.y, v2.z, v2.w);
             S.in_c = take ? cn : kNoChunk;
@@ -953,7 +957,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn < a + kInCh;
 #if RIO_BUF
-            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, 0);
+            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, RIO_IN_CP);
             S.in = make_uint4(v.x, v.y, v.z, v.w);
 #else
             S.in = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
