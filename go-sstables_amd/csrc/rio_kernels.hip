@@ -691,6 +691,11 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
 #ifndef RIO_COPY_GRID
 #define RIO_COPY_GRID 4096
 #endif
+// files whose records average fewer bytes than this copy with 4 lanes per record instead of 16
+#ifndef RIO_COPY_SMALL
+#define RIO_COPY_SMALL 128
+#endif
+constexpr uint64_t kCopySmall = RIO_COPY_SMALL;
 #ifndef RIO_WALK_OCC
 #define RIO_WALK_OCC 5
 #endif
@@ -1375,19 +1380,17 @@ __device__ __forceinline__ void copy_fwd(uint8_t* dst, uint64_t d, const uint8_t
 // the reference benchmark's random records; k_snappy_pipe exits at once for those): 16-lane groups,
 // one record per group; each lane moves 16 bytes per step (unaligned load and store; the record's
 // last piece is stored exactly).
-__global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
-    const ScanState* st = P.state;
-    if (st->hdr_status != RIO_OK || st->capacity_fail) return;
-    const bool none = st->compression == RIO_COMP_NONE;
-    if (!none && !(st->compression == RIO_COMP_SNAPPY && !st->any_mixed)) return;
-    const uint64_t n = st->n_records;
-    const uint32_t lane = threadIdx.x & 15;
-    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
 #if RIO_COPY2
-    // each group's next record's sizes are loaded while the current one is copied, and a record moves in
-    // 1 KiB rounds (four 16-byte loads per lane in flight, then the four stores): the copy was a chain of
-    // dependent round trips (sizes, literal header byte, then 256 bytes at a time)
+// kG lanes per record (16, or 4 for files of small records: their 16-lane groups left 12 lanes idle and took a
+// dependent round trip per 50-byte record, C5's index copy 0.12 ms for 61 MB); each group's next record's sizes
+// are loaded while the current one is copied, and a record moves in rounds of 64 kG bytes (four 16-byte loads per
+// lane in flight, then the four stores): the copy was a chain of dependent round trips (sizes, literal header
+// byte, then 256 bytes at a time)
+template <uint32_t kG>
+__device__ __forceinline__ void copy_groups(const FrameParams& P, uint64_t n, bool none) {
+    const uint32_t lane = threadIdx.x & (kG - 1);
+    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kG;
+    const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) / kG;
     auto meta = [&](uint64_t i, uint64_t& o0, uint64_t& len, const uint8_t*& src) __attribute__((always_inline)) {
         o0 = P.out_off[i];
         len = P.out_off[i + 1] - o0;
@@ -1405,16 +1408,16 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
         const uint8_t* nsrc = P.file;
         if (i + ngrp < n) meta(i + ngrp, no0, nlen, nsrc);
         uint8_t* dst = P.out + o0;
-        for (uint64_t k0 = 0; k0 < len; k0 += 1024) {
+        for (uint64_t k0 = 0; k0 < len; k0 += 64 * kG) {
             uint4 v[4];
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
-                const uint64_t k = k0 + 256 * j + 16 * lane;
+                const uint64_t k = k0 + 16 * kG * j + 16 * lane;
                 v[j] = k < len ? (RIO_COPY2 == 2 ? ldu16_nt(src + k) : ldu16(src + k)) : zero4();
             }
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
-                const uint64_t k = k0 + 256 * j + 16 * lane;
+                const uint64_t k = k0 + 16 * kG * j + 16 * lane;
                 if (k + 16 <= len) {
                     if (RIO_COPY2 == 2)
                         stu16_nt(dst + k, v[j]);
@@ -1429,7 +1432,25 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
         len = nlen;
         src = nsrc;
     }
+}
+#endif
+
+__global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
+    const ScanState* st = P.state;
+    if (st->hdr_status != RIO_OK || st->capacity_fail) return;
+    const bool none = st->compression == RIO_COMP_NONE;
+    if (!none && !(st->compression == RIO_COMP_SNAPPY && !st->any_mixed)) return;
+    const uint64_t n = st->n_records;
+#if RIO_COPY2
+    // wave-uniform: the file's mean record size picks the group width
+    if (st->total_bytes < kCopySmall * n)
+        copy_groups<4>(P, n, none);
+    else
+        copy_groups<16>(P, n, none);
 #else
+    const uint32_t lane = threadIdx.x & 15;
+    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
     for (uint64_t i = grp; i < n; i += ngrp) {
         const uint64_t o0 = P.out_off[i], len = P.out_off[i + 1] - o0;
         if (len == 0) continue;
