@@ -470,6 +470,10 @@ def run_sstable(args, world, rank, local, device):
     n = CONFIGS["c5"][0]
     mine = shard_files(SST_TABLES, world, rank)
     dec = DeviceDecoder(local)
+    # data.rio on a context of its own (as the reader opens index.rio and data.rio as two files): a context picks
+    # its framing walk from its previous file's record sizes, which alternating 50-byte index and 1 KiB data files
+    # on one context would always get wrong for the data file
+    decd = DeviceDecoder(local, own_ctx=True)
     lib = L.lib()
     i64 = dict(dtype=torch.int64, device=device)
     # a real stream: the null stream's handle (0) would send the calls to the ctx's own stream and
@@ -485,7 +489,7 @@ def run_sstable(args, world, rank, local, device):
         # the files' header codecs as decode hints: only those codecs' kernels are launched
         T["ci"], T["cd"] = header_codec(index_img), header_codec(data_img)
         T["ib"], ii = dec.decode(T["d_index"], T["li"], comp=T["ci"])
-        T["db"], di = dec.decode(T["d_data"], T["ld"], comp=T["cd"])
+        T["db"], di = decd.decode(T["d_data"], T["ld"], comp=T["cd"])
         if ii["n_records"] != n or di["n_records"] != n:
             raise RuntimeError(f"sstable decode failed: {ii} {di}")
         T["nb_d"] = di["total_out_bytes"]
@@ -505,7 +509,7 @@ def run_sstable(args, world, rank, local, device):
                                     T["key_off"].data_ptr(), T["key_len"].data_ptr(), T["value_off"].data_ptr(),
                                     T["checksum"].data_ptr(), T["pres"].data_ptr(), sp)
             if marks: marks[2].record(stream)
-            dec.launch(T["d_data"], T["ld"], T["db"], stream, T["cd"])
+            decd.launch(T["d_data"], T["ld"], T["db"], stream, T["cd"])
             if marks: marks[3].record(stream)
             lib.rio_sst_validate(dec.ctx, T["db"].out.data_ptr(), T["db"].out_off.data_ptr(),
                                  T["db"].rec_off.data_ptr(), n, T["value_off"].data_ptr(), T["checksum"].data_ptr(), n,
