@@ -521,10 +521,21 @@ def run_sstable(args, world, rank, local, device):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(device)
-    for T in tables:
-        pres, vres = T["pres"], T["vres"]
-        if int(pres[0].item()) != -1 or int(vres[0].item()) != -1 or int(vres[1].item()) != -1:
-            raise RuntimeError(f"sstable validation failed: {pres.tolist()} {vres.tolist()}")
+
+    def digests():
+        # every table's parse / validation verdicts and a digest of everything the step writes (index and data
+        # records, the parsed entries, every value's CRC-64)
+        out = []
+        for T in tables:
+            pres, vres = T["pres"], T["vres"]
+            if int(pres[0].item()) != -1 or int(vres[0].item()) != -1 or int(vres[1].item()) != -1:
+                raise RuntimeError(f"sstable validation failed: {pres.tolist()} {vres.tolist()}")
+            out.append(tuple(device_digest(x) for x in (T["ib"].out, T["ib"].out_off, T["db"].out, T["db"].out_off,
+                                                       T["key_off"], T["key_len"], T["value_off"], T["checksum"],
+                                                       T["crc"])))
+        return out
+
+    want = digests()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(device)
@@ -533,6 +544,8 @@ def run_sstable(args, world, rank, local, device):
         step()
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
+    if digests() != want:
+        raise RuntimeError("sstable bench: the timed steps did not rebuild the warmup's outputs")
     if world > 1:
         torch.distributed.barrier()
     ev = []
@@ -565,6 +578,9 @@ def run_sstable(args, world, rank, local, device):
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": dom,
                      "kernel_ms": round(stage[dom], 4), "alg_bytes_per_launch": alg[dom]},
         "stages_ms_per_table": {k: round(v, 4) for k, v in stage.items()},
+        # the warmup's verdicts (every key parsed, every value's CRC-64 equal to its entry's) and device digests of all
+        # the step's outputs, rebuilt identically by the timed steps
+        "verified": True,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and tables:
         sys.path.insert(0, os.path.join(HERE, "tests"))
