@@ -593,6 +593,35 @@ __device__ __forceinline__ uint64_t wave_excl_scan64(uint64_t v, uint32_t lane, 
     return e;
 }
 
+// The same within 16-lane groups (a wave's four DPP rows; lane = the lane within its group): exclusive prefix
+// and the group's total
+__device__ __forceinline__ uint64_t group16_excl_scan64(uint64_t v, uint32_t lane, uint64_t& total) {
+    if (__all(v < (1ull << 26))) {
+        uint32_t x = (uint32_t)v;
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+        total = (uint32_t)__shfl((int)x, 15, 16);
+        return x - (uint32_t)v;
+    }
+    uint64_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 16; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 16);
+        if (lane >= d) x += y;
+    }
+    total = __shfl(x, 15, 16);
+    return x - v;
+}
+
+// a predicate's lanes within the caller's group of G lanes (G = 16 or 64), bit 0 = the group's lane 0
+template <uint32_t G>
+__device__ __forceinline__ uint64_t group_ballot(bool b) {
+    const uint64_t m = __ballot(b);
+    return G == 64 ? m : (m >> (threadIdx.x & 48u)) & 0xFFFFull;
+}
+
 // Cooperative chunk walk: one wave per chunk, processed in windows of up to 64 candidates.
 //   1. fill: the wave reads 4 KiB at a time (four 1 KiB coalesced blocks, loads in flight
 //      together) and compacts the positions of the canonical magic bytes 91 8d 4c (find_entry's
@@ -1223,6 +1252,7 @@ struct PlaceFlags {
     bool huge;           // a stream or record past 32-bit sizes
 };
 
+template <uint32_t G>
 __device__ PlaceFlags place_chunk(const FrameParams& P, uint64_t c, uint64_t base_idx, uint64_t base_bytes,
                                   uint64_t owned, bool snappy, bool pay_all, uint32_t lane) {
     PlaceFlags fl{kNone, 0, false, false};
@@ -1239,17 +1269,17 @@ __device__ PlaceFlags place_chunk(const FrameParams& P, uint64_t c, uint64_t bas
         ro_n = so[lane];
         pay_n = sp[lane];
     }
-    for (uint64_t k0 = 0; k0 < owned; k0 += 64) {
+    for (uint64_t k0 = 0; k0 < owned; k0 += G) {
         const uint64_t k = k0 + lane;
         const bool v = k < owned;
         const uint64_t l = l_n, ro = ro_n, pay = pay_n, len = v ? l & kLenMask : 0;
-        if (k + 64 < owned) {
-            l_n = sl[k + 64];
-            ro_n = so[k + 64];
-            pay_n = sp[k + 64];
+        if (k + G < owned) {
+            l_n = sl[k + G];
+            ro_n = so[k + G];
+            pay_n = sp[k + G];
         }
         uint64_t wsum;
-        const uint64_t excl = wave_excl_scan64(len, lane, wsum);
+        const uint64_t excl = G == 64 ? wave_excl_scan64(len, lane, wsum) : group16_excl_scan64(len, lane, wsum);
         bool bad = false;
         if (v) {
             const uint64_t i = base_idx + k;
@@ -1271,17 +1301,17 @@ __device__ PlaceFlags place_chunk(const FrameParams& P, uint64_t c, uint64_t bas
             // (what golang/snappy emits for incompressible input) decodes as a copy
             if (snappy && fg == 0) mixed |= !snappy_single_literal(P.file + start, slen, len);
         }
-        const uint64_t bm = __ballot(bad);
+        const uint64_t bm = group_ballot<G>(bad);
         if (bm) {
             fl.n_bad += (uint64_t)__popcll(bm);
             if (fl.first_bad == kNone) fl.first_bad = base_idx + k0 + (uint64_t)__builtin_ctzll(bm);
         }
         carry += wsum;
-        snappy = snappy && !__any(mixed);
-        mixed = mixed || !snappy;  // keep the wave's verdict
+        snappy = snappy && !group_ballot<G>(mixed);
+        mixed = mixed || !snappy;  // keep the group's verdict
     }
-    fl.mixed = __any(mixed);
-    fl.huge = __any(huge);
+    fl.mixed = group_ballot<G>(mixed) != 0;
+    fl.huge = group_ballot<G>(huge) != 0;
     return fl;
 }
 
@@ -1299,9 +1329,12 @@ __device__ __forceinline__ void merge_place_flags(const FrameParams& P, const Pl
 // Placement: one wave per chunk (place_chunk). Its prologue also does what used to be two launches:
 // the capacity check + sentinel out_off[n] (block 0) and, on the device-resident path, the zero-tail
 // test of a magic mismatch (grid-stride).
+// G lanes per chunk: 64 (a wave) for the wave walk's 32 KiB chunks, 16 for the lane walk's small ones (2..21
+// records of 768 B .. 8 KiB: a wave per chunk left most lanes idle, C2-ref-random place 0.058 -> 0.080 ms)
+template <uint32_t G>
 __global__ void __launch_bounds__(256) k_place(FrameParams P) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & (G - 1);
+    const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
     ScanState* st = P.state;
     if (st->hdr_status != RIO_OK) return;
     if (P.redo && (!st->gz_redo || st->compression != P.redo)) return;  // another codec's redo round
@@ -1346,7 +1379,7 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     // once any wave has found a mixed record the file takes k_snappy_pipe: later waves skip the probe
     const bool snappy = st->compression == RIO_COMP_SNAPPY && !*(volatile const uint32_t*)&st->any_mixed;
     const bool pay_all = st->compression == RIO_COMP_GZIP || st->compression == RIO_COMP_LZW;
-    const PlaceFlags f = place_chunk(P, c, pl.base_idx, pl.base_bytes, pl.owned, snappy, pay_all, lane);
+    const PlaceFlags f = place_chunk<G>(P, c, pl.base_idx, pl.base_bytes, pl.owned, snappy, pay_all, lane);
     if (lane == 0) merge_place_flags(P, f);
 }
 
@@ -2144,6 +2177,17 @@ hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 }
 
 // Host API phase A: framing, then the zero-tail test and the sizes (k_finalize) for the caller.
+// k_place: 16 lanes per chunk for the lane walk's chunks (RIO_PLACE16=0: a wave always)
+#ifndef RIO_PLACE16
+#define RIO_PLACE16 1
+#endif
+static void launch_place(const FrameParams& P, hipStream_t s) {
+    if (RIO_PLACE16 && P.walk_lane)
+        hipLaunchKernelGGL(k_place<16>, dim3(blocks_for(P.n_chunks, 16)), dim3(256), 0, s, P);
+    else
+        hipLaunchKernelGGL(k_place<64>, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+}
+
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
     launch_frame(P, s, ev);
     hipLaunchKernelGGL(k_zero, dim3(256), dim3(256), 0, s, P);
@@ -2166,7 +2210,7 @@ static void launch_gzip_redo(const FrameParams& P0, hipStream_t s) {
     P.redo = RIO_COMP_GZIP;
     launch_gzip_resize(P, s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
-    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+    launch_place(P, s);
     launch_gzip_decode(P, s);
 }
 
@@ -2176,7 +2220,7 @@ static void launch_lzw_redo(const FrameParams& P0, hipStream_t s) {
     P.redo = RIO_COMP_LZW;
     launch_lzw_resize(P, s);
     hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
-    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+    launch_place(P, s);
     launch_lzw_decode(P, s);
 }
 
@@ -2200,7 +2244,7 @@ static void launch_decoders(const FrameParams& P, hipStream_t s, bool snappy_mai
 
 // Decode: placement (+ capacity check, zero tail), the decoders, k_finish (verify + result).
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
-    hipLaunchKernelGGL(k_place, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+    launch_place(P, s);
     if (ev) (void)hipEventRecord(ev[3], s);
     launch_decoders(P, s, true);
     if (ev) (void)hipEventRecord(ev[4], s);
@@ -2212,7 +2256,7 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 // of them (k_snappy_pipe_batch / k_snappy_coop_batch), the other decode kernels per file
 hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev) {
     for (uint32_t f = 0; f < B.n; f++)
-        hipLaunchKernelGGL(k_place, dim3(blocks_for(B.f[f].n_chunks, 4)), dim3(256), 0, s, B.f[f]);
+        launch_place(B.f[f], s);
     if (ev) (void)hipEventRecord(ev[3], s);
     launch_snappy_batch(B, s);
     for (uint32_t f = 0; f < B.n; f++) launch_decoders(B.f[f], s, false);
