@@ -132,7 +132,8 @@ def host_cores() -> int:
 
 def device_digest(t) -> str:
     """Position-sensitive digest of a device tensor's bytes, computed on the device (int64 word sums per
-    4096-word row, the row sums weighted by their index; the tail words and bytes separately). Used to
+    4096-word row, the row sums weighted by their index, every word weighted by its place in its row; the
+    tail words and bytes separately). Used to
     show that the timed steps rebuilt exactly the bytes the warmup produced."""
     import torch
 
@@ -144,9 +145,12 @@ def device_digest(t) -> str:
     m = w.numel() // rows * rows
     parts = [n]
     if m:
-        rs = w[:m].view(-1, rows).sum(dim=1)
+        blk = w[:m].view(-1, rows)
+        rs = blk.sum(dim=1)
         wt = torch.arange(1, rs.numel() + 1, device=t.device, dtype=torch.int64) * 2654435761
-        parts += [int(rs.sum().item()), int((rs * wt).sum().item())]
+        # words weighted by their place in the row too (int64 products wrap): a permutation inside a row shows
+        wr = torch.arange(1, rows + 1, device=t.device, dtype=torch.int64) * 0x9E3779B97F4A7C1
+        parts += [int(rs.sum().item()), int((rs * wt).sum().item()), int((blk * wr).sum().item())]
     if w.numel() > m:
         tail = w[m:]
         wt = torch.arange(1, tail.numel() + 1, device=t.device, dtype=torch.int64) * 40503

@@ -77,3 +77,32 @@ def test_file_traffic_says_whether_it_is_this_tree(tmp_path):
     assert bench.file_traffic("c2", str(f))["traffic_source"]["same_tree"] is True
     # another config's file is not used
     assert bench.file_traffic("c3", str(f)) == {"traffic": None}
+
+
+def test_device_digest_sees_every_byte_and_its_place():
+    """bench.verify's digest (the timed steps must rebuild the warmup's bytes): equal bytes give equal digests;
+    a flipped bit, two words swapped inside one 4096-word row or across rows, or a changed tail byte do not."""
+    import torch
+
+    g = torch.Generator().manual_seed(5)
+    base = torch.randint(0, 256, (3 * 4096 * 8 + 45,), dtype=torch.uint8, generator=g)
+    d0 = bench.device_digest(base)
+    assert bench.device_digest(base.clone()) == d0
+    w = base[: 3 * 4096 * 8].view(torch.int64)
+
+    def changed(edit):
+        x = base.clone()
+        edit(x, x[: 3 * 4096 * 8].view(torch.int64))
+        return bench.device_digest(x) != d0
+
+    assert int(w[10]) != int(w[20]) and int(w[5]) != int(w[4096 + 5])
+
+    def swap(i, j):
+        def f(x, xw):
+            xw[i], xw[j] = int(w[j]), int(w[i])
+        return f
+
+    assert changed(lambda x, xw: x.__setitem__(777, int(x[777]) ^ 1))
+    assert changed(swap(10, 20))  # inside one row
+    assert changed(swap(5, 4096 + 5))  # the same place in two rows
+    assert changed(lambda x, xw: x.__setitem__(x.numel() - 3, (int(x[-3]) + 1) % 256))
