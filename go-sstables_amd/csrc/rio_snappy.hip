@@ -87,6 +87,10 @@ __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
 #ifndef RIO_NT
 #define RIO_NT 1
 #endif
+// RIO_FAR_CP (experiment): cache-policy bits of the far-history buffer loads (gfx950: 1 sc0, 2 nt, 16 sc1)
+#ifndef RIO_FAR_CP
+#define RIO_FAR_CP ((RIO_NT & 2) ? 2 : 0)
+#endif
 // mean decoded bytes per record from which a wave's flush stores are plain (snappy_lane's kPlain)
 constexpr uint64_t kPlainStoreMin = 4096;
 __device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
@@ -925,7 +929,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             if constexpr (!kMulti && !kLow) {
                 // no descriptor to fetch and no source below the arena: the arena descriptor alone
                 const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, (S.kind == 2 && !(RIO_EXP_MEM & 2)) ? o32 + qsrc - r : kOob, 0,
-                                                                      (RIO_NT & 2) ? 2 : 0);
+                                                                      RIO_FAR_CP);
                 S.aux = make_uint4(v.x, v.y, v.z, v.w);
             } else
 #endif
