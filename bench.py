@@ -1152,7 +1152,7 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     if world > 1:
         dist.barrier()
     stage = backend.stage_ms()  # per-stage HIP-event means over the timed steps
-    backend.set_timing(1)
+    backend.set_timing(0)
 
     def verify(what: str) -> None:
         """The decode's result struct and a device-side digest of out / out_off / rec_off / flags after
@@ -1179,7 +1179,7 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
                 backend.step()
             backend.sync()
             cold = backend.stage_ms()
-            backend.set_timing(1)
+            backend.set_timing(0)
             verify("MALL-flushed steps")
         cold_ms = sum(cold) if len(cold) == 4 else 0.0
         # whole job: every rank's bytes over the slowest rank's cold step
@@ -1346,7 +1346,7 @@ def run_decode_inproc(args, devices: list[int], make_be, sizes=None) -> dict:
     stage = bes[0].stage_ms() if plan[0] else []
     for k, (be, part) in enumerate(zip(bes, plan)):
         if part:
-            be.set_timing(1)
+            be.set_timing(0)
             if be.infos() != infos[k] or be.checksums() != digests[k]:
                 raise RuntimeError(f"bench: device slot {k}'s timed steps decoded different results from its warmup")
     total = sum(lengths)

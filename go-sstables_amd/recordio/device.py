@@ -143,6 +143,8 @@ class DeviceDecoder:
         return b, info
 
     def stage_ms(self):
+        """Mean walk / scan / placement / decode milliseconds of the calls recorded since rio_ctx_set_timing
+        (empty while timing is off, the context's default)."""
         ms = (ctypes.c_float * 4)()
         n = L.lib().rio_ctx_last_stage_ms(self.ctx, ms, 4)
         return list(ms)[:n]

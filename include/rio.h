@@ -214,8 +214,10 @@ int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uint8_t* const
 /* Upper bound on records in a file of `len` bytes (the smallest record is v2's empty one, 5 bytes:
  * magic, u = 0, c = 0; v3 / v4 / v1 take 6 / 7 / 20). */
 uint64_t rio_max_records(uint64_t len);
-/* Kernel-timing probe for benchmarks: per-stage device milliseconds of the last
- * rio_device_decode on this ctx (frame, scan, decode); fills up to n entries, returns count. */
+/* Kernel-timing probe for benchmarks: per-stage device milliseconds (walk, scan, placement, decode) averaged
+ * over the decodes recorded since rio_ctx_set_timing; fills up to n entries, returns the count (0 when timing
+ * is off). rio_ctx_set_timing(ctx, slots): record HIP events around the stages of the next `slots` calls
+ * (a ring; 0 = off, the default: the events cost ~3 us each per call). */
 int rio_ctx_last_stage_ms(rio_ctx* ctx, float* ms, int n);
 int rio_ctx_set_timing(rio_ctx* ctx, int enable);
 
