@@ -1,7 +1,9 @@
 """rio_device_decode_ex captured into a HIP graph (include/rio.h: the device-resident call has no host
 synchronisation and is graph-capturable): replaying the captured decode gives the oracle's records, and a
 replay after new bytes of the same length were written into the captured file buffer decodes those bytes
-(every launch reads the file, the sizes and the state from device memory, nothing is baked in at capture)."""
+(every launch reads the file, the sizes and the state from device memory, nothing is baked in at capture). And the
+per-stage timing events: off on a new context (rio_ctx_last_stage_ms gives nothing), recorded once rio_ctx_set_timing asks,
+with the decode's results unchanged either way."""
 import numpy as np
 import pytest
 
@@ -81,3 +83,35 @@ def test_graph_replay_decodes_new_bytes_in_the_captured_buffer():
             g.replay()
         torch.cuda.synchronize()
         assert_same_as_oracle(_arrays(b, dec.info(b)), orc.file_reader_decode_arrays(np.asarray(img)), "graph new bytes")
+
+
+def test_stage_timing_is_off_until_asked():
+    import torch
+
+    from recordio import _lib as L
+    from recordio import generate
+    from recordio.device import DeviceDecoder, to_device_file
+
+    img = generate(20_000, 1024, 2, kind=1, seed=31)
+    want = orc.file_reader_decode_arrays(np.asarray(img))
+    dec = DeviceDecoder(0, own_ctx=True)
+    d_file, n = to_device_file(img)
+    b, info = dec.decode(d_file, n, comp=2)
+    assert dec.stage_ms() == []
+    assert L.lib().rio_ctx_set_timing(dec.ctx, 4) == L.RIO_OK
+    s = torch.cuda.Stream(device=0)
+    for _ in range(3):
+        _clear(b)
+        torch.cuda.synchronize()  # the clear runs on torch's stream, the decode on s
+        dec.launch(d_file, n, b, s, 2)
+    torch.cuda.synchronize()
+    ms = dec.stage_ms()
+    assert len(ms) == 4 and all(x > 0 for x in ms), ms
+    assert_same_as_oracle(_arrays(b, dec.info(b)), want, "timed")
+    assert L.lib().rio_ctx_set_timing(dec.ctx, 0) == L.RIO_OK
+    _clear(b)
+    torch.cuda.synchronize()
+    dec.launch(d_file, n, b, s, 2)
+    torch.cuda.synchronize()
+    assert dec.stage_ms() == []
+    assert_same_as_oracle(_arrays(b, dec.info(b)), want, "untimed")
