@@ -175,10 +175,12 @@ struct rio_ctx {
     uint64_t chunk_bytes = 32768;
     // framing walk (RIO_WALK_LANE): 0 k_walk (one wave per chunk_bytes chunk), 1 k_walk_lane (one lane per
     // lane_chunk_bytes chunk, RIO_LANE_CHUNK_BYTES), 2 auto (default): the lane walk when the context's
-    // previous decode had records of kLaneWalkMin..kLaneWalkMax bytes on average (walk_hint, written by
-    // that decode's finalize_info into page-locked host memory: no host synchronisation), else the wave walk
+    // previous decode had records of kLaneWalkMin..kLaneWalkMax bytes on average (512 B and up on files of 1 GiB and
+    // more; walk_hint, written by that decode's finalize_info into page-locked host memory: no host
+    // synchronisation), else the wave walk
     uint32_t walk_mode = 2;
     uint64_t lane_chunk_bytes = 16384;
+    uint64_t lane_walk_min = 512;  // kLaneWalkSmallMin (RIO_LANE_WALK_MIN)
     uint64_t* walk_hint = nullptr;
     uint64_t coop_min = ~0ull >> 8;
     hipEvent_t* next_events() {
@@ -232,6 +234,11 @@ struct rio_ctx {
 // 1 KiB incompressible records walk 0.269 -> 0.142 ms; 560-byte records even; 48-byte and 36 KiB records
 // slower, so those keep k_walk)
 constexpr uint64_t kLaneWalkMin = 768, kLaneWalkMax = 8192, kLaneWalkChunks = 32768;
+// 512..767-byte records take the lane walk only on files of kLaneWalkSmallChunks lane chunks and more (~30 hops per
+// lane want a wave per SIMD of lanes): C2's 561-byte records in 535 MiB measured even (walk 0.143 -> 0.155 ms, decode
+// 0.999 -> 0.988), the same records in a 5 GB file walk 1.10 -> 0.67 ms (profiles/r5/r5be_lane_walk_min_ab.txt).
+// RIO_LANE_WALK_MIN overrides kLaneWalkSmallMin.
+constexpr uint64_t kLaneWalkSmallMin = 512, kLaneWalkSmallChunks = 65536;
 
 static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P, FileArenas& A) {
     memset(&P, 0, sizeof P);
@@ -245,7 +252,9 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     bool lane = ctx->walk_mode == 1;
     if (ctx->walk_mode == 2 && ctx->walk_hint && len / ctx->lane_chunk_bytes >= kLaneWalkChunks) {
         const uint64_t m = *reinterpret_cast<volatile uint64_t*>(ctx->walk_hint);
-        lane = m >= kLaneWalkMin && m <= kLaneWalkMax;
+        const uint64_t chunks = len / ctx->lane_chunk_bytes;
+        lane = (m >= kLaneWalkMin && m <= kLaneWalkMax) ||
+               (m >= ctx->lane_walk_min && m < kLaneWalkMin && chunks >= kLaneWalkSmallChunks);
     }
     const uint64_t cb = lane ? ctx->lane_chunk_bytes : ctx->chunk_bytes;
     P.walk_lane = lane ? 1u : 0u;
@@ -306,6 +315,7 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     if (c->chunk_bytes < 64 || c->chunk_bytes > (1ull << 30) || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
     c->walk_mode = (uint32_t)std::min<uint64_t>(env_u64("RIO_WALK_LANE", 2), 2);
     c->lane_chunk_bytes = env_u64("RIO_LANE_CHUNK_BYTES", 16384);
+    c->lane_walk_min = env_u64("RIO_LANE_WALK_MIN", kLaneWalkSmallMin);
     if (c->lane_chunk_bytes < 64 || c->lane_chunk_bytes > (1ull << 30) || (c->lane_chunk_bytes & 15))
         c->lane_chunk_bytes = 16384;
     if (hipHostMalloc(reinterpret_cast<void**>(&c->walk_hint), sizeof(uint64_t), hipHostMallocPortable) != hipSuccess) {
