@@ -34,6 +34,8 @@
 namespace rio {
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_frame_ev(const FrameParams& P, hipStream_t s, hipEvent_t walk_start, hipEvent_t walk_stop,
+                           hipEvent_t scan_stop);
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* key_off,
@@ -504,16 +506,13 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
             HIP_TRY(A.rec_desc.ensure((rec_cap[k] + 1) * 16));
             P.rec_desc = A.rec_desc.as<uint4>();
         }
-        // stage events bracket the whole batch: [0] before the first file's framing, [1..2] after
-        // the last file's walk / scan, [3] after placement, [4] after the decode kernels
+        // stage events bracket the whole batch, on the kernels' own dispatches: [0] at the first file's walk start,
+        // [1] at the last file's scan end, [2] .. [4] in launch_phase_b_batch (placement start / end, k_finish start)
         hipEvent_t* e = (ev && g == 0) ? ev : nullptr;
         hipEvent_t* last = (ev && g + kMaxBatch >= n_files) ? ev : nullptr;
-        if (e) HIP_TRY(hipEventRecord(e[0], s));
-        for (uint32_t j = 0; j < B.n; j++) HIP_TRY(launch_frame(B.f[j], s, nullptr));
-        if (last) {
-            HIP_TRY(hipEventRecord(last[1], s));
-            HIP_TRY(hipEventRecord(last[2], s));
-        }
+        for (uint32_t j = 0; j < B.n; j++)
+            HIP_TRY(launch_frame_ev(B.f[j], s, (e && j == 0) ? e[0] : nullptr, nullptr,
+                                    (last && j + 1 == B.n) ? last[1] : nullptr));
         HIP_TRY(launch_phase_b_batch(B, s, last));
     }
     return order_after(ctx, s);

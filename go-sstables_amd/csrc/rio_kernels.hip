@@ -19,6 +19,7 @@
 // Host-API phase A (rio_frame) adds k_zero + k_finalize after the scan. Seek map (k_count91 ..
 // k_seek_jump) and single-record k_read_at / k_seek_next serve the ReadAtI handle.
 // Byte/integer work only: no MFMA. All offsets 64-bit.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -2163,17 +2164,30 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
     return (unsigned)(b == 0 ? 1 : b);
 }
 
-// Framing: k_walk (file header, state reset, chunk walk), k_scan_blocks (both scan levels).
-hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
-    if (ev) (void)hipEventRecord(ev[0], s);
-    if (P.walk_lane)
-        hipLaunchKernelGGL(k_walk_lane, dim3(blocks_for(P.n_chunks, kWalkLaneBlock)), dim3(kWalkLaneBlock), 0, s, P);
+// Stage timing rides on the kernels' own dispatches (hipExtLaunchKernelGGL's start / stop events): a separate
+// hipEventRecord puts a marker packet between two kernels and cost ~5.6 us of idle queue each (rocprofv3 trace of a
+// C2 step, profiles/r5/r5bh_ext_events_ab.txt); without events the launches are plain.
+template <typename K>
+static void launch_ev(K kernel, dim3 g, dim3 b, hipStream_t s, hipEvent_t start, hipEvent_t stop, const FrameParams& P) {
+    if (start || stop)
+        hipExtLaunchKernelGGL(kernel, g, b, 0, s, start, stop, 0, P);
     else
-        hipLaunchKernelGGL(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), 0, s, P);
-    if (ev) (void)hipEventRecord(ev[1], s);
-    hipLaunchKernelGGL(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), 0, s, P);
-    if (ev) (void)hipEventRecord(ev[2], s);
+        hipLaunchKernelGGL(kernel, g, b, 0, s, P);
+}
+
+// Framing: k_walk (file header, state reset, chunk walk), k_scan_blocks (both scan levels). walk_start / walk_stop /
+// scan_stop: the stage events (any may be null).
+hipError_t launch_frame_ev(const FrameParams& P, hipStream_t s, hipEvent_t walk_start, hipEvent_t walk_stop,
+                           hipEvent_t scan_stop) {
+    if (P.walk_lane)
+        launch_ev(k_walk_lane, dim3(blocks_for(P.n_chunks, kWalkLaneBlock)), dim3(kWalkLaneBlock), s, walk_start, walk_stop, P);
+    else
+        launch_ev(k_walk, dim3(blocks_for(P.n_chunks, kWalkWaves)), dim3(64 * kWalkWaves), s, walk_start, walk_stop, P);
+    launch_ev(k_scan_blocks, dim3(blocks_for(P.n_chunks, kScanBlock)), dim3(kScanBlock), s, nullptr, scan_stop, P);
     return hipGetLastError();
+}
+hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
+    return ev ? launch_frame_ev(P, s, ev[0], ev[1], ev[2]) : launch_frame_ev(P, s, nullptr, nullptr, nullptr);
 }
 
 // Host API phase A: framing, then the zero-tail test and the sizes (k_finalize) for the caller.
@@ -2181,11 +2195,11 @@ hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 #ifndef RIO_PLACE16
 #define RIO_PLACE16 1
 #endif
-static void launch_place(const FrameParams& P, hipStream_t s) {
+static void launch_place(const FrameParams& P, hipStream_t s, hipEvent_t start = nullptr, hipEvent_t stop = nullptr) {
     if (RIO_PLACE16 && P.walk_lane)
-        hipLaunchKernelGGL(k_place<16>, dim3(blocks_for(P.n_chunks, 16)), dim3(256), 0, s, P);
+        launch_ev(k_place<16>, dim3(blocks_for(P.n_chunks, 16)), dim3(256), s, start, stop, P);
     else
-        hipLaunchKernelGGL(k_place<64>, dim3(blocks_for(P.n_chunks, 4)), dim3(256), 0, s, P);
+        launch_ev(k_place<64>, dim3(blocks_for(P.n_chunks, 4)), dim3(256), s, start, stop, P);
 }
 
 hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
@@ -2243,25 +2257,25 @@ static void launch_decoders(const FrameParams& P, hipStream_t s, bool snappy_mai
 }
 
 // Decode: placement (+ capacity check, zero tail), the decoders, k_finish (verify + result).
+// stage events: [3] at the placement's end, [4] at k_finish's start, so the decode stage is the decoders' span
 hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
-    launch_place(P, s);
-    if (ev) (void)hipEventRecord(ev[3], s);
+    launch_place(P, s, nullptr, ev ? ev[3] : nullptr);
     launch_decoders(P, s, true);
-    if (ev) (void)hipEventRecord(ev[4], s);
-    hipLaunchKernelGGL(k_finish, dim3(64), dim3(256), 0, s, P);
+    launch_ev(k_finish, dim3(64), dim3(256), s, ev ? ev[4] : nullptr, nullptr, P);
     return hipGetLastError();
 }
 
 // rio_device_decode_batch: phase B of every file of the batch; the Snappy decoders run once over all
 // of them (k_snappy_pipe_batch / k_snappy_coop_batch), the other decode kernels per file
+// stage events: [2] at the first placement's start (the framing of every file ends at [1]), [3] at the last
+// placement's end, [4] at the first k_finish's start
 hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev) {
     for (uint32_t f = 0; f < B.n; f++)
-        launch_place(B.f[f], s);
-    if (ev) (void)hipEventRecord(ev[3], s);
+        launch_place(B.f[f], s, (ev && f == 0) ? ev[2] : nullptr, (ev && f + 1 == B.n) ? ev[3] : nullptr);
     launch_snappy_batch(B, s);
     for (uint32_t f = 0; f < B.n; f++) launch_decoders(B.f[f], s, false);
-    if (ev) (void)hipEventRecord(ev[4], s);
-    for (uint32_t f = 0; f < B.n; f++) hipLaunchKernelGGL(k_finish, dim3(64), dim3(256), 0, s, B.f[f]);
+    for (uint32_t f = 0; f < B.n; f++)
+        launch_ev(k_finish, dim3(64), dim3(256), s, (ev && f == 0) ? ev[4] : nullptr, nullptr, B.f[f]);
     return hipGetLastError();
 }
 
