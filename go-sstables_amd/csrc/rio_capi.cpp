@@ -36,8 +36,8 @@ hipError_t launch_phase_a(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_frame(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
 hipError_t launch_frame_ev(const FrameParams& P, hipStream_t s, hipEvent_t walk_start, hipEvent_t walk_stop,
                            hipEvent_t scan_stop);
-hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev);
-hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev);
+hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev, hipEvent_t done = nullptr);
+hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev, hipEvent_t done = nullptr);
 hipError_t launch_sst_index(const uint8_t* arena, const uint64_t* off, uint64_t n, uint64_t* key_off,
                             uint64_t* key_len, uint64_t* value_off, uint64_t* checksum, uint64_t* result,
                             hipStream_t s);
@@ -403,6 +403,17 @@ static int order_before(rio_ctx* ctx, hipStream_t s) {
     if (ctx->order_valid && ctx->order_stream != s) HIP_TRY(hipStreamWaitEvent(s, ctx->order_ev, 0));
     return RIO_OK;
 }
+// the device-resident calls hand the order event to their last kernel (k_finish) as its completion event instead
+// of recording it behind the call: no marker packet between this call and the next (profiles/r5/r5bi_order_event_ab.txt)
+static int order_event(rio_ctx* ctx, hipEvent_t& e) {
+    if (!ctx->order_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
+    e = ctx->order_ev;
+    return RIO_OK;
+}
+static void order_mark(rio_ctx* ctx, hipStream_t s) {
+    ctx->order_stream = s;
+    ctx->order_valid = true;
+}
 static int order_after(rio_ctx* ctx, hipStream_t s) {
     if (!ctx->order_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(ctx->order_ev, s));
@@ -459,10 +470,13 @@ extern "C" int rio_device_decode_ex(rio_ctx* ctx, const uint8_t* d_file, uint64_
     P.comp_hint = compression;
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     if (int rc2 = order_before(ctx, s)) return rc2;
+    hipEvent_t oe;
+    if (int rc3 = order_event(ctx, oe)) return rc3;
     hipEvent_t* ev = ctx->next_events();
     HIP_TRY(launch_frame(P, s, ev));
-    HIP_TRY(launch_phase_b(P, s, ev));
-    return order_after(ctx, s);
+    HIP_TRY(launch_phase_b(P, s, ev, oe));
+    order_mark(ctx, s);
+    return RIO_OK;
 }
 
 // Batch of device-resident files (BASELINE configs[3]: the 8 files of a GPU's shard in one step):
@@ -483,6 +497,9 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     if (int rc = order_before(ctx, s)) return rc;
+    if (n_files == 0) return RIO_OK;  // nothing enqueued: the previous call's order event still stands
+    hipEvent_t oe;
+    if (int rc = order_event(ctx, oe)) return rc;
     while (ctx->batch.size() < std::min<uint32_t>(n_files, kMaxBatch)) ctx->batch.emplace_back(new FileArenas());
     hipEvent_t* ev = ctx->next_events();
     for (uint32_t g = 0; g < n_files; g += kMaxBatch) {
@@ -513,9 +530,10 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
         for (uint32_t j = 0; j < B.n; j++)
             HIP_TRY(launch_frame_ev(B.f[j], s, (e && j == 0) ? e[0] : nullptr, nullptr,
                                     (last && j + 1 == B.n) ? last[1] : nullptr));
-        HIP_TRY(launch_phase_b_batch(B, s, last));
+        HIP_TRY(launch_phase_b_batch(B, s, last, g + kMaxBatch >= n_files ? oe : nullptr));
     }
-    return order_after(ctx, s);
+    order_mark(ctx, s);
+    return RIO_OK;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -2169,10 +2169,19 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
 // C2 step, profiles/r5/r5bh_ext_events_ab.txt); without events the launches are plain.
 template <typename K>
 static void launch_ev(K kernel, dim3 g, dim3 b, hipStream_t s, hipEvent_t start, hipEvent_t stop, const FrameParams& P) {
-    if (start || stop)
-        hipExtLaunchKernelGGL(kernel, g, b, 0, s, start, stop, 0, P);
-    else
+    if (!start && !stop) {
         hipLaunchKernelGGL(kernel, g, b, 0, s, P);
+        return;
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+        hipExtLaunchKernelGGL(kernel, g, b, 0, s, start, stop, 0, P);
+        return;
+    }
+    // under stream capture the events become record nodes around the kernel
+    if (start) (void)hipEventRecord(start, s);
+    hipLaunchKernelGGL(kernel, g, b, 0, s, P);
+    if (stop) (void)hipEventRecord(stop, s);
 }
 
 // Framing: k_walk (file header, state reset, chunk walk), k_scan_blocks (both scan levels). walk_start / walk_stop /
@@ -2257,11 +2266,12 @@ static void launch_decoders(const FrameParams& P, hipStream_t s, bool snappy_mai
 }
 
 // Decode: placement (+ capacity check, zero tail), the decoders, k_finish (verify + result).
-// stage events: [3] at the placement's end, [4] at k_finish's start, so the decode stage is the decoders' span
-hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
+// stage events: [3] at the placement's end, [4] at k_finish's start, so the decode stage is the decoders' span;
+// `done` (the context's order event) completes with k_finish
+hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev, hipEvent_t done) {
     launch_place(P, s, nullptr, ev ? ev[3] : nullptr);
     launch_decoders(P, s, true);
-    launch_ev(k_finish, dim3(64), dim3(256), s, ev ? ev[4] : nullptr, nullptr, P);
+    launch_ev(k_finish, dim3(64), dim3(256), s, ev ? ev[4] : nullptr, done, P);
     return hipGetLastError();
 }
 
@@ -2269,13 +2279,13 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev) {
 // of them (k_snappy_pipe_batch / k_snappy_coop_batch), the other decode kernels per file
 // stage events: [2] at the first placement's start (the framing of every file ends at [1]), [3] at the last
 // placement's end, [4] at the first k_finish's start
-hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev) {
+hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev, hipEvent_t done) {
     for (uint32_t f = 0; f < B.n; f++)
         launch_place(B.f[f], s, (ev && f == 0) ? ev[2] : nullptr, (ev && f + 1 == B.n) ? ev[3] : nullptr);
     launch_snappy_batch(B, s);
     for (uint32_t f = 0; f < B.n; f++) launch_decoders(B.f[f], s, false);
     for (uint32_t f = 0; f < B.n; f++)
-        launch_ev(k_finish, dim3(64), dim3(256), s, (ev && f == 0) ? ev[4] : nullptr, nullptr, B.f[f]);
+        launch_ev(k_finish, dim3(64), dim3(256), s, (ev && f == 0) ? ev[4] : nullptr, f + 1 == B.n ? done : nullptr, B.f[f]);
     return hipGetLastError();
 }
 
