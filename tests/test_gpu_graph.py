@@ -115,3 +115,28 @@ def test_stage_timing_is_off_until_asked():
     torch.cuda.synchronize()
     assert dec.stage_ms() == []
     assert_same_as_oracle(_arrays(b, dec.info(b)), want, "untimed")
+
+
+def test_graph_capture_with_stage_timing_on():
+    """Under stream capture the stage events (normally on the kernels' own dispatches) are recorded as graph nodes:
+    capture works with timing on, replays give the oracle's records, and the captured events time the replay."""
+    import torch
+
+    from recordio import _lib as L
+    from recordio import generate
+    from recordio.device import DeviceDecoder, to_device_file
+
+    img = generate(20_000, 1024, 2, kind=1, seed=41)
+    dec = DeviceDecoder(0, own_ctx=True)
+    d_file, n = to_device_file(img)
+    b, _ = dec.decode(d_file, n, comp=2)
+    assert L.lib().rio_ctx_set_timing(dec.ctx, 1) == L.RIO_OK
+    g, s = _captured(dec, d_file, n, b, 2)
+    _clear(b)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize()
+    assert_same_as_oracle(_arrays(b, dec.info(b)), orc.file_reader_decode_arrays(np.asarray(img)), "graph timed")
+    ms = dec.stage_ms()
+    assert len(ms) == 4 and all(x >= 0 for x in ms) and ms[3] > 0, ms
