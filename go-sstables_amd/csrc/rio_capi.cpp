@@ -175,6 +175,7 @@ struct rio_ctx {
     std::vector<std::array<hipEvent_t, 5>> ev;
     uint64_t ev_cursor = 0;
     uint64_t chunk_bytes = 32768;
+    bool chunk_auto = true;  // RIO_CHUNK_BYTES unset: larger wave-walk chunks for large records (kBigRecordChunk)
     // framing walk (RIO_WALK_LANE): 0 k_walk (one wave per chunk_bytes chunk), 1 k_walk_lane (one lane per
     // lane_chunk_bytes chunk, RIO_LANE_CHUNK_BYTES), 2 auto (default): the lane walk when the context's
     // previous decode had records of kLaneWalkMin..kLaneWalkMax bytes on average (512 B and up on files of 1 GiB and
@@ -241,6 +242,10 @@ constexpr uint64_t kLaneWalkMin = 768, kLaneWalkMax = 8192, kLaneWalkChunks = 32
 // 0.999 -> 0.988), the same records in a 5 GB file walk 1.10 -> 0.67 ms (profiles/r5/r5be_lane_walk_min_ab.txt).
 // RIO_LANE_WALK_MIN overrides kLaneWalkSmallMin.
 constexpr uint64_t kLaneWalkSmallMin = 512, kLaneWalkSmallChunks = 65536;
+// records of more than kLaneWalkMax bytes on average: wave-walk chunks of at least kBigRecordChunk (a 32 KiB chunk holds
+// at most a few such records and the placement runs a wave per chunk with most lanes idle: C4 place 0.123 -> 0.076 ms,
+// walk 0.61 -> 0.585, +1.2 %, profiles/r5/r5bl_c4_chunk_ab.txt); not when RIO_CHUNK_BYTES sets the size
+constexpr uint64_t kBigRecordChunk = 65536;
 
 static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P, FileArenas& A) {
     memset(&P, 0, sizeof P);
@@ -258,7 +263,9 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
         lane = (m >= kLaneWalkMin && m <= kLaneWalkMax) ||
                (m >= ctx->lane_walk_min && m < kLaneWalkMin && chunks >= kLaneWalkSmallChunks);
     }
-    const uint64_t cb = lane ? ctx->lane_chunk_bytes : ctx->chunk_bytes;
+    uint64_t cb = lane ? ctx->lane_chunk_bytes : ctx->chunk_bytes;
+    if (!lane && ctx->chunk_auto && ctx->walk_hint && *reinterpret_cast<volatile uint64_t*>(ctx->walk_hint) > kLaneWalkMax)
+        cb = std::max<uint64_t>(cb, kBigRecordChunk);
     P.walk_lane = lane ? 1u : 0u;
     P.walk_hint = ctx->walk_hint;
     P.chunk_bytes = cb;
@@ -312,6 +319,7 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     auto* c = new rio_ctx();
     c->device = device;
     c->chunk_bytes = env_u64("RIO_CHUNK_BYTES", 32768);
+    c->chunk_auto = std::getenv("RIO_CHUNK_BYTES") == nullptr;
     // k_walk's candidate bounds take 32-bit differences inside a chunk (magic_mask): chunks stay below
     // 1 GiB; anything outside [64, 1 GiB] or not a multiple of 16 falls back to the default
     if (c->chunk_bytes < 64 || c->chunk_bytes > (1ull << 30) || (c->chunk_bytes & 15)) c->chunk_bytes = 32768;
