@@ -1574,7 +1574,7 @@ __global__ void k_finalize(FrameParams P) {
 // each (k_snappy_pipe lists the lanes; every record when more than kFailLanes did) in place (a record
 // that decoded is rewritten with the same bytes) and flagged where golang/snappy's Decode returns
 // ErrCorrupt; then the last block to finish publishes the result (k_finalize's work). One launch.
-__global__ void __launch_bounds__(256) k_finish(FrameParams P) {
+__device__ __forceinline__ void finish_file(const FrameParams& P) {
     __shared__ uint32_t last;
     ScanState* st = P.state;
     if (st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_SNAPPY && st->n_fail_lanes) {
@@ -1606,6 +1606,9 @@ __global__ void __launch_bounds__(256) k_finish(FrameParams P) {
         finalize_info(P);
     }
 }
+__global__ void __launch_bounds__(256) k_finish(FrameParams P) { finish_file(P); }
+// the files of a batch in one launch: blockIdx.y is the file (each file's 64 blocks take its own ticket)
+__global__ void __launch_bounds__(256) k_finish_batch(FrameBatch B) { finish_file(B.f[blockIdx.y]); }
 
 // ------------------------------------------------------------------------------------------
 // Single record at an arbitrary offset: MMapReader.ReadNextAt (mmap_reader.go:130-203, 298-356)
@@ -2167,8 +2170,8 @@ static inline unsigned blocks_for(uint64_t n, unsigned bs) {
 // Stage timing rides on the kernels' own dispatches (hipExtLaunchKernelGGL's start / stop events): a separate
 // hipEventRecord puts a marker packet between two kernels and cost ~5.6 us of idle queue each (rocprofv3 trace of a
 // C2 step, profiles/r5/r5bh_ext_events_ab.txt); without events the launches are plain.
-template <typename K>
-static void launch_ev(K kernel, dim3 g, dim3 b, hipStream_t s, hipEvent_t start, hipEvent_t stop, const FrameParams& P) {
+template <typename K, typename A>
+static void launch_ev(K kernel, dim3 g, dim3 b, hipStream_t s, hipEvent_t start, hipEvent_t stop, const A& P) {
     if (!start && !stop) {
         hipLaunchKernelGGL(kernel, g, b, 0, s, P);
         return;
@@ -2278,14 +2281,13 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev, h
 // rio_device_decode_batch: phase B of every file of the batch; the Snappy decoders run once over all
 // of them (k_snappy_pipe_batch / k_snappy_coop_batch), the other decode kernels per file
 // stage events: [2] at the first placement's start (the framing of every file ends at [1]), [3] at the last
-// placement's end, [4] at the first k_finish's start
+// placement's end, [4] at k_finish_batch's start
 hipError_t launch_phase_b_batch(const FrameBatch& B, hipStream_t s, hipEvent_t* ev, hipEvent_t done) {
     for (uint32_t f = 0; f < B.n; f++)
         launch_place(B.f[f], s, (ev && f == 0) ? ev[2] : nullptr, (ev && f + 1 == B.n) ? ev[3] : nullptr);
     launch_snappy_batch(B, s);
     for (uint32_t f = 0; f < B.n; f++) launch_decoders(B.f[f], s, false);
-    for (uint32_t f = 0; f < B.n; f++)
-        launch_ev(k_finish, dim3(64), dim3(256), s, (ev && f == 0) ? ev[4] : nullptr, f + 1 == B.n ? done : nullptr, B.f[f]);
+    launch_ev(k_finish_batch, dim3(64, B.n), dim3(256), s, ev ? ev[4] : nullptr, done, B);
     return hipGetLastError();
 }
 
