@@ -269,36 +269,47 @@ def file_traffic(config: str, path: str | None) -> dict:
     return {"traffic": None}
 
 
-def cpu_baseline(images, rec_offs=None, n_records=None, budget_s: float = 20.0) -> dict:
+def cpu_baseline(images, rec_offs=None, n_records=None, budget_s: float = 20.0, check=None) -> dict:
     """The oracle (oracle/rio_oracle.c, a C restatement of the reference reader) on host cores, timed
     on a bounded sample of the same workload:
       one core  — FileReader.ReadNext loop over one file (orc_file_reader_decode), sequential;
       all cores — MMapReader.ReadNextAt record-parallel over each file's known offset table
-                  (orc_parallel_read_at), the files one after another."""
+                  (orc_parallel_read_at), the files one after another.
+    check(out, out_off, rec_off, flags): called once with the oracle's arrays of images[0] from the first
+    one-core run (outside its timing), so the device result the bench timed is compared with the oracle
+    on the full file (`verified` as a correctness claim, not only warmup-vs-timed reproducibility)."""
     sys.path.insert(0, os.path.join(HERE, "tests"))
+    import numpy as np
     import oracle_py as orc
 
     lib = orc.lib()
     image = images[0]
+    checked = None
 
-    def one_file(img):
+    def one_file(img, keep):
+        nonlocal checked
         res = orc.OrcFileResult()
+        t0 = time.perf_counter()
         lib.orc_file_reader_decode(img.ctypes.data, img.shape[0], ctypes.byref(res))
-        n = res.n_records
+        dt = time.perf_counter() - t0
+        n, nb = res.n_records, res.total_out_bytes
+        if keep:
+            def arr(ptr, cnt, dt_):
+                return np.ctypeslib.as_array(ptr, shape=(cnt,)).view(dt_) if cnt else np.zeros(0, dt_)
+            checked = check(arr(res.out, nb, np.uint8), arr(res.out_off, n + 1, np.uint64),
+                            arr(res.rec_off, n, np.uint64), arr(res.flags, n, np.uint8))
         lib.orc_file_result_free(ctypes.byref(res))
-        return n
+        return n, dt
 
     runs, t_total = 0, 0.0
     while runs < 5 and t_total < budget_s:
-        t0 = time.perf_counter()
-        got = one_file(image)
-        t_total += time.perf_counter() - t0
+        got, dt = one_file(image, check is not None and runs == 0)
+        t_total += dt
         runs += 1
         if n_records is not None and got != n_records:
             raise RuntimeError("oracle baseline decoded a different record count")
     one = image.shape[0] / 2**30 * runs / t_total
     cores = host_cores()
-    import numpy as np
 
     # all cores: MMapReader.ReadNextAt record-parallel over every file's known offset table, the files
     # one after another, so a set of fewer files than cores (C4: 8 files, 16 cores) still uses the
@@ -316,11 +327,14 @@ def cpu_baseline(images, rec_offs=None, n_records=None, budget_s: float = 20.0) 
     used = cores
     how = (f"ReadNextAt over the known record offsets of {len(images)} file(s) "
            f"({sum(o.shape[0] for o in offs)} records), {cores} threads, x{runs_a} runs")
-    return {"value": round(all_v, 4), "unit": "GiB/s", "cores": used, "kind": "port",
-            "sample": f"{how}; {os.cpu_count()} cpus visible on the host, CPU share {cores}, {_cpu_model()}",
-            "one_core": {"value": round(one, 4), "unit": "GiB/s", "cores": 1,
-                         "sample": f"one file ({image.shape[0]} B) x{runs} runs, sequential FileReader.ReadNext-loop "
-                                   "restatement"}}
+    res = {"value": round(all_v, 4), "unit": "GiB/s", "cores": used, "kind": "port",
+           "sample": f"{how}; {os.cpu_count()} cpus visible on the host, CPU share {cores}, {_cpu_model()}",
+           "one_core": {"value": round(one, 4), "unit": "GiB/s", "cores": 1,
+                        "sample": f"one file ({image.shape[0]} B) x{runs} runs, sequential FileReader.ReadNext-loop "
+                                  "restatement"}}
+    if check is not None:
+        res["oracle_match"] = checked
+    return res
 
 
 def _cpu_model() -> str:
@@ -1244,8 +1258,10 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
                      "kernel_ms": round(decode_ms, 4), "alg_bytes_per_launch": alg_bytes,
                      **{k: v for k, v in tr.items() if k != "traffic"}},
         # every pass after the warmup (the timed steps, the MALL-flushed steps) rebuilt the warmup's result
-        # struct and the same device-side digest of out / out_off / rec_off / flags (verify() above)
-        "verified": True,
+        # struct and the same device-side digest of out / out_off / rec_off / flags (verify() above); "verified" is
+        # set below once the cpu_baseline leg has compared the first file with the oracle (None when it is skipped)
+        "reproducible": True,
+        "verified": None,
         "verify": {"method": "rio_file_info + device digest of out, out_off, rec_off, flags: warmup vs after "
                              "the timed steps (and after the MALL-flushed pass)",
                    "digest_out": digests[0][0] if digests else None},
@@ -1261,7 +1277,23 @@ def run_decode(args, world, rank, backend, sizes=None) -> dict:
     if warm:
         line["warm_mall"] = warm
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(images, backend.rec_offs(n), n_rec)
+        def against_oracle(out, out_off, rec_off, flags):
+            """The oracle's decode of images[0] against the device arrays the timed steps left (their digests)."""
+            import numpy as np
+            import torch
+
+            dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+            up = [device_digest(torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev))
+                  for a in (out, out_off, rec_off, flags)]
+            return tuple(up) == tuple(digests[0])
+
+        line["cpu_baseline"] = cpu_baseline(images, backend.rec_offs(n), n_rec, check=against_oracle)
+        ok = line["cpu_baseline"].get("oracle_match")
+        if ok is False:
+            raise RuntimeError("bench: the device decode of the first file differs from the oracle's")
+        line["verified"] = bool(ok)
+        line["verify"]["oracle"] = ("the oracle's FileReader loop (oracle/rio_oracle.c) over the whole first file: device "
+                                    "digests of its out, out_off, rec_off, flags equal the timed decode's")
     if rank == 0 and world == 1 and not args.no_e2e and not batch:
         line["e2e"] = e2e_rate(images[0], nb)
     return line
@@ -1364,7 +1396,7 @@ def run_decode_inproc(args, devices: list[int], make_be, sizes=None) -> dict:
                    "devices": devices, "files_per_device": [len(p) for p in plan]},
         "stages_ms_device0": ({"walk": round(stage[0], 4), "scan": round(stage[1], 4), "place": round(stage[2], 4),
                                "decode": round(stage[3], 4)} if len(stage) == 4 else None),
-        "verified": True,
+        "reproducible": True,
         "mode": "inproc" + (" (rehearsal: a device listed more than once)" if len(set(devices)) < nd else ""),
     }
 

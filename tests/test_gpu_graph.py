@@ -140,3 +140,39 @@ def test_graph_capture_with_stage_timing_on():
     assert_same_as_oracle(_arrays(b, dec.info(b)), orc.file_reader_decode_arrays(np.asarray(img)), "graph timed")
     ms = dec.stage_ms()
     assert len(ms) == 4 and all(x >= 0 for x in ms) and ms[3] > 0, ms
+
+
+def test_reserve_covers_the_walk_flip_then_graph_capture(monkeypatch):
+    """rio_ctx_reserve sizes the arenas for every walk the automatic choice can take: a context whose
+    first decode takes the wave walk and whose hint then flips the next one to the lane walk (1 KiB records, lane
+    chunks of 1 KiB here so 40 000 records fill the lane walk's chunk count) allocates nothing after the reserve,
+    and that next call, captured into a HIP graph, replays to the oracle's records."""
+    import torch
+
+    from recordio import _lib as L
+    from recordio import generate
+    from recordio.device import DeviceDecoder, to_device_file
+
+    monkeypatch.setenv("RIO_LANE_CHUNK_BYTES", "1024")
+    img = generate(40_000, 1024, 0, kind=0, seed=31)
+    dec = DeviceDecoder(0, own_ctx=True)  # the context reads RIO_LANE_CHUNK_BYTES at creation
+    d_file, n = to_device_file(img)
+    assert L.lib().rio_ctx_reserve(dec.ctx, n, 40_000, 1) == 0
+    held = L.lib().rio_ctx_arena_bytes(dec.ctx)
+    b = dec.alloc(40_000, 40_000 * 1024)
+    s = torch.cuda.Stream(device=0)
+    dec.launch(d_file, n, b, s, 0)  # fresh hint: the wave walk; its finalize writes ~1 036 bytes per record
+    s.synchronize()
+    assert L.lib().rio_ctx_arena_bytes(dec.ctx) == held
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        dec.launch(d_file, n, b, s, 0)  # the lane walk: 32 times the chunks, no allocation
+    assert L.lib().rio_ctx_arena_bytes(dec.ctx) == held
+    _clear(b)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize()
+    assert L.lib().rio_ctx_arena_bytes(dec.ctx) == held
+    got = _arrays(b, dec.info(b))
+    assert_same_as_oracle(got, orc.file_reader_decode_arrays(np.asarray(img)), "reserve + walk flip + graph")

@@ -158,7 +158,8 @@ def test_bench_run_decode_world2(config, files_per_rank):
         assert steps == 1 + 1 + 3 + 3 and "mall_flushed" in line
         assert line["n_gpus"] == 2 and line["config"]["files_this_rank"] == files_per_rank
         assert line["config"]["records"] == 150 * files_per_rank
-        assert line["verified"] is True and line["verify"]["digest_out"]
+        assert line["reproducible"] is True and line["verify"]["digest_out"]
+        assert line["verified"] is None  # the oracle comparison rides on rank 0's cpu_baseline leg at N=1 only
     assert got[0][2]["value"] == got[1][2]["value"] > 0
 
 
@@ -183,7 +184,7 @@ def test_bench_fails_when_timed_steps_diverge():
     with pytest.raises(RuntimeError, match="different results"):
         bench.run_decode(args, 1, 0, _DriftingBackend(), sizes=(150, 2048))
     line = bench.run_decode(args, 1, 0, OracleBackend(), sizes=(150, 2048))
-    assert line["verified"] is True and line["roofline"]["traffic"] is None
+    assert line["reproducible"] is True and line["roofline"]["traffic"] is None
 
 
 def _bench_cli(args, env_extra=None, timeout=300):
@@ -241,7 +242,7 @@ def test_bench_inproc_devices(config, per_dev):
     line = lines[0]
     assert line["n_gpus"] == 2 and line["config"]["devices"] == [0, 0]
     assert line["config"]["files_per_device"] == per_dev
-    assert line["verified"] is True and "rehearsal" in line["mode"] and line["value"] > 0
+    assert line["reproducible"] is True and "rehearsal" in line["mode"] and line["value"] > 0
 
 
 def test_bench_world_size_mismatch_refused():
@@ -249,3 +250,28 @@ def test_bench_world_size_mismatch_refused():
     r = _bench_cli(["--gpus", "4", "--steps", "1", "--warmup", "0"],
                    env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_cpu_baseline_hands_the_oracle_arrays_to_the_check():
+    """bench.cpu_baseline calls `check` once with the oracle's out / out_off / rec_off / flags of the first file (the
+    bench compares them with the device digests of the timed decode) and reports its answer as oracle_match."""
+    import numpy as np
+
+    import bench
+    import oracle_py as orc
+    from recordio import generate
+
+    img = generate(300, 1024, 2, kind=1, seed=5)
+    want = orc.file_reader_decode_arrays(img)
+    seen = []
+
+    def check(out, out_off, rec_off, flags):
+        seen.append(1)
+        return (np.array_equal(out, want["out"]) and np.array_equal(out_off.astype(np.int64), want["out_off"]) and
+                np.array_equal(rec_off.astype(np.int64), want["rec_off"]) and np.array_equal(flags, want["flags"]))
+
+    res = bench.cpu_baseline([img], np.asarray(want["rec_off"], dtype=np.uint64), 300, budget_s=0.2, check=check)
+    assert seen == [1] and res["oracle_match"] is True
+    res = bench.cpu_baseline([img], np.asarray(want["rec_off"], dtype=np.uint64), 300, budget_s=0.2,
+                             check=lambda *a: False)
+    assert res["oracle_match"] is False
