@@ -10,7 +10,7 @@ rio_device_decode call. value = input file bytes decoded by all ranks / max-over
 Multi-GPU: one process per GPU (torchrun); every rank decodes its own file (file sharding, no
 data-path collective; the only collectives are the timing barrier and the max-over-ranks).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2x|c2g|c2l|c1|c3|c4|c5|wal|idx|enc|readat]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2r|c2x|c2g|c2l|c1|c1s|c3|c4|c5|wal|idx|enc|readat]
 
 c5 (SSTable load + validation + scan), wal (ordered WAL replay from host files) idx (batched
 DiskKeyIndex.Get) and enc (device v4 encode) print their own
@@ -42,6 +42,9 @@ CONFIGS = {
     "c2x": (9_000_000, 1024, 2, 1, "C2 past 4 GiB: recordio v4, 9M x 1 KiB snappy records (text-like), a 4.6 GB file "
                                    "(the read benchmark's largest sizes, recordio_read_test.go:26-27)"),
     "c1": (100_000, 1024, 0, 0, "C1: recordio v4, 100k x 1 KiB uncompressed records (ref generator)"),
+    "c1s": (32_389, 1024, 0, 0, "C1 at the read benchmark's smallest size: recordio v4, a 32 MiB file of 1 KiB "
+                                "uncompressed records (recordio_read_test.go:19: records written until the file "
+                                "reaches 32 MiB)"),
     "c3": (10_000_000, 64, 2, 1, "C3: recordio v4, 10M x 64 B snappy records (header-bound)"),
     "c4": (16_384, 65536, 2, 1, "C4: recordio v4, 8 files x 16384 x 64 KiB snappy records (decompress-bound), "
                                 "sharded over the GPUs"),

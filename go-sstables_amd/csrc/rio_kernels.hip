@@ -1074,6 +1074,7 @@ __device__ __forceinline__ RunSum chunk_run(const FrameParams& P, uint64_t c) {
 constexpr int kScanBlock = 256;
 
 __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]);
+__device__ void scan_finish(const FrameParams& P, const RunSum& total);
 
 // Level 1: inclusive scan of 256 chunk runs per block in LDS (Hillis-Steele, 8 steps). The last
 // block to finish (arrival ticket) runs level 2 over the block runs: one launch for the scan.
@@ -1157,7 +1158,6 @@ __device__ void slow_path(const FrameParams& P, uint32_t ver, uint32_t comp) {
 __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
     __shared__ RunSum carry_s;
     ScanState* st = P.state;
-    const uint32_t ver = st->version, comp = st->compression;
     const int t = threadIdx.x;
     if (P.n_chunks == 0) {
         if (t == 0) {
@@ -1190,6 +1190,14 @@ __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
     }
     const RunSum total = carry_s;
     if (t != 0) return;
+    scan_finish(P, total);
+}
+
+// The file's state from the composed run of all chunks (one thread): the terminal status, the counts, or the
+// sequential repair when a speculative entry did not chain.
+__device__ void scan_finish(const FrameParams& P, const RunSum& total) {
+    ScanState* st = P.state;
+    const uint32_t ver = st->version, comp = st->compression;
     // total.key is chunk 0's forced entry (8): total describes the true chain unless broken.
     if (total.broken) {
         slow_path(P, ver, comp);

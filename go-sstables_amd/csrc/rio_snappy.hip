@@ -40,10 +40,9 @@ namespace {
 constexpr uint32_t kInCh = 4;                    // input ring: 4 chunks = 64 bytes per lane
 constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 // chunks per wave: the balance against the per-chunk drain and setup (A/B on MI355X, records per lane
-// per chunk: C3 64-B records 19 -> 9: decode 0.906 -> 0.870 ms; 4: 0.922, 1: 1.92; C2 stays at 1)
-#ifndef RIO_CHUNKS_PER_WAVE
-#define RIO_CHUNKS_PER_WAVE 8
-#endif
+// per chunk: C3 64-B records 19 -> 9: decode 0.906 -> 0.870 ms; 4: 0.922, 1: 1.92; C2 stays at 1; one chunk of
+// ceil(n / lanes) records per lane on C2: +10 %, round 6)
+constexpr uint64_t kChunksPerWave = 8;
 // copies reaching further back than kFarOff read the output arena (flushed: see snappy_lane); the
 // flush is pipelined one step (+16 bytes of lag). Anything from that bound (208) up to what the
 // history ring still holds (233, static_assert below) is correct; 232 turns the copies of offset
@@ -51,12 +50,8 @@ constexpr uint32_t kD = 4;                       // pipeline depth in iterations
 constexpr uint32_t kFarOff = 232;
 constexpr uint32_t kNoChunk = ~0u;               // slot carries no input chunk
 constexpr uint32_t kLitEff = ~0u;                // "offset" of a literal element (see snappy_lane)
-// RIO_STORE_LATE: the flush store after the step's loads (one more step of flush lag for a far load to see)
-#ifndef RIO_STORE_LATE
-#define RIO_STORE_LATE 1
-#endif
-static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128 + 16 + (RIO_STORE_LATE ? 16 : 0),
-              "far history must be flushed before the parser reads it");
+// the flush store is issued after the step's loads: one more step of flush lag for a far load to see (+16)
+static_assert(kFarOff >= 16 * (kD - 1) + 16 + 128 + 16 + 16, "far history must be flushed before the parser reads it");
 static_assert(kSnappyBlock % 64 == 0, "whole waves");
 
 // materialize x in a VGPR here: the selects that use it can no longer be turned into branches that
@@ -67,55 +62,30 @@ __device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
     return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 
-// cache policy (RIO_NT): 1 = non-temporal flush stores, 2 = non-temporal far loads. Round 3 chose 1 (the
-// arena stores no longer pushed the lanes' input lines out of L2: C2 HBM reads 4.1 -> 3.4 GB per launch,
-// C2 0.9 % slower, C4 3 % faster). Round 5, after the paired input loads and the late flush store: plain
-// stores (0) C4 decode 13.21 -> 12.19 ms (-7.7 %: far copies find their sources written with plain stores
-// in L2 / MALL), C2 equal (+0.2 %). 2 and 3 were slower (+5 %, +8 %, round 3).
-// RIO_LEAN (default 1): fewer VALU compares per step. On gfx950 two waves of a SIMD issue ~1.7 v_add / v_and /
-// v_or / v_xor / v_lshrrev per 4-cycle slot but ~1.15 of the 3-operand integer ops (v_cndmask_e64, v_bfi,
-// v_alignbyte ...) and ~0.95 v_cmp (scripts/op_probe.hip, profiles/r5/r5w_op_probe.txt): the record-end test as
-// one OR and one compare (was three compares), the offset doubling without its range compare, and the emit's
-// ring / far selects from the parse's masks instead of re-comparing the slot kind (C2 decode -2 %, r5x)
-// RIO_IN_CP (experiment): cache-policy bits of the input loads (0 default; 2 non-temporal)
-#ifndef RIO_IN_CP
-#define RIO_IN_CP 0
-#endif
-#ifndef RIO_LEAN
-#define RIO_LEAN 1
-#endif
-#ifndef RIO_NT
-#define RIO_NT 1
-#endif
-// RIO_FAR_CP (experiment): cache-policy bits of the far-history buffer loads (gfx950: 1 sc0, 2 nt, 16 sc1)
-#ifndef RIO_FAR_CP
-#define RIO_FAR_CP ((RIO_NT & 2) ? 2 : 0)
-#endif
+// Cache policy. Flush stores: non-temporal below kPlainStoreMin bytes per record (round 3: the arena stores no longer
+// push the lanes' input lines out of L2: C2 HBM reads 4.1 -> 3.4 GB per launch), plain from it (round 5: C4's far
+// copies find their sources in L2 / MALL, decode 13.21 -> 12.19 ms). Far and input loads plain: non-temporal far loads
+// +5 % (C2) / +11 % (C4), non-temporal input loads +10-13 % (they lose the paired loads' line reuse), sc0 / sc1 far loads
+// even (round 6, C2 and C4).
+// Compares are cheap to remove: two waves of a SIMD issue ~1.7 v_add / v_and / v_or / v_xor / v_lshrrev per 4-cycle slot
+// but ~1.15 of the 3-operand integer ops (v_cndmask_e64, v_bfi, v_alignbyte ...) and ~0.95 v_cmp (scripts/op_probe.hip,
+// profiles/r5/r5w_op_probe.txt): the record-end test is one OR and one compare, the offset doubling has no range compare,
+// the emit's ring / far selects use the parse's masks (C2 decode -2 %, r5x).
 // mean decoded bytes per record from which a wave's flush stores are plain (snappy_lane's kPlain)
 constexpr uint64_t kPlainStoreMin = 4096;
-__device__ __forceinline__ void st_out(uint8_t* p, uint4 v) {
-    if (RIO_NT & 1) stu16_nt(p, v); else stu16(p, v);
-}
-__device__ __forceinline__ uint4 ld_far(const uint8_t* p) { return (RIO_NT & 2) ? ldu16_nt(p) : ldu16(p); }
 
-// RIO_BUF: the input prefetch and the flush store go through buffer descriptors (32-bit offsets from
-// the wave's own file / arena base, wave-uniform descriptors in SGPRs); a lane with nothing to load or
-// store passes an offset past the descriptor's range, which the range check drops (no sink line, no
-// 64-bit address arithmetic or pointer selects). A wave's records span less than 0xF0000000 bytes of
-// file and arena (snappy_lane checks; a wave past that decodes its records one thread each), so every
-// real offset fits 32 bits and kOob is out of range, whatever the file's size.
-#ifndef RIO_BUF
-#define RIO_BUF 1
-#endif
+// Buffer descriptors: the input prefetch, the flush store and the far-history load use 32-bit offsets from the wave's
+// own file / arena base (wave-uniform descriptors in SGPRs); a lane with nothing to load or store passes an offset past
+// the descriptor's range, which the range check drops (no sink line, no 64-bit address arithmetic). A wave's records
+// span less than 0xF0000000 bytes of file and arena (snappy_lane checks; a wave past that decodes its records one
+// thread each), so every real offset fits 32 bits and kOob is out of range, whatever the file's size.
 constexpr uint32_t kOob = 0xFFFFFFC0u;
-// RIO_IN_PAIR: in the single-record-per-lane loop (kMulti = false: C2's and C4's shape) the input prefetch
-// loads two adjacent 16-byte chunks (32 bytes) on even steps and none on odd steps, so the second load of a
-// pair finds its line already requested by the first: half the L1 misses (L2 requests) of the lane-private
-// input stream for the same instruction count. Round 5, one box, parity subset green: C2 decode -1.7 %,
-// C4 -0.5 %; in the multi-record loop (C3) +3.5 %, so that loop keeps one chunk per step.
-#ifndef RIO_IN_PAIR
-#define RIO_IN_PAIR 1
-#endif
+// Paired input loads: in the single-record-per-lane loop (kMulti = false: C2's and C4's shape) the input prefetch
+// loads two adjacent 16-byte chunks (32 bytes) on even steps and none on odd steps, so the second load of a pair
+// finds its line already requested by the first: half the L1 misses of the lane-private input stream for the same
+// instruction count (round 5: C2 decode -1.7 %, C4 -0.5 %; the multi-record loop (C3) +3.5 %, so it keeps one chunk
+// per step). ONE load per step serving either the far piece or the next input chunk (2 vector-memory operations per
+// step instead of 3) measured +4 % on C2 and +5-12 % on C4 (round 6, profiles/r6): it loses the pairing.
 // lane k's 64-bit value (k wave-uniform) into scalars
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t k) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
@@ -135,11 +105,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
 
 // Files the 32-bit lane-stream positions cannot cover take the wave-per-record decoder.
 __device__ __forceinline__ bool snappy_wide(const FrameParams& P, const ScanState* st) {
-#if RIO_BUF
     return st->huge_streams;  // per-wave buffer bases: any file and arena size (snappy_lane)
-#else
-    return st->huge_streams || P.len >= 0xFFFFFF00ull || st->total_bytes >= 0xFFFFFF00ull;
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -516,24 +482,7 @@ __device__ __forceinline__ void coop_file(const FrameParams& P, CoopLds& S, uint
 // decode C2 1.19 -> 1.13 ms, C3 0.86 -> 0.80, C4 13.9 -> 13.6 (gpurun_out/r3k).
 // ------------------------------------------------------------------------------------------
 namespace {
-// RIO_EXP_OCC (timing-only experiment, WRONG output): a 32-row history ring, so three 4-wave
-// workgroups fit a CU (12 waves) with the same instruction stream: the upper bound of what a third
-// wave per SIMD buys
-#ifndef RIO_EXP_OCC
-#define RIO_EXP_OCC 0
-#endif
-#if RIO_EXP_OCC && !defined(RIO_TIMING_ONLY_BUILD)
-#error "RIO_EXP_OCC produces wrong output: build it only as a timing experiment (-DRIO_TIMING_ONLY_BUILD)"
-#endif
-// RIO_EXP_MEM (timing-only, WRONG output; the control flow does not depend on output bytes): bit 0 sends the
-// flush stores out of range, bit 1 the far-history loads (measures what each stream costs the decoder)
-#ifndef RIO_EXP_MEM
-#define RIO_EXP_MEM 0
-#endif
-#if RIO_EXP_MEM && !defined(RIO_TIMING_ONLY_BUILD)
-#error "RIO_EXP_MEM produces wrong output: build it only as a timing experiment (-DRIO_TIMING_ONLY_BUILD)"
-#endif
-constexpr uint32_t kColRows = RIO_EXP_OCC ? 32 : 64;  // history rows per lane: 256 bytes
+constexpr uint32_t kColRows = 64;  // history rows per lane: 256 bytes
 constexpr uint32_t kColInRows = 16;                // input rows per lane: 64 bytes = kInCh chunks
 constexpr uint32_t kColWaves = kSnappyBlock / 64;
 constexpr uint32_t kColRow = kColWaves * 256;      // bytes per row of the four waves (1 KiB)
@@ -541,16 +490,16 @@ constexpr uint32_t kColH = kColRows * kColRow;     // history image (64 KiB: 16-
 constexpr uint32_t kColI = kColInRows * kColRow;   // input image (16 KiB)
 constexpr uint32_t kColLds = kColH + kColI;
 constexpr uint32_t kCoopSlice = kColH / kColWaves; // a wave's contiguous slice for the wave decoder
-static_assert(RIO_EXP_OCC || kColH == 65536, "history addresses wrap at 16 bits");
+static_assert(kColH == 65536, "history addresses wrap at 16 bits");
 static_assert(kColInRows == 4 * kInCh, "input image holds the input ring's chunks");
 static_assert(sizeof(CoopLds) <= kCoopSlice, "wave decoder LDS must fit a history slice");
 // live history: ring-copy sources reach kFarOff + 3 bytes below the destination, the emit writes
 // the 16 bytes from d - r; the flush reads complete blocks at most 127 bytes below d
-static_assert(RIO_EXP_OCC || kFarOff + 3 + 16 + 4 <= kColRows * 4, "history image must hold the copy reach");
+static_assert(kFarOff + 3 + 16 + 4 <= kColRows * 4, "history image must hold the copy reach");
 
 struct ColSlot {
     uint4 in;        // input chunk in_c (load in flight)
-    uint4 in2;       // RIO_IN_PAIR: input chunk in_c + 1
+    uint4 in2;       // paired loads: input chunk in_c + 1
     uint4 aux;       // far-copy bytes [q - r, q - r + 16) or the next record's descriptor (in flight)
     uint32_t x0, x1, x2, x3, x4;  // literal: input rows from (src - r) & ~3 (read at parse)
     uint32_t in_c;
@@ -558,7 +507,7 @@ struct ColSlot {
     uint32_t kind;   // 0 literal, 1 ring copy, 2 far copy, 3 far copy loaded from q (see the emit)
     uint32_t q;      // ring copy: source output position; literal: byte shift of x0..x4
     uint32_t desc;   // aux carries the next record's descriptor
-    uint32_t ringm, farm;  // RIO_LEAN: kind 1 / kind 2 as all-ones masks (the emit selects by v_bfi, no compare)
+    uint32_t ringm, farm;  // kind 1 / kind 2 as all-ones masks (the emit selects by v_bfi, no compare)
 };
 __device__ __forceinline__ ColSlot col_empty_slot() {
     ColSlot S;
@@ -600,18 +549,17 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     auto hrow = [&](uint32_t b) __attribute__((always_inline)) { return ((b << 8) & (kColH - kColRow)) | wl; };
     // v_pk_add_u16: the low half wraps at 64 KiB, the high half (0) stays 0
     auto hnext = [&](uint32_t a) __attribute__((always_inline)) {
-        if (RIO_EXP_OCC) return (a + kColRow) & (kColH - 1u);
         const u16x2 v = __builtin_bit_cast(u16x2, a) + u16x2{(uint16_t)kColRow, 0};
         return __builtin_bit_cast(uint32_t, v);
     };
     auto irow = [&](uint32_t b) __attribute__((always_inline)) { return ((b << 8) & (kColI - kColRow)) | wl; };
     auto inext = [&](uint32_t a) __attribute__((always_inline)) { return (a + kColRow) & (kColI - 1u); };
 
-    constexpr bool kPair = RIO_IN_PAIR && RIO_BUF && !kMulti;  // paired input prefetch (RIO_IN_PAIR)
+    constexpr bool kPair = !kMulti;  // paired input prefetch
     // flush stores: plain (kPlain) for records of kPlainStoreMin bytes and more (C4's 64 KiB records: far
     // copies then find their sources in L2 / MALL, decode -7.7 %), non-temporal otherwise (C2 the same
-    // speed with 2.84 instead of 3.62 GB of reads per launch; C3 plain +1.8 %); RIO_NT overrides (bit 0)
-    constexpr bool kStoreNT = (RIO_NT & 1) && !kPlain;
+    // speed with 2.84 instead of 3.62 GB of reads per launch; C3 plain +1.8 %)
+    constexpr bool kStoreNT = !kPlain;
     const bool live = r0 < r1;
     uint8_t* const out = P.out;
     // d0 / o0: rec_desc and out_off of r0, loaded by the caller (zero when !live)
@@ -624,7 +572,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     const uint64_t base = start0 & ~15ull;
     const uint4* sa = reinterpret_cast<const uint4*>(P.file + base);
     const uint32_t lastc = live && base < P.len ? (uint32_t)umin((P.len - 1 - base) >> 4, (uint64_t)0x0FFFFFFF) : 0u;
-#if RIO_BUF
     // (only a file or arena of 3.75 GiB or more can hold such a wave: the common case skips the loads)
     if (P.len >= 0xF0000000ull || P.state->total_bytes >= 0xF0000000ull) {
         // the wave's input and output spans from its lowest record to the end of lane 63's last one
@@ -648,7 +595,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             return okw;
         }
     }
-#endif
     // prime the input image with chunks [0, 4)
     uint32_t whi = live ? umin(kInCh, lastc + 1) : 0u;
     for (uint32_t c = 0; c < whi; c++) {
@@ -672,7 +618,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     uint32_t nds = (kMulti && live && r0 + 1 < r1) ? 0u : 3u;
     uint32_t d = 0, fb = 0;
 
-#if RIO_BUF
     // the buffer descriptors start at the wave's lowest record (lane 0's: a wave takes consecutive
     // records), so the 32-bit offsets are relative to it and any file or arena size works; the arena
     // base stays 16 bytes below the wave's first output byte (a far copy reads from q - r, r <= 3),
@@ -692,16 +637,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 #pragma unroll
     for (uint32_t jj = 0; jj < 4; jj++)
         obase[jj] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((16u * jj + (lane >> 2)) * 4), (int)o32);
-#else
-    uint8_t* obase[4];
-#pragma unroll
-    for (uint32_t jj = 0; jj < 4; jj++) {
-        const int src = (int)((16u * jj + (lane >> 2)) * 4);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)o0);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(o0 >> 32));
-        obase[jj] = out + (((uint64_t)hi << 32) | lo);
-    }
-#endif
 
     ColSlot S0 = col_empty_slot(), S1 = col_empty_slot(), S2 = col_empty_slot(), S3 = col_empty_slot();
     uint32_t drain = 0, qsrc = 0;
@@ -730,7 +665,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
 
         // 2. emit the piece parsed kD steps ago: destination dwords of bytes [d - r, d - r + 16)
         {
-#if RIO_LEAN
             const uint32_t rm = S.ringm, fm = S.farm;
             auto bsel = [](uint32_t m, uint32_t a, uint32_t b) __attribute__((always_inline)) { return (a & m) | (b & ~m); };
             uint32_t X0 = bsel(rm, wL0, S.x0), X1 = bsel(rm, wL1, S.x1), X2 = bsel(rm, wL2, S.x2), X3 = bsel(rm, wL3, S.x3),
@@ -742,19 +676,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             D1 = bsel(fm, S.aux.y, D1);
             D2 = bsel(fm, S.aux.z, D2);
             D3 = bsel(fm, S.aux.w, D3);
-#else
-            const bool ring = S.kind == 1;
-            uint32_t X0 = ring ? wL0 : S.x0, X1 = ring ? wL1 : S.x1, X2 = ring ? wL2 : S.x2, X3 = ring ? wL3 : S.x3,
-                     X4 = ring ? wL4 : S.x4;
-            const uint32_t sh = ring ? wSh : S.q;
-            uint32_t D0 = __builtin_amdgcn_alignbyte(X1, X0, sh), D1 = __builtin_amdgcn_alignbyte(X2, X1, sh),
-                     D2 = __builtin_amdgcn_alignbyte(X3, X2, sh), D3 = __builtin_amdgcn_alignbyte(X4, X3, sh);
-            const bool far = S.kind == 2;
-            D0 = far ? S.aux.x : D0;
-            D1 = far ? S.aux.y : D1;
-            D2 = far ? S.aux.z : D2;
-            D3 = far ? S.aux.w : D3;
-#endif
             // kind 3 (rare: a far source in the first bytes of the arena, lane of the file's first
             // record): aux holds bytes [q, q + 16), shifted up by r here
             if (kLow && __builtin_expect(__any(S.kind == 3), 0)) {
@@ -847,14 +768,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t cap = 16u - umax(sh, r);
             const uint32_t n = go ? umin(rem1, umin(cap, eff1)) : 0u;
             S.n = n;
-#if RIO_LEAN
             const bool farc = !lit1 && n != 0 && eff1 > kFarOff;
             S.kind = lit1 ? 0u : (farc ? 2u : 1u);
             S.ringm = (lit1 || farc) ? 0u : ~0u;
             S.farm = farc ? ~0u : 0u;
-#else
-            S.kind = lit1 ? 0u : ((n != 0 && eff1 > kFarOff) ? 2u : 1u);
-#endif
             qsrc = pd - eff1;
             // literal rows from (s + sh - r) & ~3 (the bytes below s + sh are masked at the emit)
             const uint32_t ls = s + sh - r;
@@ -865,15 +782,10 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.x3 = col_ld(L, c3);
             S.x4 = col_ld(L, c4);
             // literal: the shift (low 2 bits) of x0..x4; a far copy's q goes unused at the emit
-#if RIO_LEAN
             S.q = (lit1 || farc) ? ls : qsrc;
-#else
-            S.q = S.kind == 1 ? qsrc : ls;
-#endif
             s += sh + (lit1 ? n : 0u);
             rem = rem1 - n;
             pd += n;
-#if RIO_LEAN
             // a piece that covered its whole offset doubles it (the source is periodic in eff1; n <= 16,
             // so eff stays <= 32, a ring copy); the record end tested as one OR (one compare, not three)
             eff = eff1 + ((n == eff1) ? n : 0u);
@@ -881,13 +793,6 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             uint32_t at_z = rem | (s ^ s_end) | (uint32_t)pdone;
             pin_v(at_z);
             if (at_z == 0) {
-#else
-            eff = (eff1 < 16 && n == eff1) ? 2 * eff1 : eff1;
-            s = badn ? s_end : s;
-            uint32_t at_end = (uint32_t)!pdone & (uint32_t)(rem == 0) & (uint32_t)(s == s_end);
-            pin_v(at_end);
-            if (at_end) {
-#endif
                 const bool bad_len = pd != rd_end;
                 bad = bad || bad_len;
                 rem = bad_len ? rd_end - pd : rem;
@@ -904,19 +809,13 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
                 nds = sw ? (k + 1 < r1 ? 0u : 3u) : nds;
             }
         }
-        // this step's owners' blocks (the far-history load below is issued after the store; with
-        // RIO_STORE_LATE after the input prefetch, so a wait for this step's loads three steps on does not
-        // also wait for this store: vmcnt retires stores and loads in issue order)
+        // this step's owners' blocks, stored after the step's loads (after the input prefetch), so a wait for this
+        // step's loads three steps on does not also wait for this store: vmcnt retires stores and loads in issue order
         auto flush_store = [&]() __attribute__((always_inline)) {
-#if RIO_BUF
             const v4u32b w = {fv_now.x, fv_now.y, fv_now.z, fv_now.w};
-            __builtin_amdgcn_raw_buffer_store_b128(w, rsrc_out, ((ofb_now >> 31) && !(RIO_EXP_MEM & 1)) ? obase[j & 3u] + fpos_now : kOob, 0,
+            __builtin_amdgcn_raw_buffer_store_b128(w, rsrc_out, (ofb_now >> 31) ? obase[j & 3u] + fpos_now : kOob, 0,
                                                    kStoreNT ? 2 : 0);
-#else
-            st_out((ofb_now >> 31) ? obase[j & 3u] + fpos_now : sink, fv_now);
-#endif
         };
-        if (!RIO_STORE_LATE) flush_store();
         fb += ((lane >> 4) == (j & 3u) && ready_now) ? 64u : 0u;
 
         // far history (destination-aligned: from q - r), or the next record's descriptor, or a placeholder
@@ -925,21 +824,17 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             S.desc = want_desc ? 1u : 0u;
             nds = want_desc ? 1u : nds;
             const uint32_t r = (pd - S.n) & 3u;  // the piece's destination alignment
-#if RIO_BUF
             if constexpr (!kMulti && !kLow) {
                 // no descriptor to fetch and no source below the arena: the arena descriptor alone
-                const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, (S.kind == 2 && !(RIO_EXP_MEM & 2)) ? o32 + qsrc - r : kOob, 0,
-                                                                      RIO_FAR_CP);
+                const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, S.kind == 2 ? o32 + qsrc - r : kOob, 0, 0);
                 S.aux = make_uint4(v.x, v.y, v.z, v.w);
-            } else
-#endif
-            {
+            } else {
                 // 16 bytes from q - r would start below the arena: load from q, shift at the emit (kind 3)
                 const bool below = kLow && low_base && S.kind == 2 && qsrc < r;
                 S.kind = below ? 3u : S.kind;
                 const uint8_t* ap = S.kind >= 2 ? gout_m3 + (qsrc + 3u - (below ? 0u : r))
                                                 : (want_desc ? reinterpret_cast<const uint8_t*>(P.rec_desc + (k + 1)) : sink);
-                S.aux = ld_far(ap);
+                S.aux = ldu16(ap);
             }
         }
 
@@ -948,8 +843,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
           if ((j & 1u) == 0) {  // a pair (cn, cn + 1) when the ring has room for both
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn + 1 < a + kInCh;
-            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, RIO_IN_CP);
-            const v4u32b v2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn + 16u : kOob, 0, RIO_IN_CP);
+            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, 0);
+            const v4u32b v2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn + 16u : kOob, 0, 0);
             S.in = make_uint4(v.x, v.y, v.z, v.w);
             S.in2 = make_uint4(v2.x, v2.y, v2.z, v2.w);
             S.in_c = take ? cn : kNoChunk;
@@ -960,17 +855,13 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         } else {
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn < a + kInCh;
-#if RIO_BUF
-            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, RIO_IN_CP);
+            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, 0);
             S.in = make_uint4(v.x, v.y, v.z, v.w);
-#else
-            S.in = *reinterpret_cast<const uint4*>(take ? reinterpret_cast<const uint8_t*>(sa + cn) : sink);
-#endif
             S.in_c = take ? cn : kNoChunk;
             cn += take ? 1u : 0u;
         }
 
-        if (RIO_STORE_LATE) flush_store();
+        flush_store();
 
         // 6. land the next slot's input chunk(s), then read the next step's parser window
         if constexpr (kPair) {
@@ -1079,8 +970,7 @@ __global__ void __launch_bounds__(kSnappyBlock) k_snappy_pipe(FrameParams P) {
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t g = (uint64_t)wave * gridDim.x + blockIdx.x;
     uint8_t* sink = P.sink + g * 64;
-    constexpr uint64_t kCpw = RIO_CHUNKS_PER_WAVE;
-    const uint64_t rpc = n >= kCpw * 64 * waves ? n / (kCpw * 64 * waves) : 1;
+    const uint64_t rpc = n >= kChunksPerWave * 64 * waves ? n / (kChunksPerWave * 64 * waves) : 1;
     const uint64_t per = 64 * rpc, nchunks = (n + per - 1) / per;
     uint64_t chunk = g;
     while (chunk < nchunks) {

@@ -4,14 +4,17 @@
 // decoder (80 KiB of LDS per 4-wave workgroup), three vector-memory operations per step in the decoder's order:
 //   store   cooperative flush: owners 16 (j % 4) .. + 15, each quad stores one owner's next 64-B block
 //           when the owner has one complete (output grows 1024 / 136 bytes per step);
-//   far     16 B at a 4-aligned position 232..1000 bytes below the lane's output position, in 11 % of
-//           the steps (C2: 16 far pieces per record), from a hash of (record, step);
+//   far     16 B at a 4-aligned position 232..1000 bytes below the lane's output position, 16 per record
+//           (C2's far pieces; 11 % of 136 steps), from a hash of (record, step);
 //   input   the lane's next 16-B input chunk whenever its parse position (560 B per record) needs it,
 //           4 chunks ahead (the decoder's 64-B input ring).
 // Loads are consumed 3 steps after issue (4 rotating slots, as the decoder's vmcnt schedule). V VALU per
 // step (v_alignbyte chains) stand in for the decode. Modes switch one stream to out-of-range offsets, or
 // the input to a quad-cooperative prefetch (4 lanes load 64 contiguous bytes of one owner's record; each
 // owner is served every 4th step).
+// Round 6: the step count per record (kSteps) and LDS dword reads / writes per step (kR / kW, per-lane columns of
+// the decoder's image layout: conflict-free) are template parameters, so candidate step shapes are priced before
+// they are built: "cand" rows (main) give each candidate's (steps, VALU, VMEM streams, LDS ops).
 // Standalone: hipcc --offload-arch=gfx950 -O3 scripts/mem_replay.hip -o scripts/mem_replay && scripts/mem_replay
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,7 +33,6 @@ constexpr uint32_t kRecs = 1u << 20;
 constexpr uint32_t kInStride = 576;  // compressed record + header
 constexpr uint32_t kInLen = 560;
 constexpr uint32_t kOutLen = 1024;
-constexpr uint32_t kSteps = 136;
 constexpr uint32_t kOob = 0xFFFFFFC0u;
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
@@ -43,7 +45,7 @@ __device__ __forceinline__ uint32_t hsh(uint32_t a, uint32_t b) {
     return h ^ (h >> 13);
 }
 
-template <int kMode, int kV>
+template <int kMode, int kV, int kSteps = 136, int kR = 0, int kW = 0>
 __global__ void __launch_bounds__(256) k_replay(const uint8_t* in, uint8_t* out, uint32_t* res, uint32_t* next) {
     extern __shared__ uint32_t lds[];
     const uint32_t lane = threadIdx.x & 63;
@@ -87,7 +89,7 @@ __global__ void __launch_bounds__(256) k_replay(const uint8_t* in, uint8_t* out,
             {
                 const uint32_t h = hsh(r, j);
                 const uint32_t back = 232 + (h >> 8) % 768;
-                const bool far = (h & 1023) < 113 && d >= back + 16 && kMode != kNoFar && kMode != kNone && kMode != kNoFarCoopIn;
+                const bool far = (h & 1023) < 16u * 1024u / kSteps && d >= back + 16 && kMode != kNoFar && kMode != kNone && kMode != kNoFarCoopIn;
                 if (kMode == kMerged) {
                     // one load per step: the far piece when there is one, else the input chunk
                     const uint32_t need = 4 + (j * kInLen / kSteps) / 16;
@@ -122,6 +124,15 @@ __global__ void __launch_bounds__(256) k_replay(const uint8_t* in, uint8_t* out,
                     cn += go ? 1 : 0;
                 }
             }
+            // LDS: kR dword reads and kW dword writes of this lane's own column (row stride 1 KiB, as the decoder's
+            // images), rows from the step index; the reads feed the VALU chains so they are not dropped
+            {
+                const uint32_t col = (threadIdx.x >> 6) * 64 + lane;
+#pragma unroll
+                for (int k = 0; k < kR; k++) x1 ^= lds[(((j * 7 + k * 5 + x3) & 63) << 8) | col];
+#pragma unroll
+                for (int k = 0; k < kW; k++) lds[(((j * 3 + k) & 63) << 8) | col] = x2 + k;
+            }
 #pragma unroll
             for (int k = 0; k < kV / 4; k++) {
                 asm volatile("v_alignbyte_b32 %0, %0, %0, 1" : "+v"(x));
@@ -144,17 +155,18 @@ __global__ void __launch_bounds__(256) k_replay(const uint8_t* in, uint8_t* out,
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w ^ x ^ x1 ^ x2 ^ x3) == 0x12345678u) res[0] = 1;
 }
 
-template <int kMode, int kV>
+template <int kMode, int kV, int kSteps = 136, int kR = 0, int kW = 0>
 static void run(const char* name, const uint8_t* in, uint8_t* out, uint32_t* res, uint32_t* next) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_replay<kMode, kV>), hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_replay<kMode, kV, kSteps, kR, kW>),
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
     float best = 1e9;
     for (int it = 0; it < 4; it++) {
         CK(hipMemset(next, 0, 4));
         CK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL((k_replay<kMode, kV>), dim3(512), dim3(256), 80 * 1024, 0, in, out, res, next);
+        hipLaunchKernelGGL((k_replay<kMode, kV, kSteps, kR, kW>), dim3(512), dim3(256), 80 * 1024, 0, in, out, res, next);
         CK(hipGetLastError());
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
@@ -162,7 +174,7 @@ static void run(const char* name, const uint8_t* in, uint8_t* out, uint32_t* res
         CK(hipEventElapsedTime(&ms, e0, e1));
         if (it > 0 && ms < best) best = ms;
     }
-    printf("replay %-28s V=%3d: %7.3f ms\n", name, kV, best);
+    printf("replay %-34s S=%3d V=%3d R=%2d W=%2d: %7.3f ms\n", name, kSteps, kV, kR, kW, best);
     fflush(stdout);
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
@@ -181,7 +193,22 @@ static void row(const uint8_t* in, uint8_t* out, uint32_t* res, uint32_t* next) 
     run<kMasked, kV>("idle lanes exec-masked", in, out, res, next);
 }
 
-int main() {
+// round 6 candidates (steps per record from scripts/lane_sim-style counts on C2, VALU / LDS per step from hipcc -S of
+// each step shape): current decoder, the merged far + input load, two-piece steps (a second element in the
+// same 16-byte destination window), both
+static void candidates(const uint8_t* in, uint8_t* out, uint32_t* res, uint32_t* next) {
+    run<kAll, 160, 136, 18, 4>("cand current (3 VMEM)", in, out, res, next);
+    run<kMerged, 166, 136, 18, 4>("cand merged load (2 VMEM)", in, out, res, next);
+    run<kAll, 160, 136, 0, 0>("cand current, no LDS", in, out, res, next);
+    run<kAll, 128, 136, 18, 4>("cand current at 128 VALU", in, out, res, next);
+    run<kMerged, 128, 136, 18, 4>("cand merged at 128 VALU", in, out, res, next);
+    run<kAll, 230, 96, 24, 4>("cand two-piece shared window", in, out, res, next);
+    run<kMerged, 236, 96, 24, 4>("cand two-piece + merged", in, out, res, next);
+    run<kAll, 260, 86, 28, 8>("cand two-piece separate windows", in, out, res, next);
+    run<kMerged, 200, 96, 24, 4>("cand two-piece + merged at 200", in, out, res, next);
+}
+
+int main(int argc, char** argv) {
     setvbuf(stdout, nullptr, _IONBF, 0);
     uint8_t *in, *out;
     uint32_t *res, *next;
@@ -191,6 +218,11 @@ int main() {
     CK(hipMalloc(&next, 64));
     CK(hipMemset(in, 3, (size_t)kRecs * kInStride));
     CK(hipMemset(out, 0, (size_t)kRecs * kOutLen));
+    if (argc > 1) {  // "cand": the round-6 candidate rows only
+        for (int rep = 0; rep < 2; rep++) candidates(in, out, res, next);
+        printf("done\n");
+        return 0;
+    }
     for (int rep = 0; rep < 2; rep++) {
         row<0>(in, out, res, next);
         row<128>(in, out, res, next);
