@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 5 evidence, the other bench lines (each decode config with its own live PMC traffic).
-# usage: scripts/r5_lines.sh <tag> "<configs>"
+# Round evidence, the other bench lines (each decode config with its own live PMC traffic).
+# usage: scripts/round_lines.sh <tag> "<configs>"
 set -u
 TAG=$1; CFGS=$2; OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 for c in $CFGS; do

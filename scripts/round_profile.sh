@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 5 evidence, call 1: the full GPU suite and smoke, the default bench line (live PMC traffic), its rocprofv3
+# Round evidence, call 1: the full GPU suite and smoke, the default bench line (live PMC traffic), its rocprofv3
 # kernel trace, and the C2 / C4 FETCH_SIZE / WRITE_SIZE passes (scripts/traffic.py records the source tree).
-# usage: scripts/r5_profile.sh <tag>
+# usage: scripts/round_profile.sh <tag>   (round 5: r5bj, round 6: r6g ...)
 set -u
 TAG=$1; OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 step() {

@@ -2,7 +2,7 @@
 # Address-path / LDS / issue counters of k_snappy_pipe on C2: the stock build (2 waves per SIMD)
 # and the timing-only 3-wave build (librio_occ.so). One --pmc set per pass, kernel trace only, each pass under its
 # own timeout; counters the device does not list are dropped from a set before it runs.
-# usage: [CFG=c3] [PASSES="1 7"] scripts/r5_ta_pmc.sh <tag> [libs...]   (libs: base occ ...; default "base occ")
+# usage: [CFG=c3] [PASSES="1 7"] scripts/ta_pmc.sh <tag> [libs...]   (libs: base occ ...; default "base occ")
 set -u
 TAG=$1; shift
 LIBS=${*:-base occ}
