@@ -80,9 +80,6 @@ constexpr uint64_t kPlainStoreMin = 4096;
 // span less than 0xF0000000 bytes of file and arena (snappy_lane checks; a wave past that decodes its records one
 // thread each), so every real offset fits 32 bits and kOob is out of range, whatever the file's size.
 constexpr uint32_t kOob = 0xFFFFFFC0u;
-#ifndef RIO_IN_COOP
-#define RIO_IN_COOP 0
-#endif
 // Paired input loads: in the single-record-per-lane loop (kMulti = false: C2's and C4's shape) the input prefetch
 // loads two adjacent 16-byte chunks (32 bytes) on even steps and none on odd steps, so the second load of a pair
 // finds its line already requested by the first: half the L1 misses of the lane-private input stream for the same
@@ -503,7 +500,6 @@ static_assert(kFarOff + 3 + 16 + 4 <= kColRows * 4, "history image must hold the
 struct ColSlot {
     uint4 in;        // input chunk in_c (load in flight)
     uint4 in2;       // paired loads: input chunk in_c + 1
-    uint32_t pin_c;  // RIO_IN_COOP: the partner lane's pair (its in_c) that half of in / in2 belongs to
     uint4 aux;       // far-copy bytes [q - r, q - r + 16) or the next record's descriptor (in flight)
     uint32_t x0, x1, x2, x3, x4;  // literal: input rows from (src - r) & ~3 (read at parse)
     uint32_t in_c;
@@ -520,7 +516,6 @@ __device__ __forceinline__ ColSlot col_empty_slot() {
     S.aux = zero4();
     S.x0 = S.x1 = S.x2 = S.x3 = S.x4 = 0;
     S.in_c = kNoChunk;
-    S.pin_c = kNoChunk;
     S.n = 0;
     S.kind = 1;
     S.ringm = ~0u;
@@ -848,22 +843,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
           if ((j & 1u) == 0) {  // a pair (cn, cn + 1) when the ring has room for both
             const uint32_t a = s >> 4;
             const bool take = cn <= lastc && cn + 1 < a + kInCh;
-#if RIO_IN_COOP
-            // lanes 2i and 2i + 1 load each pair together: instruction A the even lane's pair (its chunk cn from the even
-            // lane, cn + 1 from the odd one), instruction B the odd lane's, so a pair's two 16-byte halves are one
-            // instruction's neighbouring lanes on one line (one L1->L2 request) instead of two instructions' requests
-            const uint32_t off = take ? base32 + 16u * cn : kOob, inc = take ? cn : kNoChunk;
-            const uint32_t poff = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)off, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-            const uint32_t pinc = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0xB1, 0xF, 0xF, false);
-            const bool odd = (lane & 1u) != 0;
-            const uint32_t po16 = poff + 16u;  // kOob + 16 stays past the range
-            const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, odd ? po16 : off, 0, 0);
-            const v4u32b v2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, odd ? off : po16, 0, 0);
-            S.pin_c = pinc;
-#else
             const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn : kOob, 0, 0);
             const v4u32b v2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc_file, take ? base32 + 16u * cn + 16u : kOob, 0, 0);
-#endif
             S.in = make_uint4(v.x, v.y, v.z, v.w);
             S.in2 = make_uint4(v2.x, v2.y, v2.z, v2.w);
             S.in_c = take ? cn : kNoChunk;
@@ -886,31 +867,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
         if constexpr (kPair) {
           if ((j & 1u) == 1) {  // the slot landing now was filled on an even step
             const bool landed = N.in_c != kNoChunk;
-#if RIO_IN_COOP
-            // each lane holds one half of its own pair and one half of its partner's: its own chunk (even lane: in,
-            // odd lane: in2) goes to its own column, the other half to the partner's column (lane ^ 1), chunk pin_c + 1
-            {
-                const bool odd = (lane & 1u) != 0, plnd = N.pin_c != kNoChunk;
-                const uint32_t own = wl | ((N.in_c & (kInCh - 1)) << 12);
-                const uint32_t oth = (wl ^ 4u) | (((N.pin_c + 1) & (kInCh - 1)) << 12);
-                const uint32_t aA = odd ? oth : own, aB = odd ? own : oth;
-                if (odd ? plnd : landed) {
-                    col_st(L, aA, N.in.x);
-                    col_st(L, aA + kColRow, N.in.y);
-                    col_st(L, aA + 2 * kColRow, N.in.z);
-                    col_st(L, aA + 3 * kColRow, N.in.w);
-                }
-                if (odd ? landed : plnd) {
-                    col_st(L, aB, N.in2.x);
-                    col_st(L, aB + kColRow, N.in2.y);
-                    col_st(L, aB + 2 * kColRow, N.in2.z);
-                    col_st(L, aB + 3 * kColRow, N.in2.w);
-                }
-            }
-            if (false) {
-#else
             if (landed) {
-#endif
                 const uint32_t a = wl | ((N.in_c & (kInCh - 1)) << 12);
                 const uint32_t a2 = wl | (((N.in_c + 1) & (kInCh - 1)) << 12);
                 col_st(L, a, N.in.x);
