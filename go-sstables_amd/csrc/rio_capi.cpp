@@ -246,6 +246,21 @@ constexpr uint64_t kLaneWalkSmallMin = 512, kLaneWalkSmallChunks = 65536;
 // at most a few such records and the placement runs a wave per chunk with most lanes idle: C4 place 0.123 -> 0.076 ms,
 // walk 0.61 -> 0.585, +1.2 %, profiles/r5/r5bl_c4_chunk_ab.txt); not when RIO_CHUNK_BYTES sets the size
 constexpr uint64_t kBigRecordChunk = 65536;
+// files of fewer than kSmallFileChunks default-size chunks walk smaller ones (the largest power of two <= len /
+// kSmallFileChunks, at least kSmallFileChunkMin): a 32 MiB file's 1024 chunks were one wave per SIMD, each walking
+// 32 KiB as a chain of dependent load rounds (round 6 on MI355X, RIO_CHUNK_BYTES sweep: 32 MiB of 1 KiB records
+// 0.117 -> 0.084 ms at 8 KiB chunks, 100 MB 0.159 -> 0.152 ms at 16 KiB; 4 KiB chunks were slower on both,
+// profiles/r6/r6j_small_file_chunks.txt)
+constexpr uint64_t kSmallFileChunks = 4096, kSmallFileChunkMin = 8192;
+static uint64_t wave_chunk_bytes(const rio_ctx* ctx, uint64_t len) {
+    const uint64_t cb = ctx->chunk_bytes;
+    if (!ctx->chunk_auto) return cb;
+    const uint64_t want = len / kSmallFileChunks;
+    if (want >= cb) return cb;
+    uint64_t p = kSmallFileChunkMin;
+    while (p * 2 <= want) p *= 2;
+    return std::min(cb, p);
+}
 
 // bytes of a file's framing arenas at chunk size cb: scratch (per array) and meta
 struct ArenaSizes {
@@ -285,7 +300,7 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
         lane = (m >= kLaneWalkMin && m <= kLaneWalkMax) ||
                (m >= ctx->lane_walk_min && m < kLaneWalkMin && chunks >= kLaneWalkSmallChunks);
     }
-    uint64_t cb = lane ? ctx->lane_chunk_bytes : ctx->chunk_bytes;
+    uint64_t cb = lane ? ctx->lane_chunk_bytes : wave_chunk_bytes(ctx, len);
     if (!lane && ctx->chunk_auto && ctx->walk_hint && *reinterpret_cast<volatile uint64_t*>(ctx->walk_hint) > kLaneWalkMax)
         cb = std::max<uint64_t>(cb, kBigRecordChunk);
     P.walk_lane = lane ? 1u : 0u;
@@ -301,7 +316,8 @@ static int ctx_frame_params(rio_ctx* ctx, const uint8_t* d_file, uint64_t len, F
     const uint64_t nc = std::max<uint64_t>(P.n_chunks, 1), nb = std::max<uint64_t>(P.n_blocks, 1);
     uint64_t scr = z.scratch, meta_need = z.meta;
     if (reserve_all) {
-        for (uint64_t c : {ctx->chunk_bytes, ctx->lane_chunk_bytes, std::max<uint64_t>(ctx->chunk_bytes, kBigRecordChunk)}) {
+        for (uint64_t c : {wave_chunk_bytes(ctx, len), ctx->chunk_bytes, ctx->lane_chunk_bytes,
+                           std::max<uint64_t>(ctx->chunk_bytes, kBigRecordChunk)}) {
             const ArenaSizes y = arena_sizes(len, c);
             scr = std::max(scr, y.scratch);
             meta_need = std::max(meta_need, y.meta);

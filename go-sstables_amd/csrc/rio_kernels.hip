@@ -30,6 +30,43 @@
 
 namespace rio {
 
+// RIO_SCAN_PROBE=1 (diagnostic builds only): 100 MHz wall-clock stamps of the framing kernels' phases in a
+// device array, printed after each decode by k_probe_dump (where a small file's framing time goes)
+#ifndef RIO_SCAN_PROBE
+#define RIO_SCAN_PROBE 0
+#endif
+#if RIO_SCAN_PROBE
+__device__ unsigned long long g_probe[32];
+#define PROBE_MIN(i) atomicMin(&g_probe[i], (unsigned long long)wall_clock64())
+#define PROBE_MAX(i) atomicMax(&g_probe[i], (unsigned long long)wall_clock64())
+#else
+#define PROBE_MIN(i) ((void)0)
+#define PROBE_MAX(i) ((void)0)
+#endif
+
+// Code prefetch (RIO_CODE_PF, default on): after a MALL flush a launch's instruction fetches come from HBM one
+// 64-byte line at a time, a dependent miss chain through the kernel's straight-line code (round 6 probe: the
+// scan's cold chain 36 -> 31 us with the next 4 KiB of its code read as data at entry, profiles/r6/
+// r6k_small_file_framing.txt). Lane t < lines of the calling wave loads the dword at pc + 64 t into L2 (one line
+// each; the SQC's misses then hit L2); code_pf_done consumes the value where the wave waits anyway. `lines` stays
+// within the kernel's own code: tests/test_build.py checks every prefetching kernel against the code object.
+#ifndef RIO_CODE_PF
+#define RIO_CODE_PF 1
+#endif
+__device__ __forceinline__ uint32_t code_pf(uint32_t lines) {
+    uint32_t v = 0;
+    if (RIO_CODE_PF && threadIdx.x < lines)
+        v = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(__builtin_amdgcn_s_getpc() +
+                                                                                  64u * threadIdx.x);
+    return v;
+}
+__device__ __forceinline__ void code_pf_done(uint32_t v) {
+    if (RIO_CODE_PF) asm volatile("" ::"v"(v));
+}
+// lines per kernel (tests/test_build.py: within each kernel's own code); the wide grids prefetch from their first
+// 16 blocks only (two per XCD: each XCD's L2 then holds the code)
+constexpr uint32_t kPfScan = 64, kPfPlace = 48, kPfCopy = 64, kPfFinish = 64, kPfWalk = 64, kPfBlocks = 16;
+
 // ------------------------------------------------------------------------------------------
 // Byte-level primitives
 // ------------------------------------------------------------------------------------------
@@ -736,6 +773,8 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
 #endif
     __shared__ WalkLds W[kWalkWaves];
     __shared__ uint32_t crct[1024];
+    const uint32_t pf = code_pf(blockIdx.x < kPfBlocks ? kPfWalk : 0);
+    if (threadIdx.x == 0) PROBE_MIN(0);
     if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
     crc32c_tab_init(crct);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -883,7 +922,9 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         else if (entry != kNone)
             s.exit = p;  // the chain left the chunk (or ended at the file end) cleanly
         P.chunks[c] = s;
+        PROBE_MAX(1);
     }
+    code_pf_done(pf);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1083,12 +1124,25 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
     __shared__ uint32_t last;
     const int t = threadIdx.x;
     const uint64_t c = (uint64_t)blockIdx.x * kScanBlock + t;
+    const uint32_t pf = code_pf(kPfScan);
+#if RIO_SCAN_PROBE
+    uint64_t pt[7];
+    pt[0] = wall_clock64();
+    if (t == 0) {
+        PROBE_MIN(2);
+        PROBE_MAX(3);
+    }
+#endif
     if (P.state->hdr_status != RIO_OK) return;  // block-uniform
     if (P.redo && (!P.state->gz_redo || P.state->compression != P.redo)) return;  // another codec's redo round
     RunSum v = c < P.n_chunks ? chunk_run(P, c) : run_identity();
     int cur = 0;
     buf[cur][t] = v;
     __syncthreads();
+#if RIO_SCAN_PROBE
+    pt[1] = wall_clock64();
+#endif
+#pragma unroll 1
     for (int d = 1; d < kScanBlock; d <<= 1) {
         RunSum x = buf[cur][t];
         if (t >= d) x = combine(buf[cur][t - d], x);
@@ -1096,17 +1150,35 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_blocks(FrameParams P) {
         cur ^= 1;
         __syncthreads();
     }
+#if RIO_SCAN_PROBE
+    pt[2] = wall_clock64();
+#endif
     if (c < P.n_chunks) P.chunk_excl[c] = t > 0 ? buf[cur][t - 1] : run_identity();
     if (t == kScanBlock - 1) P.block_runs[blockIdx.x] = buf[cur][t];
     // release this block's run, take a ticket; the last arriver acquires every block's run
     __syncthreads();
+#if RIO_SCAN_PROBE
+    pt[3] = wall_clock64();
+#endif
     if (t == 0) {
         __threadfence();
+#if RIO_SCAN_PROBE
+        pt[4] = wall_clock64();
+#endif
         last = atomicAdd(&P.state->scan_ticket, 1u) == gridDim.x - 1;
+#if RIO_SCAN_PROBE
+        pt[5] = wall_clock64();
+#endif
     }
+    code_pf_done(pf);
     __syncthreads();
     if (!last) return;
     __threadfence();
+#if RIO_SCAN_PROBE
+    pt[6] = wall_clock64();
+    if (t == 0)
+        for (int k = 0; k < 7; k++) g_probe[4 + k] = pt[k];
+#endif
     scan_top(P, buf);
 }
 
@@ -1166,6 +1238,34 @@ __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
         }
         return;  // (len == 8: the first ReadNext hits EOF)
     }
+    if (P.n_blocks <= 64) {
+        // one wave, no block barriers: entries 0..63 of the 256-wide Hillis-Steele below are exactly this 64-lane
+        // one (its steps d >= 64 leave them alone), and its total is entry 63 (combine returns the other operand
+        // of an identity unchanged): the same association, so the same RunSums (files up to 16384 chunks)
+        if (t >= 64) return;
+        buf[0][t] = t < P.n_blocks ? P.block_runs[t] : run_identity();
+        wave_sync_lds();
+        int cur = 0;
+#pragma unroll 1
+        for (int d = 1; d < 64; d <<= 1) {
+            RunSum x = buf[cur][t];
+            if (t >= d) x = combine(buf[cur][t - d], x);
+            buf[cur ^ 1][t] = x;
+            cur ^= 1;
+            wave_sync_lds();
+        }
+        if ((uint64_t)t < P.n_blocks) P.block_excl[t] = combine(run_identity(), t > 0 ? buf[cur][t - 1] : run_identity());
+        if (t != 0) return;
+        const RunSum total = combine(run_identity(), buf[cur][63]);
+#if RIO_SCAN_PROBE
+        g_probe[19] = wall_clock64();
+#endif
+        scan_finish(P, total);
+#if RIO_SCAN_PROBE
+        g_probe[20] = wall_clock64();
+#endif
+        return;
+    }
     if (t == 0) carry_s = run_identity();
     __syncthreads();
     for (uint64_t base = 0; base < P.n_blocks; base += kScanBlock) {
@@ -1174,6 +1274,10 @@ __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
         int cur = 0;
         buf[cur][t] = v;
         __syncthreads();
+#if RIO_SCAN_PROBE
+        if (t == 0 && base == 0) g_probe[18] = wall_clock64();
+#endif
+#pragma unroll 1
         for (int d = 1; d < kScanBlock; d <<= 1) {
             RunSum x = buf[cur][t];
             if (t >= d) x = combine(buf[cur][t - d], x);
@@ -1190,7 +1294,13 @@ __device__ void scan_top(const FrameParams& P, RunSum (*buf)[kScanBlock]) {
     }
     const RunSum total = carry_s;
     if (t != 0) return;
+#if RIO_SCAN_PROBE
+    g_probe[19] = wall_clock64();
+#endif
     scan_finish(P, total);
+#if RIO_SCAN_PROBE
+    g_probe[20] = wall_clock64();
+#endif
 }
 
 // The file's state from the composed run of all chunks (one thread): the terminal status, the counts, or the
@@ -1345,6 +1455,11 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const uint32_t lane = threadIdx.x & (G - 1);
     const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
     ScanState* st = P.state;
+    const uint32_t pf = code_pf(blockIdx.x < kPfBlocks ? kPfPlace : 0);
+    if (threadIdx.x == 0) {
+        PROBE_MIN(11);
+        PROBE_MAX(12);
+    }
     if (st->hdr_status != RIO_OK) return;
     if (P.redo && (!st->gz_redo || st->compression != P.redo)) return;  // another codec's redo round
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1390,6 +1505,8 @@ __global__ void __launch_bounds__(256) k_place(FrameParams P) {
     const bool pay_all = st->compression == RIO_COMP_GZIP || st->compression == RIO_COMP_LZW;
     const PlaceFlags f = place_chunk<G>(P, c, pl.base_idx, pl.base_bytes, pl.owned, snappy, pay_all, lane);
     if (lane == 0) merge_place_flags(P, f);
+    if (lane == 0) PROBE_MAX(13);
+    code_pf_done(pf);
 }
 
 __global__ void __launch_bounds__(256) k_zero(FrameParams P) {
@@ -1479,6 +1596,8 @@ __device__ __forceinline__ void copy_groups(const FrameParams& P, uint64_t n, bo
 
 __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
     const ScanState* st = P.state;
+    const uint32_t pf = code_pf(blockIdx.x < kPfBlocks ? kPfCopy : 0);
+    if (threadIdx.x == 0 && (blockIdx.x & 63) == 0) PROBE_MIN(14);
     if (st->hdr_status != RIO_OK || st->capacity_fail) return;
     const bool none = st->compression == RIO_COMP_NONE;
     if (!none && !(st->compression == RIO_COMP_SNAPPY && !st->any_mixed)) return;
@@ -1489,6 +1608,8 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
         copy_groups<4>(P, n, none);
     else
         copy_groups<16>(P, n, none);
+    if (threadIdx.x == 0 && (blockIdx.x & 63) == 63) PROBE_MAX(15);
+    code_pf_done(pf);
 #else
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
@@ -1585,6 +1706,8 @@ __global__ void k_finalize(FrameParams P) {
 __device__ __forceinline__ void finish_file(const FrameParams& P) {
     __shared__ uint32_t last;
     ScanState* st = P.state;
+    const uint32_t pf = code_pf(kPfFinish);
+    if (threadIdx.x == 0) PROBE_MIN(16);
     if (st->hdr_status == RIO_OK && !st->capacity_fail && st->compression == RIO_COMP_SNAPPY && st->n_fail_lanes) {
         auto verify = [&](uint64_t i) {
             if (P.flags[i] & (RIO_FLAG_NIL | RIO_FLAG_CORRUPT | RIO_FLAG_EOF)) return;
@@ -1612,8 +1735,24 @@ __device__ __forceinline__ void finish_file(const FrameParams& P) {
     if (last && threadIdx.x == 0) {
         __threadfence();
         finalize_info(P);
+        PROBE_MAX(17);
     }
+    code_pf_done(pf);
 }
+
+#if RIO_SCAN_PROBE
+// the stamps of the decode that just ran, in us from the walk's first wave; then reset for the next one
+__global__ void k_probe_dump() {
+    const unsigned long long t0 = g_probe[0];
+    auto us = [&](int i) { return g_probe[i] >= t0 && g_probe[i] != ~0ull ? (double)(g_probe[i] - t0) * 0.01 : -1.0; };
+    printf("PROBE walk_end %.2f scan_first %.2f scan_lastin %.2f | last blk in %.2f ld %.2f hs %.2f st %.2f fence %.2f "
+           "atomic %.2f acq %.2f top_ld %.2f top %.2f fin %.2f | place_first %.2f place_lastin %.2f place_end %.2f | "
+           "copy_first %.2f copy_end %.2f | finish_first %.2f finish_end %.2f\n",
+           us(1), us(2), us(3), us(4), us(5), us(6), us(7), us(8), us(9), us(10), us(18), us(19), us(20), us(11),
+           us(12), us(13), us(14), us(15), us(16), us(17));
+    for (int i = 0; i < 32; i++) g_probe[i] = (i == 0 || i == 2 || i == 11 || i == 14 || i == 16) ? ~0ull : 0ull;
+}
+#endif
 __global__ void __launch_bounds__(256) k_finish(FrameParams P) { finish_file(P); }
 // the files of a batch in one launch: blockIdx.y is the file (each file's 64 blocks take its own ticket)
 __global__ void __launch_bounds__(256) k_finish_batch(FrameBatch B) { finish_file(B.f[blockIdx.y]); }
@@ -2283,6 +2422,9 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev, h
     launch_place(P, s, nullptr, ev ? ev[3] : nullptr);
     launch_decoders(P, s, true);
     launch_ev(k_finish, dim3(64), dim3(256), s, ev ? ev[4] : nullptr, done, P);
+#if RIO_SCAN_PROBE
+    hipLaunchKernelGGL(k_probe_dump, dim3(1), dim3(1), 0, s);
+#endif
     return hipGetLastError();
 }
 

@@ -95,6 +95,60 @@ def test_chunk_size_independent(chunk, monkeypatch):
         L.lib().rio_ctx_destroy(h)
 
 
+def _big_uncompressed(seed, hi, n=3000):
+    """Uncompressed records averaging >= 256 bytes: sizes around the copy's 16-byte pieces and its 1 KiB rounds
+    (k_copy_records, 16-lane groups), empty and nil records."""
+    import random
+
+    rng = random.Random(seed)
+    recs = []
+    for _ in range(n):
+        if rng.random() < 0.03:
+            recs.append(None)
+            continue
+        ln = rng.choice([0, 1, 15, 16, 17, 255, 256, 1023, 1024, 1025, 2048, rng.randint(0, hi)])
+        recs.append(rng.randbytes(ln))
+    return corpus.encode_file(recs, 0)
+
+
+@pytest.mark.parametrize("seed,hi", [(21, 600), (22, 3000), (23, 20000)])
+def test_uncompressed_large_records_whole_file(seed, hi):
+    """Whole files, a truncated end and a zero tail of large uncompressed records (the 16-lane copy groups): every
+    decode is the oracle's."""
+    img = _big_uncompressed(seed, hi)
+    for name, im in ((f"s{seed}", img), (f"s{seed}_trunc", img[: len(img) * 2 // 3]),
+                     (f"s{seed}_zero_tail", img + bytes(5000))):
+        o = orc.file_reader_decode_arrays(im)
+        assert o["total_out_bytes"] >= 256 * o["n_records"], name
+        assert_same_as_oracle(gpu_decode_arrays(im), o, name)
+
+
+@pytest.mark.parametrize("chunk", [64, 1024, 16384])
+def test_uncompressed_large_records_any_chunk_size(chunk, monkeypatch):
+    """The same files when records span many chunks (64-byte chunks: most own no record) or share one."""
+    import ctypes
+
+    from recordio import _lib as L
+    from recordio.device import DeviceDecoder, to_device_file
+
+    monkeypatch.setenv("RIO_CHUNK_BYTES", str(chunk))
+    h = ctypes.c_void_p()
+    assert L.lib().rio_ctx_create(0, ctypes.byref(h)) == 0
+    try:
+        dec = DeviceDecoder.__new__(DeviceDecoder)
+        dec.device, dec.ctx = 0, h.value
+        img = _big_uncompressed(24, 5000, n=1500)
+        o = orc.file_reader_decode_arrays(img)
+        d_file, n = to_device_file(img)
+        b, info = dec.decode(d_file, n)
+        k = info["n_records"]
+        g = dict(info, out=b.out[: info["total_out_bytes"]].cpu().numpy(), out_off=b.out_off[: k + 1].cpu().numpy(),
+                 rec_off=b.rec_off[:k].cpu().numpy(), flags=b.flags[:k].cpu().numpy())
+        assert_same_as_oracle(g, o, f"big_uncompressed@{chunk}")
+    finally:
+        L.lib().rio_ctx_destroy(h)
+
+
 def _handle_read_next_at(r, off):
     """C-ABI status and details of the reader handle's ReadNextAt (rio_reader_read_next_at)."""
     import ctypes
