@@ -80,6 +80,14 @@ constexpr uint64_t kPlainStoreMin = 4096;
 // span less than 0xF0000000 bytes of file and arena (snappy_lane checks; a wave past that decodes its records one
 // thread each), so every real offset fits 32 bits and kOob is out of range, whatever the file's size.
 constexpr uint32_t kOob = 0xFFFFFFC0u;
+// Far windows inside the copy's line (RIO_FAR_LINE, files of plain-store records: C4): a far piece's 16-byte window
+// [q - r, q - r + 16) that straddles a 128-byte line costs two L2 -> fabric requests though the piece's own bytes
+// [q, q + n) may sit in one line; then the window moves: back to the line's last 16 bytes (kind 4, shifted down at
+// the emit) or, when the bytes lie in the next line, to q itself (kind 3, shifted up). 5.6 % of C4's far requests
+// (host count over its streams, profiles/r6).
+#ifndef RIO_FAR_LINE
+#define RIO_FAR_LINE 1
+#endif
 // Paired input loads: in the single-record-per-lane loop (kMulti = false: C2's and C4's shape) the input prefetch
 // loads two adjacent 16-byte chunks (32 bytes) on even steps and none on odd steps, so the second load of a pair
 // finds its line already requested by the first: half the L1 misses of the lane-private input stream for the same
@@ -633,6 +641,8 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
     const __amdgpu_buffer_rsrc_t rsrc_file = uniform_rsrc(P.file + w_in, P.len + RIO_DEVICE_PAD - umin(w_in, P.len));
     const __amdgpu_buffer_rsrc_t rsrc_out = uniform_rsrc(P.out + w_out, P.state->total_bytes + 16 - umin(w_out, P.state->total_bytes));
     const uint32_t base32 = (uint32_t)(base - w_in), o32 = (uint32_t)(o0 - w_out);
+    // the arena descriptor base's position in its 128-byte line (wave-uniform)
+    const uint32_t line0 = (uint32_t)reinterpret_cast<uintptr_t>(P.out + w_out) & 127u;
     uint32_t obase[4];  // the flush owners' arena offsets
 #pragma unroll
     for (uint32_t jj = 0; jj < 4; jj++)
@@ -678,13 +688,28 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             D3 = bsel(fm, S.aux.w, D3);
             // kind 3 (rare: a far source in the first bytes of the arena, lane of the file's first
             // record): aux holds bytes [q, q + 16), shifted up by r here
-            if (kLow && __builtin_expect(__any(S.kind == 3), 0)) {
+            constexpr bool kLine = kPlain && RIO_FAR_LINE && !kMulti;
+            if ((kLow || kLine) && __builtin_expect(__any(S.kind == 3), 0)) {
                 if (S.kind == 3) {
                     const uint32_t u = 4u - (d & 3u);
                     D0 = __builtin_amdgcn_alignbyte(S.aux.x, 0u, u);
                     D1 = __builtin_amdgcn_alignbyte(S.aux.y, S.aux.x, u);
                     D2 = __builtin_amdgcn_alignbyte(S.aux.z, S.aux.y, u);
                     D3 = __builtin_amdgcn_alignbyte(S.aux.w, S.aux.z, u);
+                }
+            }
+            // kind 4 (kLine): aux holds bytes [q - r - S.q, + 16), S.q in [1, 15]: shifted down by S.q bytes (dword
+            // rotate by S.q >> 2, then the byte shift; the bytes pulled in past aux's end are never the piece's)
+            if (kLine && __any(S.kind == 4)) {
+                if (S.kind == 4) {
+                    const bool h2 = (S.q & 8u) != 0, h1 = (S.q & 4u) != 0;
+                    const uint32_t T0 = h2 ? S.aux.z : S.aux.x, T1 = h2 ? S.aux.w : S.aux.y;
+                    const uint32_t T2 = h2 ? 0u : S.aux.z, T3 = h2 ? 0u : S.aux.w;
+                    const uint32_t R0 = h1 ? T1 : T0, R1 = h1 ? T2 : T1, R2 = h1 ? T3 : T2, R3 = h1 ? 0u : T3;
+                    D0 = __builtin_amdgcn_alignbyte(R1, R0, S.q);
+                    D1 = __builtin_amdgcn_alignbyte(R2, R1, S.q);
+                    D2 = __builtin_amdgcn_alignbyte(R3, R2, S.q);
+                    D3 = __builtin_amdgcn_alignbyte(0u, R3, S.q);
                 }
             }
             // bytes below d keep the row's content (v_bfi_b32); the shift uses the low 5 bits: 8 (d & 3)
@@ -826,7 +851,18 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             const uint32_t r = (pd - S.n) & 3u;  // the piece's destination alignment
             if constexpr (!kMulti && !kLow) {
                 // no descriptor to fetch and no source below the arena: the arena descriptor alone
-                const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, S.kind == 2 ? o32 + qsrc - r : kOob, 0, 0);
+                uint32_t fo = o32 + qsrc - r;
+                if constexpr (kPlain && RIO_FAR_LINE) {
+                    // the window's place in its line; a straddling window moves inside the piece's own line
+                    const uint32_t a = (line0 + fo) & 127u, back = a - 112u;
+                    const bool strad = S.kind == 2 && a > 112u;
+                    const bool inB = strad && a + r + S.n <= 128u && fo >= back;  // bytes in the window's first line
+                    const bool inA = strad && a + r >= 128u;                     // bytes in the next line: from q
+                    fo = inB ? fo - back : (inA ? fo + r : fo);
+                    S.kind = inB ? 4u : (inA ? 3u : S.kind);
+                    S.q = inB ? back : S.q;
+                }
+                const v4u32b v = __builtin_amdgcn_raw_buffer_load_b128(rsrc_out, S.kind >= 2 ? fo : kOob, 0, 0);
                 S.aux = make_uint4(v.x, v.y, v.z, v.w);
             } else {
                 // 16 bytes from q - r would start below the arena: load from q, shift at the emit (kind 3)
