@@ -184,6 +184,7 @@ struct rio_ctx {
     uint32_t walk_mode = 2;
     uint64_t lane_chunk_bytes = 16384;
     uint64_t lane_walk_min = 512;  // kLaneWalkSmallMin (RIO_LANE_WALK_MIN)
+    uint64_t walk_slots = 5120;    // resident k_walk waves: CUs x 4 SIMDs x kWalkWavesPerSimd (wave_chunk_bytes)
     uint64_t* walk_hint = nullptr;
     uint64_t coop_min = ~0ull >> 8;
     hipEvent_t* next_events() {
@@ -246,20 +247,19 @@ constexpr uint64_t kLaneWalkSmallMin = 512, kLaneWalkSmallChunks = 65536;
 // at most a few such records and the placement runs a wave per chunk with most lanes idle: C4 place 0.123 -> 0.076 ms,
 // walk 0.61 -> 0.585, +1.2 %, profiles/r5/r5bl_c4_chunk_ab.txt); not when RIO_CHUNK_BYTES sets the size
 constexpr uint64_t kBigRecordChunk = 65536;
-// files of fewer than kSmallFileChunks default-size chunks walk smaller ones (the largest power of two <= len /
-// kSmallFileChunks, at least kSmallFileChunkMin): a 32 MiB file's 1024 chunks were one wave per SIMD, each walking
-// 32 KiB as a chain of dependent load rounds (round 6 on MI355X, RIO_CHUNK_BYTES sweep: 32 MiB of 1 KiB records
-// 0.117 -> 0.084 ms at 8 KiB chunks, 100 MB 0.159 -> 0.152 ms at 16 KiB; 4 KiB chunks were slower on both,
-// profiles/r6/r6j_small_file_chunks.txt)
-constexpr uint64_t kSmallFileChunks = 4096, kSmallFileChunkMin = 8192;
+// Small files walk smaller chunks: the smallest multiple of 4 KiB (the walk's fill round) whose chunk count fits one round
+// of resident walk waves (CUs x 4 SIMDs x RIO_WALK_OCC = 5 waves: 5 120 on MI355X), at least kSmallFileChunkMin; files
+// that need more than one round at the default size keep it. A 32 MiB file's 1 024 default chunks were one wave per SIMD,
+// each walking 32 KiB as a chain of dependent fill rounds; a chunk count just past one round runs a second round for a
+// few waves (round 6 on MI355X: 32 MiB of 1 KiB records 0.117 -> 0.084 ms at 8 KiB chunks; 100 MB 0.171 -> 0.15 ms at
+// 20 KiB (5 059 waves), against 16 KiB (6 100: two rounds) and 19 KiB (5 325); profiles/r6/r6j_small_file_chunks.txt)
+constexpr uint64_t kSmallFileChunkMin = 8192, kWalkWavesPerSimd = 5;
 static uint64_t wave_chunk_bytes(const rio_ctx* ctx, uint64_t len) {
     const uint64_t cb = ctx->chunk_bytes;
     if (!ctx->chunk_auto) return cb;
-    const uint64_t want = len / kSmallFileChunks;
-    if (want >= cb) return cb;
-    uint64_t p = kSmallFileChunkMin;
-    while (p * 2 <= want) p *= 2;
-    return std::min(cb, p);
+    const uint64_t slots = ctx->walk_slots;
+    const uint64_t want = ((len + slots - 1) / slots + 4095) & ~4095ull;
+    return std::min(cb, std::max(want, kSmallFileChunkMin));
 }
 
 // bytes of a file's framing arenas at chunk size cb: scratch (per array) and meta
@@ -373,6 +373,9 @@ extern "C" int rio_ctx_create(int device, rio_ctx** out) {
     c->walk_mode = (uint32_t)std::min<uint64_t>(env_u64("RIO_WALK_LANE", 2), 2);
     c->lane_chunk_bytes = env_u64("RIO_LANE_CHUNK_BYTES", 16384);
     c->lane_walk_min = env_u64("RIO_LANE_WALK_MIN", kLaneWalkSmallMin);
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->walk_slots = (uint64_t)cus * 4 * kWalkWavesPerSimd;
     if (c->lane_chunk_bytes < 64 || c->lane_chunk_bytes > (1ull << 30) || (c->lane_chunk_bytes & 15))
         c->lane_chunk_bytes = 16384;
     if (hipHostMalloc(reinterpret_cast<void**>(&c->walk_hint), sizeof(uint64_t), hipHostMallocPortable) != hipSuccess) {

@@ -101,10 +101,10 @@ def test_older_layouts_full_size(version, monkeypatch):
 def test_auto_walk_follows_the_previous_decode(monkeypatch):
     """RIO_WALK_LANE unset (auto): a context's decode takes the lane walk (16 KiB chunks, info.n_chunks shows
     which) when its previous decode had records of 768 B .. 8 KiB on average and the file fills 32768 lane
-    chunks, else the wave walk (32 KiB chunks; a file of fewer than 4096 of them walks the largest power of two
-    <= len / 4096, at least 8 KiB: wave_cb). DeviceDecoder.decode runs a capacity probe first, which records the
-    file's mean for the real decode: a fresh context's first file is framed by the wave walk in the probe only. Every decode is the
-    oracle's."""
+    chunks, else the wave walk (32 KiB chunks; a smaller file walks the smallest 4 KiB multiple whose chunks fit one
+    round of resident walk waves, at least 8 KiB: wave_cb). DeviceDecoder.decode runs a capacity probe first, which
+    records the file's mean for the real decode: a fresh context's first file is framed by the wave walk in the
+    probe only. Every decode is the oracle's."""
     from recordio.device import DeviceDecoder
 
     monkeypatch.delenv("RIO_WALK_LANE", raising=False)
@@ -114,13 +114,13 @@ def test_auto_walk_follows_the_previous_decode(monkeypatch):
     small = corpus.generate(200_000, 64, 2, kind=1, seed=8)
     chunks = lambda img, cb: (len(img) - 8 + cb - 1) // cb  # noqa: E731
 
-    def wave_cb(img):  # rio_capi.cpp wave_chunk_bytes
-        want, p = len(img) // 4096, 8192
-        if want >= 32768:
-            return 32768
-        while p * 2 <= want:
-            p *= 2
-        return min(p, 32768)
+    import torch
+
+    slots = torch.cuda.get_device_properties(0).multi_processor_count * 4 * 5
+
+    def wave_cb(img):  # rio_capi.cpp wave_chunk_bytes: one round of resident walk waves, 4 KiB multiples
+        want = ((len(img) + slots - 1) // slots + 4095) // 4096 * 4096
+        return min(32768, max(want, 8192))
 
     got = []
     short = corpus.generate(40_000, 1024, 2, kind=0, seed=9)  # large records, too few lane chunks
