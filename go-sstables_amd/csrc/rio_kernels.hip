@@ -49,7 +49,7 @@ __device__ unsigned long long g_probe[32];
 // scan's cold chain 36 -> 31 us with the next 4 KiB of its code read as data at entry, profiles/r6/
 // r6k_small_file_framing.txt). Lane t < lines of the calling wave loads the dword at pc + 64 t into L2 (one line
 // each; the SQC's misses then hit L2); code_pf_done consumes the value where the wave waits anyway. `lines` stays
-// within the kernel's own code: tests/test_build.py checks every prefetching kernel against the code object.
+// within the kernel's own code: tests/test_kernel_lint.py checks every prefetching kernel against the code object.
 #ifndef RIO_CODE_PF
 #define RIO_CODE_PF 1
 #endif
@@ -63,7 +63,7 @@ __device__ __forceinline__ uint32_t code_pf(uint32_t lines) {
 __device__ __forceinline__ void code_pf_done(uint32_t v) {
     if (RIO_CODE_PF) asm volatile("" ::"v"(v));
 }
-// lines per kernel (tests/test_build.py: within each kernel's own code); the wide grids prefetch from their first
+// lines per kernel (tests/test_kernel_lint.py: within each kernel's own code); the wide grids prefetch from their first
 // 16 blocks only (two per XCD: each XCD's L2 then holds the code)
 constexpr uint32_t kPfScan = 64, kPfPlace = 48, kPfCopy = 64, kPfFinish = 64, kPfWalk = 64, kPfBlocks = 16;
 
