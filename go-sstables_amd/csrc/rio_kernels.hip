@@ -44,24 +44,21 @@ __device__ unsigned long long g_probe[32];
 #define PROBE_MAX(i) ((void)0)
 #endif
 
-// Code prefetch (RIO_CODE_PF, default on): after a MALL flush a launch's instruction fetches come from HBM one
+// Code prefetch: after a MALL flush a launch's instruction fetches come from HBM one
 // 64-byte line at a time, a dependent miss chain through the kernel's straight-line code (round 6 probe: the
 // scan's cold chain 36 -> 31 us with the next 4 KiB of its code read as data at entry, profiles/r6/
 // r6k_small_file_framing.txt). Lane t < lines of the calling wave loads the dword at pc + 64 t into L2 (one line
 // each; the SQC's misses then hit L2); code_pf_done consumes the value where the wave waits anyway. `lines` stays
 // within the kernel's own code: tests/test_kernel_lint.py checks every prefetching kernel against the code object.
-#ifndef RIO_CODE_PF
-#define RIO_CODE_PF 1
-#endif
 __device__ __forceinline__ uint32_t code_pf(uint32_t lines) {
     uint32_t v = 0;
-    if (RIO_CODE_PF && threadIdx.x < lines)
+    if (threadIdx.x < lines)
         v = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(__builtin_amdgcn_s_getpc() +
                                                                                   64u * threadIdx.x);
     return v;
 }
 __device__ __forceinline__ void code_pf_done(uint32_t v) {
-    if (RIO_CODE_PF) asm volatile("" ::"v"(v));
+    asm volatile("" ::"v"(v));
 }
 // lines per kernel (tests/test_kernel_lint.py: within each kernel's own code); the wide grids prefetch from their first
 // 16 blocks only (two per XCD: each XCD's L2 then holds the code)

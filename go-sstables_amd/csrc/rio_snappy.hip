@@ -80,14 +80,11 @@ constexpr uint64_t kPlainStoreMin = 4096;
 // span less than 0xF0000000 bytes of file and arena (snappy_lane checks; a wave past that decodes its records one
 // thread each), so every real offset fits 32 bits and kOob is out of range, whatever the file's size.
 constexpr uint32_t kOob = 0xFFFFFFC0u;
-// Far windows inside the copy's line (RIO_FAR_LINE, files of plain-store records: C4): a far piece's 16-byte window
+// Far windows inside the copy's line (files of plain-store records: C4; kLine in snappy_lane): a far piece's 16-byte window
 // [q - r, q - r + 16) that straddles a 128-byte line costs two L2 -> fabric requests though the piece's own bytes
 // [q, q + n) may sit in one line; then the window moves: back to the line's last 16 bytes (kind 4, shifted down at
 // the emit) or, when the bytes lie in the next line, to q itself (kind 3, shifted up). 5.6 % of C4's far requests
 // (host count over its streams, profiles/r6).
-#ifndef RIO_FAR_LINE
-#define RIO_FAR_LINE 1
-#endif
 // Paired input loads: in the single-record-per-lane loop (kMulti = false: C2's and C4's shape) the input prefetch
 // loads two adjacent 16-byte chunks (32 bytes) on even steps and none on odd steps, so the second load of a pair
 // finds its line already requested by the first: half the L1 misses of the lane-private input stream for the same
@@ -688,7 +685,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             D3 = bsel(fm, S.aux.w, D3);
             // kind 3 (rare: a far source in the first bytes of the arena, lane of the file's first
             // record): aux holds bytes [q, q + 16), shifted up by r here
-            constexpr bool kLine = kPlain && RIO_FAR_LINE && !kMulti;
+            constexpr bool kLine = kPlain && !kMulti;
             if ((kLow || kLine) && __builtin_expect(__any(S.kind == 3), 0)) {
                 if (S.kind == 3) {
                     const uint32_t u = 4u - (d & 3u);
@@ -852,7 +849,7 @@ __device__ __forceinline__ bool snappy_lane(const FrameParams& P, uint64_t r0, u
             if constexpr (!kMulti && !kLow) {
                 // no descriptor to fetch and no source below the arena: the arena descriptor alone
                 uint32_t fo = o32 + qsrc - r;
-                if constexpr (kPlain && RIO_FAR_LINE) {
+                if constexpr (kPlain) {
                     // the window's place in its line; a straddling window moves inside the piece's own line
                     const uint32_t a = (line0 + fo) & 127u, back = a - 112u;
                     const bool strad = S.kind == 2 && a > 112u;

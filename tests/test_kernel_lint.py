@@ -38,8 +38,6 @@ def test_code_prefetch_stays_inside_each_kernel(tmp_path):
     if not os.path.exists(obj) or not all(os.path.exists(t) for t in tools):
         pytest.skip("no built rio_kernels.o or no ROCm LLVM tools")
     src = open(os.path.join(CSRC, "rio_kernels.hip")).read()
-    if re.search(r"#define RIO_CODE_PF 0", src):
-        pytest.skip("code prefetch off")
     lines = {k: int(v) for k, v in re.findall(r"kPf(\w+) = (\d+)", src)}
     co, fb = str(tmp_path / "k.elf"), str(tmp_path / "fatbin")
     # the host object carries the device code as an offload bundle in .hip_fatbin
