@@ -744,12 +744,9 @@ __device__ __forceinline__ uint32_t magic_mask(const uint32_t (&d)[5], uint64_t 
 // spilled to scratch beat 5 (walk 0.210 -> 0.185 ms on C2). With the packed DPP fill scans and the
 // 32-bit LEB128 packing the spills landed in the fill loop: 6 waves 0.413 ms on C3, 5 waves (96
 // VGPRs, no scratch) 0.300 ms, against 0.363 before (C2 0.183 -> 0.164 ms)
-// RIO_COPY2 (default 2): k_copy_records with the next record's sizes prefetched and 1 KiB in flight per
-// 16-lane group, non-temporal loads and stores (C2-ref-random copy 0.423 -> 0.370 ms, 5.8 TB/s; C1 +7 %,
-// C5 +4 %: profiles/r5/r5aa_copy_ab.txt); 1: the same with plain loads and stores; 0: the round-4 loop
-#ifndef RIO_COPY2
-#define RIO_COPY2 2
-#endif
+// k_copy_records (round 5): the next record's sizes prefetched and 1 KiB in flight per 16-lane group, non-temporal loads
+// and stores (C2-ref-random copy 0.423 -> 0.370 ms, 5.8 TB/s; C1 +7 %, C5 +4 % against plain ones and the round-4 loop:
+// profiles/r5/r5aa_copy_ab.txt)
 // k_copy_records' grid (4096 x 256: C1's 100 k records over twice the groups, copy 0.067 -> 0.057 ms; C2-ref-random
 // -2 %; 1024: C1 +45 %; two records in flight per group: +10 %, r5ab)
 #ifndef RIO_COPY_GRID
@@ -1536,7 +1533,6 @@ __device__ __forceinline__ void copy_fwd(uint8_t* dst, uint64_t d, const uint8_t
 // the reference benchmark's random records; k_snappy_pipe exits at once for those): 16-lane groups,
 // one record per group; each lane moves 16 bytes per step (unaligned load and store; the record's
 // last piece is stored exactly).
-#if RIO_COPY2
 // kG lanes per record (16, or 4 for files of small records: their 16-lane groups left 12 lanes idle and took a
 // dependent round trip per 50-byte record, C5's index copy 0.12 ms for 61 MB); each group's next record's sizes
 // are loaded while the current one is copied, and a record moves in rounds of 64 kG bytes (four 16-byte loads per
@@ -1569,16 +1565,13 @@ __device__ __forceinline__ void copy_groups(const FrameParams& P, uint64_t n, bo
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
                 const uint64_t k = k0 + 16 * kG * j + 16 * lane;
-                v[j] = k < len ? (RIO_COPY2 == 2 ? ldu16_nt(src + k) : ldu16(src + k)) : zero4();
+                v[j] = k < len ? ldu16_nt(src + k) : zero4();
             }
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
                 const uint64_t k = k0 + 16 * kG * j + 16 * lane;
                 if (k + 16 <= len) {
-                    if (RIO_COPY2 == 2)
-                        stu16_nt(dst + k, v[j]);
-                    else
-                        stu16(dst + k, v[j]);
+                    stu16_nt(dst + k, v[j]);
                 } else if (k < len) {
                     st_partial(dst + k, v[j], (uint32_t)(len - k));
                 }
@@ -1589,7 +1582,6 @@ __device__ __forceinline__ void copy_groups(const FrameParams& P, uint64_t n, bo
         src = nsrc;
     }
 }
-#endif
 
 __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
     const ScanState* st = P.state;
@@ -1599,7 +1591,6 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
     const bool none = st->compression == RIO_COMP_NONE;
     if (!none && !(st->compression == RIO_COMP_SNAPPY && !st->any_mixed)) return;
     const uint64_t n = st->n_records;
-#if RIO_COPY2
     // wave-uniform: the file's mean record size picks the group width
     if (st->total_bytes < kCopySmall * n)
         copy_groups<4>(P, n, none);
@@ -1607,27 +1598,6 @@ __global__ void __launch_bounds__(256) k_copy_records(FrameParams P) {
         copy_groups<16>(P, n, none);
     if (threadIdx.x == 0 && (blockIdx.x & 63) == 63) PROBE_MAX(15);
     code_pf_done(pf);
-#else
-    const uint32_t lane = threadIdx.x & 15;
-    const uint64_t grp = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    const uint64_t ngrp = ((uint64_t)gridDim.x * blockDim.x) >> 4;
-    for (uint64_t i = grp; i < n; i += ngrp) {
-        const uint64_t o0 = P.out_off[i], len = P.out_off[i + 1] - o0;
-        if (len == 0) continue;
-        uint64_t start, slen;  // 64-bit stream position and length (any file size)
-        rec_stream(P, i, start, slen);
-        const uint8_t* s0 = P.file + start;
-        const uint8_t* src = none ? s0 : s0 + snappy_literal_hdr(s0, slen, len);
-        uint8_t* dst = P.out + o0;
-        for (uint64_t k = 16 * lane; k < len; k += 256) {
-            const uint4 v = ldu16(src + k);
-            if (k + 16 <= len)
-                stu16(dst + k, v);
-            else
-                st_partial(dst + k, v, (uint32_t)(len - k));
-        }
-    }
-#endif
 }
 
 __device__ void finalize_info(const FrameParams& P) {
