@@ -938,45 +938,55 @@ __device__ uint64_t find_entry_lane(const FrameParams& P, uint64_t cs, uint64_t 
                                     const uint32_t* crct) {
     const uint8_t* f = P.file;
     const uint32_t m3 = magic3(ver);
-    // 64 + 4 bytes from q0 (16-B aligned: the 64 lie inside the padded file, q0 < len, pad 64; the next
-    // dword only when it starts inside the file); the next step's bytes are loaded before this step's
-    // candidates are tested, so the scan has two steps of loads in flight
-    auto fetch = [&](uint64_t q, uint4& a, uint4& b, uint4& c, uint4& d, uint32_t& t) __attribute__((always_inline)) {
-        a = *reinterpret_cast<const uint4*>(f + q);
-        b = *reinterpret_cast<const uint4*>(f + q + 16);
-        c = *reinterpret_cast<const uint4*>(f + q + 32);
-        d = *reinterpret_cast<const uint4*>(f + q + 48);
-        t = q + 64 < P.len ? *reinterpret_cast<const uint32_t*>(f + q + 64) : 0u;
+    // a whole 128-byte line per step (8 loads, the next dword too), the next line loaded before this one's candidates are
+    // tested: two steps in flight. Round 6: the entry search was a chain of dependent 64-byte steps, ~3.5 us each under
+    // the walk's load (probe build), C2-ref-random walk 0.129 -> 0.117 ms (profiles/r6/r6r_lane_walk_entry.txt). 16-byte
+    // loads at or past the file end read nothing (the device pad covers 64 bytes only).
+    auto fetch = [&](uint64_t q, uint4 (&v)[8], uint32_t& t) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            v[j] = q + 16 * j < P.len ? *reinterpret_cast<const uint4*>(f + q + 16 * j) : zero4();
+        t = q + 128 < P.len ? *reinterpret_cast<const uint32_t*>(f + q + 128) : 0u;
     };
-    uint64_t q0 = cs & ~15ull;
-    if (q0 >= ce) return kNone;
-    uint4 a, b, cc, d;
+    uint64_t q0 = cs & ~127ull;
+    uint4 a[8];
     uint32_t t;
-    fetch(q0, a, b, cc, d, t);
+    fetch(q0, a, t);
     for (;;) {
-        const uint64_t q1 = q0 + 64;
-        uint4 na = zero4(), nb = zero4(), nc = zero4(), nd = zero4();
+        const uint64_t q1 = q0 + 128;
+        uint4 na[8];
         uint32_t nt = 0;
-        if (q1 < ce) fetch(q1, na, nb, nc, nd, nt);
-        const uint32_t w0[5] = {a.x, a.y, a.z, a.w, b.x}, w1[5] = {b.x, b.y, b.z, b.w, cc.x};
-        const uint32_t w2[5] = {cc.x, cc.y, cc.z, cc.w, d.x}, w3[5] = {d.x, d.y, d.z, d.w, t};
-        uint64_t mm = (uint64_t)magic_mask(w0, q0, cs, ce, P.len, m3) |
-                      ((uint64_t)magic_mask(w1, q0 + 16, cs, ce, P.len, m3) << 16) |
-                      ((uint64_t)magic_mask(w2, q0 + 32, cs, ce, P.len, m3) << 32) |
-                      ((uint64_t)magic_mask(w3, q0 + 48, cs, ce, P.len, m3) << 48);
-        while (mm) {
-            const uint64_t p = q0 + (uint64_t)__builtin_ctzll(mm);
-            mm &= mm - 1;
-            Hdr h;
-            uint64_t nx, ol, pd, lf;
-            if (frame_record(f, P.len, p, ver, comp, h, nx, ol, pd, lf, crct) == RIO_OK) return p;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) na[j] = zero4();
+        if (q1 < ce) fetch(q1, na, nt);
+        // candidate bits of the line's 128 positions (static indices only: the blocks stay in registers)
+        uint64_t mlo = 0, mhi = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t nx = j < 7 ? a[j + 1].x : t;
+            const uint32_t d[5] = {a[j].x, a[j].y, a[j].z, a[j].w, nx};
+            const uint64_t m = (uint64_t)magic_mask(d, q0 + 16 * j, cs, ce, P.len, m3) << (16 * (j & 3));
+            if (j < 4)
+                mlo |= m;
+            else
+                mhi |= m;
+        }
+        while (mlo | mhi) {
+            const bool lo = mlo != 0;
+            const uint64_t mm = lo ? mlo : mhi;
+            const uint64_t p = q0 + (lo ? 0u : 64u) + (uint64_t)__builtin_ctzll(mm);
+            if (lo)
+                mlo &= mlo - 1;
+            else
+                mhi &= mhi - 1;
+            Hdr hd;
+            uint64_t nxp, ol, pd, lf;
+            if (frame_record(f, P.len, p, ver, comp, hd, nxp, ol, pd, lf, crct) == RIO_OK) return p;
         }
         if (q1 >= ce) return kNone;
         q0 = q1;
-        a = na;
-        b = nb;
-        cc = nc;
-        d = nd;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) a[j] = na[j];
         t = nt;
     }
 }
@@ -1037,18 +1047,38 @@ __device__ void walk_from_lane(const FrameParams& P, uint64_t c, uint64_t p, uin
 }
 
 constexpr uint32_t kWalkLaneBlock = 256;
+#if RIO_SCAN_PROBE
+__device__ unsigned long long g_lane[1 << 18][4];
+#endif
 __global__ void __launch_bounds__(kWalkLaneBlock) k_walk_lane(FrameParams P) {
     __shared__ uint32_t crct[1024];
+#if RIO_SCAN_PROBE
+    const unsigned long long ta = wall_clock64();
+#endif
     if (blockIdx.x == 0 && threadIdx.x == 0) init_state(P);
     crc32c_tab_init(crct);
     const uint64_t c = (uint64_t)blockIdx.x * kWalkLaneBlock + threadIdx.x;
     uint32_t ver, comp;
     if (c >= P.n_chunks || file_header_status(P, ver, comp) != RIO_OK) return;
     const uint64_t cs = chunk_start(P, c), ce = chunk_end(P, c);
+#if RIO_SCAN_PROBE
+    const unsigned long long tb = wall_clock64();
+#endif
     const uint64_t from = c == 0 ? (uint64_t)RIO_FILE_HEADER_BYTES : find_entry_lane(P, cs, ce, ver, comp, crct);
+#if RIO_SCAN_PROBE
+    const unsigned long long tc = wall_clock64();
+#endif
     ChunkSum s = chunk_sum_empty(from);
     if (from != kNone) walk_from_lane(P, c, from, ver, comp, s, crct);
     P.chunks[c] = s;
+#if RIO_SCAN_PROBE
+    if (c < (1u << 18)) {
+        g_lane[c][0] = ta;
+        g_lane[c][1] = tb;
+        g_lane[c][2] = tc;
+        g_lane[c][3] = ((unsigned long long)s.count << 40) | (wall_clock64() & 0xFFFFFFFFFFull);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1709,7 +1739,25 @@ __device__ __forceinline__ void finish_file(const FrameParams& P) {
 
 #if RIO_SCAN_PROBE
 // the stamps of the decode that just ran, in us from the walk's first wave; then reset for the next one
-__global__ void k_probe_dump() {
+__global__ void k_probe_dump(uint64_t n_lane) {
+    if (n_lane) {  // the lane walk's per-lane stamps (us): start skew, table + header, entry search, hops, records per lane
+        const uint64_t m = n_lane < (1u << 18) ? n_lane : (1u << 18);
+        unsigned long long t0 = ~0ull, tend = 0;
+        double sk = 0, s1 = 0, s2 = 0, s3 = 0, cnt = 0, skmax = 0, s2max = 0, s3max = 0;
+        for (uint64_t c = 0; c < m; c++) t0 = g_lane[c][0] < t0 ? g_lane[c][0] : t0;
+        for (uint64_t c = 0; c < m; c++) {
+            const unsigned long long a = g_lane[c][0], b = g_lane[c][1], d = g_lane[c][2];
+            const unsigned long long e = (d & ~0xFFFFFFFFFFull) | (g_lane[c][3] & 0xFFFFFFFFFFull);
+            const unsigned long long e2 = e < d ? e + (1ull << 40) : e;
+            const double k = (double)(a - t0), x = (double)(b - a), y = (double)(d - b), z = (double)(e2 - d);
+            sk += k; s1 += x; s2 += y; s3 += z; cnt += (double)(g_lane[c][3] >> 40);
+            skmax = k > skmax ? k : skmax; s2max = y > s2max ? y : s2max; s3max = z > s3max ? z : s3max;
+            tend = e2 > tend ? e2 : tend;
+        }
+        printf("LANE n %llu span %.2f | start skew mean %.2f max %.2f | table+hdr %.2f | entry mean %.2f max %.2f | hops mean %.2f "
+               "max %.2f | records/lane %.2f\n", (unsigned long long)m, (double)(tend - t0) * 0.01, sk / m * 0.01,
+               skmax * 0.01, s1 / m * 0.01, s2 / m * 0.01, s2max * 0.01, s3 / m * 0.01, s3max * 0.01, cnt / m);
+    }
     const unsigned long long t0 = g_probe[0];
     auto us = [&](int i) { return g_probe[i] >= t0 && g_probe[i] != ~0ull ? (double)(g_probe[i] - t0) * 0.01 : -1.0; };
     printf("PROBE walk_end %.2f scan_first %.2f scan_lastin %.2f | last blk in %.2f ld %.2f hs %.2f st %.2f fence %.2f "
@@ -2390,7 +2438,7 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev, h
     launch_decoders(P, s, true);
     launch_ev(k_finish, dim3(64), dim3(256), s, ev ? ev[4] : nullptr, done, P);
 #if RIO_SCAN_PROBE
-    hipLaunchKernelGGL(k_probe_dump, dim3(1), dim3(1), 0, s);
+    hipLaunchKernelGGL(k_probe_dump, dim3(1), dim3(1), 0, s, P.walk_lane ? P.n_chunks : (uint64_t)0);
 #endif
     return hipGetLastError();
 }
