@@ -760,6 +760,10 @@ constexpr uint64_t kCopySmall = RIO_COPY_SMALL;
 #ifndef RIO_WALK_OCC
 #define RIO_WALK_OCC 5
 #endif
+#if RIO_SCAN_PROBE
+// per wave of k_walk: start, end, and the time in fill / frame / the rest, windows and fill rounds (probe build)
+__device__ unsigned long long g_wave[1 << 18][6];
+#endif
 #if RIO_WALK_OCC
 __global__ void __launch_bounds__(64 * kWalkWaves, RIO_WALK_OCC) k_walk(FrameParams P) {
 #else
@@ -786,11 +790,19 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
     uint32_t mode = (c == 0) ? 1u : 0u;  // 0 entry search, 1 chaining, 2 serial takeover at p
     uint64_t count = 0, bytes = 0, entry = p;
     uint64_t ws = cs;  // window start: candidates are positions >= ws
+#if RIO_SCAN_PROBE
+    const unsigned long long tw0 = wall_clock64();
+    unsigned long long tfill = 0, tframe = 0, nwin = 0, nround = 0, tq = 0;
+#endif
     while (ws < ce && mode < 2) {
         if (mode == 1) {
             if (p >= ce) break;
             ws = umax(ws, p);  // skip what the chain jumped over
         }
+#if RIO_SCAN_PROBE
+        tq = wall_clock64();
+        nwin++;
+#endif
         // 1. fill the window [ws, we)
         if (lane == 0) L.overflow = kNone;
         uint32_t total = 0;
@@ -848,8 +860,18 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
                 }
             }
             rd += 4096;
+#if RIO_SCAN_PROBE
+            nround++;
+#endif
         }
         wave_sync_lds();
+#if RIO_SCAN_PROBE
+        {
+            const unsigned long long t = wall_clock64();
+            tfill += t - tq;
+            tq = t;
+        }
+#endif
         const uint64_t overflow = L.overflow;
         const uint64_t we = overflow != kNone ? overflow : umin(rd, ce);  // window end
         // 2. frame one candidate per lane
@@ -863,6 +885,13 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
         if (have) e = frame_record(f, P.len, cpos, ver, comp, h, nx, ol, pd, lf, crct);
         const bool ok = have && e == RIO_OK;
         const uint64_t ok_mask = __ballot(ok);
+#if RIO_SCAN_PROBE
+        {
+            const unsigned long long t = wall_clock64();
+            tframe += t - tq;
+            tq = t;
+        }
+#endif
         const uint64_t succ_pos = __shfl_down(cpos, 1);  // next candidate's position
         // 3. entry and chain by votes
         if (mode == 0) {
@@ -917,6 +946,17 @@ __global__ void __launch_bounds__(64 * kWalkWaves) k_walk(FrameParams P) {
             s.exit = p;  // the chain left the chunk (or ended at the file end) cleanly
         P.chunks[c] = s;
         PROBE_MAX(1);
+#if RIO_SCAN_PROBE
+        if (c < (1u << 18)) {
+            const unsigned long long te = wall_clock64();
+            g_wave[c][0] = tw0;
+            g_wave[c][1] = te;
+            g_wave[c][2] = tfill;
+            g_wave[c][3] = tframe;
+            g_wave[c][4] = nwin;
+            g_wave[c][5] = nround;
+        }
+#endif
     }
     code_pf_done(pf);
 }
@@ -1739,7 +1779,27 @@ __device__ __forceinline__ void finish_file(const FrameParams& P) {
 
 #if RIO_SCAN_PROBE
 // the stamps of the decode that just ran, in us from the walk's first wave; then reset for the next one
-__global__ void k_probe_dump(uint64_t n_lane) {
+__global__ void k_probe_dump(uint64_t n_lane, uint64_t n_wave) {
+    if (n_wave) {  // the wave walk's per-wave phases (us): span, fill, frame, rest; windows and fill rounds per wave
+        const uint64_t m = n_wave < (1u << 18) ? n_wave : (1u << 18);
+        unsigned long long t0 = ~0ull, tend = 0;
+        double dur = 0, fl = 0, fr = 0, nw = 0, nr = 0, durmax = 0, sk = 0;
+        for (uint64_t c = 0; c < m; c++) t0 = g_wave[c][0] < t0 ? g_wave[c][0] : t0;
+        for (uint64_t c = 0; c < m; c++) {
+            const double d = (double)(g_wave[c][1] - g_wave[c][0]);
+            dur += d;
+            durmax = d > durmax ? d : durmax;
+            sk += (double)(g_wave[c][0] - t0);
+            fl += (double)g_wave[c][2];
+            fr += (double)g_wave[c][3];
+            nw += (double)g_wave[c][4];
+            nr += (double)g_wave[c][5];
+            tend = g_wave[c][1] > tend ? g_wave[c][1] : tend;
+        }
+        printf("WAVE n %llu span %.2f | start mean %.2f | wave mean %.2f max %.2f | fill %.2f frame %.2f rest %.2f | "
+               "windows %.2f rounds %.2f\n", (unsigned long long)m, (double)(tend - t0) * 0.01, sk / m * 0.01,
+               dur / m * 0.01, durmax * 0.01, fl / m * 0.01, fr / m * 0.01, (dur - fl - fr) / m * 0.01, nw / m, nr / m);
+    }
     if (n_lane) {  // the lane walk's per-lane stamps (us): start skew, table + header, entry search, hops, records per lane
         const uint64_t m = n_lane < (1u << 18) ? n_lane : (1u << 18);
         unsigned long long t0 = ~0ull, tend = 0;
@@ -2438,7 +2498,8 @@ hipError_t launch_phase_b(const FrameParams& P, hipStream_t s, hipEvent_t* ev, h
     launch_decoders(P, s, true);
     launch_ev(k_finish, dim3(64), dim3(256), s, ev ? ev[4] : nullptr, done, P);
 #if RIO_SCAN_PROBE
-    hipLaunchKernelGGL(k_probe_dump, dim3(1), dim3(1), 0, s, P.walk_lane ? P.n_chunks : (uint64_t)0);
+    hipLaunchKernelGGL(k_probe_dump, dim3(1), dim3(1), 0, s, P.walk_lane ? P.n_chunks : (uint64_t)0,
+                       P.walk_lane ? (uint64_t)0 : P.n_chunks);
 #endif
     return hipGetLastError();
 }
